@@ -1,0 +1,300 @@
+// CPU restatement of RTen's Conv and pooling operators (test infrastructure;
+// see rten_oracle.h).
+//
+// Follows src/ops/conv.rs:24-280 (dispatcher, pointwise, im2col path),
+// src/ops/conv/im2col.rs:75-260 (VirtualIm2Col), src/ops/conv/depthwise.rs:24-203
+// and src/ops/pooling.rs:27-375.
+#include <omp.h>
+
+#include <algorithm>
+#include <limits>
+
+#include "common.h"
+
+namespace orc {
+
+// VirtualIm2Col (im2col.rs:44-181): row r = (c, ky, kx), col = (oy, ox).
+struct Im2Col : VirtualB {
+  const float* img;  // [C,H,W] contiguous
+  int64_t C, H, W, kh, kw, sh, sw, dh, dw, pt, pl, oh, ow;
+  int64_t rows() const override { return C * kh * kw; }
+  int64_t cols() const override { return oh * ow; }
+  void pack_b(float* out, int64_t nr, int64_t k0, int64_t k1, int64_t c0,
+              int64_t c1) const override {
+    int64_t c1p = c0 + (c1 - c0 + nr - 1) / nr * nr;
+    int64_t n_rows = k1 - k0;
+    for (int64_t pc = c0; pc < c1p; pc += nr) {
+      float* po = out + (pc - c0) / nr * n_rows * nr;
+      int64_t iy0[64], ix0[64];
+      for (int64_t j = 0; j < nr; j++) {
+        int64_t col = pc + j;
+        int64_t py = col / ow, px = col % ow;
+        iy0[j] = py * sh - pt;
+        ix0[j] = px * sw - pl;
+      }
+      for (int64_t r = k0; r < k1; r++) {
+        int64_t c = r / (kh * kw), ky = (r / kw) % kh, kx = r % kw;
+        const float* chan = img + c * H * W;
+        float* o = po + (r - k0) * nr;
+        for (int64_t j = 0; j < nr; j++) {
+          int64_t y = iy0[j] + ky * dh, x = ix0[j] + kx * dw;
+          o[j] = (y >= 0 && y < H && x >= 0 && x < W) ? chan[y * W + x] : 0.f;
+        }
+      }
+    }
+  }
+};
+
+// calc_output_size_and_padding (pooling.rs:27-89).
+static int output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h, int64_t k_w,
+                                   int64_t stride_h, int64_t stride_w, int pad_mode,
+                                   const int64_t* pads_in, int64_t dil_y, int64_t dil_x,
+                                   int64_t out_hw[2], int64_t pads[4]) {
+  if (dil_y == 0 || dil_x == 0) return fail(ORC_INVALID_VALUE, "Dilations must be > 0");
+  if (stride_h == 0 || stride_w == 0) return fail(ORC_INVALID_VALUE, "Strides must be > 0");
+  if (pad_mode == 1) {
+    int64_t out_h = (in_h + stride_h - 1) / stride_h, out_w = (in_w + stride_w - 1) / stride_w;
+    int64_t th = std::max<int64_t>(0, (out_h - 1) * stride_h + (k_h - 1) * dil_y + 1 - in_h);
+    int64_t tw = std::max<int64_t>(0, (out_w - 1) * stride_w + (k_w - 1) * dil_x + 1 - in_w);
+    pads[0] = th / 2;
+    pads[1] = tw / 2;
+    pads[2] = (th + 1) / 2;
+    pads[3] = (tw + 1) / 2;
+    out_hw[0] = out_h;
+    out_hw[1] = out_w;
+    return ORC_OK;
+  }
+  for (int i = 0; i < 4; i++) pads[i] = pads_in[i];
+  int64_t ph = in_h + pads[0] + pads[2], pw = in_w + pads[1] + pads[3];
+  int64_t dkh = k_h + (k_h - 1) * (dil_y - 1), dkw = k_w + (k_w - 1) * (dil_x - 1);
+  if (ph < dkh || pw < dkw) return fail(ORC_INVALID_VALUE, "Input too small for kernel size");
+  out_hw[0] = (ph - dil_y * (k_h - 1) - 1) / stride_h + 1;
+  out_hw[1] = (pw - dil_x * (k_w - 1) - 1) / stride_w + 1;
+  return ORC_OK;
+}
+
+// conv_2d_depthwise (depthwise.rs:127-203) + conv_2d_depthwise_block (49-120).
+// Per output row: init with bias, then for each (ky, kx) in order
+// out += in * w with separate mul/add roundings.
+static void conv_depthwise(const float* x, int64_t N, int64_t C, int64_t H, int64_t W,
+                           const float* w, int64_t kh, int64_t kw, const float* bias,
+                           const int64_t pads[4], int64_t sh, int64_t sw, int64_t dh, int64_t dw,
+                           int64_t oh, int64_t ow, float* y) {
+  int64_t pt = pads[0], pl = pads[1];
+  std::vector<int64_t> omin(kw), omax(kw), imin(kw);
+  for (int64_t kx = 0; kx < kw; kx++) {
+    // min_max_out_x_coords (depthwise.rs:24-38)
+    int64_t mn = std::max<int64_t>(0, pl - kx * dw);
+    int64_t t = std::max<int64_t>(0, W + pl - kx * dw);
+    int64_t mx = std::min<int64_t>((t + sw - 1) / sw, ow);
+    omin[kx] = mn;
+    omax[kx] = mx;
+    imin[kx] = mn * sw + kx * dw - pl;
+  }
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
+  for (int64_t n = 0; n < N; n++)
+    for (int64_t c = 0; c < C; c++) {
+      const float* in = x + (n * C + c) * H * W;
+      float* out = y + (n * C + c) * oh * ow;
+      const float* kern = w + c * kh * kw;
+      float init = bias ? bias[c] : 0.f;
+      for (int64_t oy = 0; oy < oh; oy++) {
+        float* orow = out + oy * ow;
+        for (int64_t ox = 0; ox < ow; ox++) orow[ox] = init;
+        for (int64_t ky = 0; ky < kh; ky++) {
+          int64_t iy = oy * sh + ky * dh;
+          if (iy < pt || iy >= H + pt) continue;
+          const float* irow = in + (iy - pt) * W;
+          for (int64_t kx = 0; kx < kw; kx++) {
+            float s = kern[ky * kw + kx];
+            const float* src = irow + imin[kx];
+            for (int64_t ox = omin[kx]; ox < omax[kx]; ox++) {
+              float prod = src[(ox - omin[kx]) * sw] * s;
+              orow[ox] = orow[ox] + prod;
+            }
+          }
+        }
+      }
+    }
+}
+
+static int conv2d(const float* x, const int64_t xs[4], const float* w, const int64_t ws[4],
+                  const float* bias, int pad_mode, const int64_t* pads_in,
+                  const int64_t strides[2], const int64_t dil[2], int64_t groups, float* y,
+                  int64_t ys[4]) {
+  int64_t N = xs[0], C = xs[1], H = xs[2], W = xs[3];
+  int64_t O = ws[0], KC = ws[1], kh = ws[2], kw = ws[3];
+  int64_t out_hw[2], pads[4];
+  int st = output_size_and_padding(H, W, kh, kw, strides[0], strides[1], pad_mode, pads_in,
+                                   dil[0], dil[1], out_hw, pads);
+  if (st) return st;
+  int64_t oh = out_hw[0], ow = out_hw[1];
+  ys[0] = N;
+  ys[1] = O;
+  ys[2] = oh;
+  ys[3] = ow;
+  bool has_pad = pads[0] > 0 || pads[1] > 0 || pads[2] > 0 || pads[3] > 0;
+  if (kh == 1 && kw == 1 && !has_pad && groups == 1 && strides[0] == 1 && strides[1] == 1 &&
+      dil[0] == 1 && dil[1] == 1) {
+    // conv_2d_pointwise (conv.rs:24-68): serial loop over images, one GEMM
+    // each (which parallelizes internally).
+    Mat A{w, O, C, C, 1};
+    for (int64_t n = 0; n < N; n++) {
+      Mat B{x + n * C * H * W, C, H * W, H * W, 1};
+      gemm_impl(y + n * O * H * W, H * W, A, &B, nullptr, 1.f, 0.f, bias, false);
+    }
+    return ORC_OK;
+  }
+  int64_t opg = O / std::max<int64_t>(groups, 1), ipg = C / std::max<int64_t>(groups, 1);
+  if (groups == 0 || ipg != KC)
+    return fail(ORC_INCOMPATIBLE_INPUT_SHAPES,
+                "Input channels (per group) does not match kernel input channels");
+  if (C % groups != 0 || O % groups != 0)
+    return fail(ORC_INCOMPATIBLE_INPUT_SHAPES,
+                "Input channels and output channels must be divisible by group count");
+  if (C == O && groups == C) {
+    conv_depthwise(x, N, C, H, W, w, kh, kw, bias, pads, strides[0], strides[1], dil[0], dil[1],
+                   oh, ow, y);
+    return ORC_OK;
+  }
+  int64_t P = oh * ow;
+  for (int64_t g = 0; g < groups; g++) {
+    Mat A{w + g * opg * KC * kh * kw, opg, KC * kh * kw, KC * kh * kw, 1};
+    const float* gb = bias ? bias + g * opg : nullptr;
+    // Per-image parallelism (conv.rs:243-270, par_bridge).  Each image's
+    // GEMM then runs on its worker; summation order is unaffected.
+    bool par_images = N > 1;
+#pragma omp parallel for schedule(dynamic, 1) if (par_images)
+    for (int64_t n = 0; n < N; n++) {
+      Im2Col im;
+      im.img = x + (n * C + g * ipg) * H * W;
+      im.C = ipg;
+      im.H = H;
+      im.W = W;
+      im.kh = kh;
+      im.kw = kw;
+      im.sh = strides[0];
+      im.sw = strides[1];
+      im.dh = dil[0];
+      im.dw = dil[1];
+      im.pt = pads[0];
+      im.pl = pads[1];
+      im.oh = oh;
+      im.ow = ow;
+      gemm_impl(y + (n * O + g * opg) * P, P, A, nullptr, &im, 1.f, 0.f, gb, par_images);
+    }
+  }
+  return ORC_OK;
+}
+
+// pool_impl (pooling.rs:104-238).  fold over the window in (ky, kx) order.
+template <typename Fold, typename Avg>
+static int pool_impl(const float* x, const int64_t xs[4], const int64_t kernel[2],
+                     const int64_t strides[2], int pad_mode, const int64_t* pads_in, float init,
+                     Fold fold, Avg avg, float* y, int64_t ys[4]) {
+  int64_t N = xs[0], C = xs[1], H = xs[2], W = xs[3];
+  int64_t out_hw[2], pads[4];
+  int st = output_size_and_padding(H, W, kernel[0], kernel[1], strides[0], strides[1], pad_mode,
+                                   pads_in, 1, 1, out_hw, pads);
+  if (st) return st;
+  int64_t oh = out_hw[0], ow = out_hw[1], pt = pads[0], pl = pads[1];
+  ys[0] = N;
+  ys[1] = C;
+  ys[2] = oh;
+  ys[3] = ow;
+#pragma omp parallel for collapse(2)
+  for (int64_t n = 0; n < N; n++)
+    for (int64_t c = 0; c < C; c++) {
+      const float* in = x + (n * C + c) * H * W;
+      float* out = y + (n * C + c) * oh * ow;
+      for (int64_t oy = 0; oy < oh; oy++)
+        for (int64_t ox = 0; ox < ow; ox++) {
+          float acc = init;
+          int64_t cnt = 0;
+          for (int64_t ky = 0; ky < kernel[0]; ky++)
+            for (int64_t kx = 0; kx < kernel[1]; kx++) {
+              int64_t iy = oy * strides[0] + ky, ix = ox * strides[1] + kx;
+              if (iy >= pt && iy < H + pt && ix >= pl && ix < W + pl) {
+                acc = fold(acc, in[(iy - pt) * W + (ix - pl)]);
+                cnt++;
+              }
+            }
+          out[oy * ow + ox] = avg(acc, cnt);
+        }
+    }
+  return ORC_OK;
+}
+
+}  // namespace orc
+
+using namespace orc;
+
+extern "C" {
+
+int orc_output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h, int64_t k_w,
+                                int64_t stride_h, int64_t stride_w, int pad_mode,
+                                const int64_t pads_in[4], int64_t dil_h, int64_t dil_w,
+                                int64_t out_hw[2], int64_t pads_out[4]) {
+  return output_size_and_padding(in_h, in_w, k_h, k_w, stride_h, stride_w, pad_mode, pads_in,
+                                 dil_h, dil_w, out_hw, pads_out);
+}
+
+int orc_conv(const float* x, const int64_t* x_shape, int x_ndim, const float* w,
+             const int64_t* w_shape, const float* bias, int pad_mode, const int64_t* pads,
+             const int64_t* strides, const int64_t* dilations, int64_t groups, float* out,
+             int64_t* out_shape) {
+  if (x_ndim == 3) {
+    // 1-D conv via 2-D (conv.rs:96-143).
+    int64_t xs[4] = {x_shape[0], x_shape[1], 1, x_shape[2]};
+    int64_t ws[4] = {w_shape[0], w_shape[1], 1, w_shape[2]};
+    int64_t p2[4] = {0, pads ? pads[0] : 0, 0, pads ? pads[1] : 0};
+    int64_t s2[2] = {1, strides[0]}, d2[2] = {1, dilations[0]};
+    int64_t ys[4];
+    int st = conv2d(x, xs, w, ws, bias, pad_mode, p2, s2, d2, groups, out, ys);
+    if (st) return st;
+    out_shape[0] = ys[0];
+    out_shape[1] = ys[1];
+    out_shape[2] = ys[3];
+    return ORC_OK;
+  }
+  if (x_ndim != 4) return fail(ORC_INVALID_VALUE, "Input must have 4 dims (NCHW)");
+  return conv2d(x, x_shape, w, w_shape, bias, pad_mode, pads, strides, dilations, groups, out,
+                out_shape);
+}
+
+int orc_max_pool(const float* x, const int64_t x_shape[4], const int64_t kernel[2],
+                 const int64_t strides[2], int pad_mode, const int64_t pads[4], float* out,
+                 int64_t out_shape[4]) {
+  // f32::max ignores NaN operands (returns the other one).
+  return pool_impl(
+      x, x_shape, kernel, strides, pad_mode, pads, -std::numeric_limits<float>::infinity(),
+      [](float a, float b) { return std::fmax(a, b); }, [](float a, int64_t) { return a; }, out,
+      out_shape);
+}
+
+int orc_average_pool(const float* x, const int64_t x_shape[4], const int64_t kernel[2],
+                     const int64_t strides[2], int pad_mode, const int64_t pads[4],
+                     int count_include_pad, float* out, int64_t out_shape[4]) {
+  float klen = (float)(kernel[0] * kernel[1]);
+  return pool_impl(
+      x, x_shape, kernel, strides, pad_mode, pads, 0.f, [](float a, float b) { return a + b; },
+      [=](float a, int64_t cnt) { return count_include_pad ? a / klen : a / (float)cnt; }, out,
+      out_shape);
+}
+
+int orc_global_average_pool(const float* x, const int64_t x_shape[4], float* out) {
+  // global_average_pool (pooling.rs:294-342): row-major sum per channel.
+  int64_t N = x_shape[0], C = x_shape[1], HW = x_shape[2] * x_shape[3];
+  float denom = (float)HW;
+#pragma omp parallel for collapse(2)
+  for (int64_t n = 0; n < N; n++)
+    for (int64_t c = 0; c < C; c++) {
+      const float* p = x + (n * C + c) * HW;
+      float s = 0.f;
+      for (int64_t i = 0; i < HW; i++) s += p[i];
+      out[n * C + c] = s / denom;
+    }
+  return ORC_OK;
+}
+
+}  // extern "C"
