@@ -1,0 +1,223 @@
+/*
+ * rten_hip.h — C ABI of the MI355X (gfx950) operator backend for RTen.
+ *
+ * This is the drop-in boundary: each entry point replaces the CPU body of one
+ * RTen `Operator::run` / `run_in_place` (src/ops/mod.rs:821-913) on the f32 hot
+ * path, and the graph entry points replace `Model::run` -> `Graph::run`
+ * (src/model.rs:580-592, src/graph.rs:733-1073).  A Rust `impl Operator`
+ * registered through `OpRegistry::register_op` (src/op_registry.rs:44-49)
+ * binds these with `extern "C"`.
+ *
+ * Conventions
+ *  - Plain C types only.  All float pointers are DEVICE pointers (HBM) unless a
+ *    function says "host".  The caller owns every buffer.
+ *  - Tensors are described by rtenhip_tensor: shape + ELEMENT strides, like
+ *    rten-tensor's DynLayout (rten-tensor/src/layout.rs:518-525).
+ *  - Every op returns rtenhip_status; codes 1..6 are RTen's OpError variants
+ *    (src/ops/mod.rs:666-686) and rtenhip_last_error_message() returns the same
+ *    message string the reference returns.  7 = HIP runtime error.
+ *  - Work is enqueued on the context's stream (rtenhip_set_stream); calls are
+ *    asynchronous and never allocate or synchronize unless stated, so they can
+ *    be captured in a hipGraph.
+ *  - In-place (y == x) is allowed exactly where the reference's op has
+ *    run_in_place (unary ops, Add/Mul/Sub/Div on the larger operand,
+ *    BatchNormalization, Softmax).
+ */
+#ifndef RTEN_HIP_H
+#define RTEN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  RTENHIP_OK = 0,
+  RTENHIP_INCORRECT_INPUT_TYPE = 1,      /* OpError::IncorrectInputType */
+  RTENHIP_INCORRECT_OUTPUT_TYPE = 2,     /* OpError::IncorrectOutputType */
+  RTENHIP_INCOMPATIBLE_INPUT_SHAPES = 3, /* OpError::IncompatibleInputShapes */
+  RTENHIP_MISSING_INPUTS = 4,            /* OpError::MissingInputs */
+  RTENHIP_INVALID_VALUE = 5,             /* OpError::InvalidValue */
+  RTENHIP_UNSUPPORTED_VALUE = 6,         /* OpError::UnsupportedValue */
+  RTENHIP_HIP_ERROR = 7,
+} rtenhip_status;
+
+#define RTENHIP_MAX_DIMS 8
+
+typedef struct {
+  float* data;                       /* device pointer */
+  int32_t ndim;
+  int64_t shape[RTENHIP_MAX_DIMS];
+  int64_t strides[RTENHIP_MAX_DIMS]; /* element strides */
+} rtenhip_tensor;
+
+/* Fused epilogue applied after bias (and residual) by GEMM / Conv. */
+typedef enum {
+  RTENHIP_ACT_NONE = 0,
+  RTENHIP_ACT_RELU = 1, /* Relu: f32::max(x, 0) (unary_elementwise.rs:571) */
+  RTENHIP_ACT_CLIP = 2, /* Clip: f32::clamp(x, lo, hi) (unary_elementwise.rs:314-323) */
+} rtenhip_act;
+
+typedef struct rtenhip_ctx rtenhip_ctx;
+
+/* ---- context ----------------------------------------------------------- */
+rtenhip_ctx* rtenhip_create(int device);
+void rtenhip_destroy(rtenhip_ctx* ctx);
+/* Stream used by all subsequent calls on ctx (a hipStream_t; NULL = default). */
+rtenhip_status rtenhip_set_stream(rtenhip_ctx* ctx, void* stream);
+void* rtenhip_get_stream(rtenhip_ctx* ctx);
+const char* rtenhip_last_error_message(void);
+/* Blocks until the context's stream is idle. */
+rtenhip_status rtenhip_synchronize(rtenhip_ctx* ctx);
+/* Device memory helpers (hipMalloc / hipFree / hipMemcpy H2D, D2H, D2D). */
+void* rtenhip_malloc(rtenhip_ctx* ctx, size_t bytes);
+void rtenhip_free(rtenhip_ctx* ctx, void* ptr);
+rtenhip_status rtenhip_memcpy_h2d(rtenhip_ctx* ctx, void* dst, const void* src, size_t bytes);
+rtenhip_status rtenhip_memcpy_d2h(rtenhip_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Kernel library identification: "gfx950" build tag + version. */
+const char* rtenhip_build_info(void);
+
+/* ---- shape helpers ------------------------------------------------------ */
+/* calc_output_size_and_padding (src/ops/pooling.rs:27-89).  pad_mode 0 = Fixed
+ * pads [top, left, bottom, right], 1 = Same (SAME_UPPER). */
+rtenhip_status rtenhip_output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h,
+                                               int64_t k_w, int64_t stride_h, int64_t stride_w,
+                                               int pad_mode, const int64_t pads_in[4],
+                                               int64_t dil_h, int64_t dil_w, int64_t out_hw[2],
+                                               int64_t pads_out[4]);
+
+/* ---- GEMM engine -------------------------------------------------------- */
+/* GemmExecutor::gemm_bias (src/gemm.rs:465-542, gemm_impl 733-930):
+ *   out[M,N] = alpha * A[M,K] @ B[K,N] + beta * out  (+ bias[m])
+ * A[m,k] at a[m*a_rs + k*a_cs], B[k,n] at b[k*b_rs + n*b_cs], out row stride
+ * out_rs.  beta == 0: out is not read.  K is summed in KC=256 blocks exactly as
+ * the reference does, so results are bit-identical to RTen's CPU path for
+ * alpha == 1 (and any alpha on full 6x16 tiles).  M == 1 with unpacked
+ * inputs takes the reference's gemv path (gemm.rs:651-704) and order. */
+rtenhip_status rtenhip_gemm_f32(rtenhip_ctx* ctx, int64_t m, int64_t n, int64_t k,
+                                const float* a, int64_t a_rs, int64_t a_cs, const float* b,
+                                int64_t b_rs, int64_t b_cs, float* out, int64_t out_rs,
+                                float alpha, float beta, const float* bias);
+
+/* ---- operators (Operator::run bodies) ----------------------------------- */
+/* Conv (src/ops/conv.rs:86-280).  x NCHW or NCW, w OIHW/OIW, bias [O] or NULL.
+ * residual (same shape as y) or NULL is added after the bias, then `act`
+ * (fusion of the following Add / Relu / Clip nodes; pass NULL/NONE for the
+ * plain operator).  y must be preallocated with the output shape
+ * (rtenhip_conv_output_shape). */
+rtenhip_status rtenhip_conv_output_shape(const rtenhip_tensor* x, const rtenhip_tensor* w,
+                                         int pad_mode, const int64_t* pads,
+                                         const int64_t* strides, const int64_t* dilations,
+                                         int64_t groups, int64_t* out_shape, int32_t* out_ndim);
+rtenhip_status rtenhip_conv_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                const rtenhip_tensor* w, const float* bias, int pad_mode,
+                                const int64_t* pads, const int64_t* strides,
+                                const int64_t* dilations, int64_t groups, const float* residual,
+                                int act, float act_lo, float act_hi, rtenhip_tensor* y);
+
+/* ONNX Gemm (src/ops/matmul.rs:27-81): y = alpha*op(a)@op(b) + beta*c, c
+ * broadcast to [M,N] (c may be NULL). */
+rtenhip_status rtenhip_gemm_op_f32(rtenhip_ctx* ctx, const rtenhip_tensor* a,
+                                   const rtenhip_tensor* b, const rtenhip_tensor* c, float alpha,
+                                   float beta, int trans_a, int trans_b, rtenhip_tensor* y);
+
+/* MatMul (src/ops/matmul.rs:123-239): batched + broadcast. */
+rtenhip_status rtenhip_matmul_f32(rtenhip_ctx* ctx, const rtenhip_tensor* a,
+                                  const rtenhip_tensor* b, rtenhip_tensor* y);
+
+/* MaxPool / AveragePool (src/ops/pooling.rs:104-375), NCHW. */
+rtenhip_status rtenhip_max_pool_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                    const int64_t kernel[2], const int64_t strides[2],
+                                    int pad_mode, const int64_t pads[4], rtenhip_tensor* y);
+rtenhip_status rtenhip_average_pool_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                        const int64_t kernel[2], const int64_t strides[2],
+                                        int pad_mode, const int64_t pads[4],
+                                        int count_include_pad, rtenhip_tensor* y);
+/* GlobalAveragePool (src/ops/pooling.rs:294-342). */
+rtenhip_status rtenhip_global_average_pool_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                               rtenhip_tensor* y);
+
+/* BatchNormalization (src/ops/norm.rs:18-128); y may alias x. */
+rtenhip_status rtenhip_batch_norm_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                      const float* scale, const float* bias, const float* mean,
+                                      const float* var, float epsilon, rtenhip_tensor* y);
+
+/* LayerNormalization (src/ops/norm.rs:245-299); bias may be NULL. */
+rtenhip_status rtenhip_layer_norm_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                      const rtenhip_tensor* scale, const rtenhip_tensor* bias,
+                                      int64_t axis, float epsilon, rtenhip_tensor* y);
+
+/* Softmax (src/ops/norm.rs:332-448 + rten-vecmath softmax.rs); y may alias x. */
+rtenhip_status rtenhip_softmax_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, int64_t axis,
+                                   rtenhip_tensor* y);
+
+/* Unary float ops (src/ops/unary_elementwise.rs; numerics of rten-vecmath). */
+typedef enum {
+  RTENHIP_UNARY_RELU = 0,
+  RTENHIP_UNARY_CLIP = 1, /* p0 = min, p1 = max */
+  RTENHIP_UNARY_GELU = 2,
+  RTENHIP_UNARY_ERF = 3,
+  RTENHIP_UNARY_SIGMOID = 4,
+  RTENHIP_UNARY_TANH = 5,
+  RTENHIP_UNARY_EXP = 6,
+  RTENHIP_UNARY_SILU = 7,
+} rtenhip_unary_op;
+rtenhip_status rtenhip_unary_f32(rtenhip_ctx* ctx, int op, const rtenhip_tensor* x, float p0,
+                                 float p1, rtenhip_tensor* y);
+
+/* Broadcasting binary ops (src/ops/binary_elementwise.rs:158-439). */
+typedef enum {
+  RTENHIP_BINARY_ADD = 0,
+  RTENHIP_BINARY_SUB = 1,
+  RTENHIP_BINARY_MUL = 2,
+  RTENHIP_BINARY_DIV = 3,
+} rtenhip_binary_op;
+rtenhip_status rtenhip_binary_f32(rtenhip_ctx* ctx, int op, const rtenhip_tensor* a,
+                                  const rtenhip_tensor* b, rtenhip_tensor* y);
+
+/* ---- graph executor (Graph::run, src/graph.rs:733-1073) ------------------ */
+typedef struct rtenhip_graph rtenhip_graph;
+
+rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx);
+void rtenhip_graph_destroy(rtenhip_graph* g);
+/* Node ids are returned (>= 0) or -1 on error. */
+int32_t rtenhip_graph_add_value(rtenhip_graph* g, const char* name);
+/* Constant f32 tensor from HOST data (uploaded once, like a .rten constant). */
+int32_t rtenhip_graph_add_constant(rtenhip_graph* g, const char* name, const float* host_data,
+                                   const int64_t* shape, int32_t ndim);
+/* Operator node.  op_type is the sg::OperatorType name (schema.fbs:12-121),
+ * attrs a "key=v1,v2;key=v" string (e.g. "pads=3,3,3,3;strides=2,2;groups=1").
+ * Input id -1 = absent optional input. */
+int32_t rtenhip_graph_add_op(rtenhip_graph* g, const char* name, const char* op_type,
+                             const char* attrs, const int32_t* inputs, int32_t n_inputs,
+                             const int32_t* outputs, int32_t n_outputs);
+/* Load-time optimisation: fuse Conv+Add+Relu/Clip epilogues and fold
+ * Flatten/Reshape (metadata).  Numerics are unchanged (bit-identical). */
+rtenhip_status rtenhip_graph_optimize(rtenhip_graph* g);
+/* Plan + run.  Inputs are device tensors; outputs are written into
+ * caller-provided device tensors whose shapes the executor checks.  The plan
+ * is cached per (inputs, outputs) like get_cached_plan (graph.rs:768-795). */
+rtenhip_status rtenhip_graph_run(rtenhip_graph* g, const int32_t* input_ids,
+                                 const rtenhip_tensor* inputs, int32_t n_inputs,
+                                 const int32_t* output_ids, rtenhip_tensor* outputs,
+                                 int32_t n_outputs);
+/* Output shape of a value after the last run (or -1). */
+int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape);
+/* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled. */
+rtenhip_status rtenhip_graph_set_timing(rtenhip_graph* g, int enabled);
+const char* rtenhip_graph_timing_report(rtenhip_graph* g);
+
+/* .rten V2 model loader (src/model.rs:265-522): parses the file bytes (host),
+ * uploads constants, builds the graph.  Returns NULL on error. */
+rtenhip_graph* rtenhip_model_load(rtenhip_ctx* ctx, const uint8_t* bytes, size_t len);
+int32_t rtenhip_model_input_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
+int32_t rtenhip_model_output_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
+int32_t rtenhip_graph_node_id(rtenhip_graph* g, const char* name);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTEN_HIP_H */

@@ -1,0 +1,454 @@
+// C ABI entry points (include/rten_hip.h): host-side validation and dispatch
+// for each operator, mirroring the reference's Operator::run bodies
+// (shape checks, error kinds and messages) and launching the HIP kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <thread>
+#include <tuple>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+
+namespace rtenhip {
+
+static thread_local std::string g_err;
+
+void set_error(int code, const std::string& msg) {
+  (void)code;
+  g_err = msg;
+}
+rtenhip_status fail(rtenhip_status code, const char* msg) {
+  set_error(code, msg);
+  return code;
+}
+rtenhip_status hip_fail(hipError_t e, const char* where) {
+  set_error(RTENHIP_HIP_ERROR, std::string("HIP error ") + hipGetErrorString(e) + " at " + where);
+  return RTENHIP_HIP_ERROR;
+}
+
+hipStream_t stream_of(rtenhip_ctx* ctx) { return reinterpret_cast<Ctx*>(ctx)->stream; }
+
+Ctx::Ctx(int dev) : device(dev) {
+  if (const char* s = getenv("RTEN_NUM_THREADS")) {
+    int v = atoi(s);
+    if (v > 0) ref_threads = v;
+  }
+  if (ref_threads <= 0) {
+    unsigned hc = std::thread::hardware_concurrency();
+    ref_threads = hc ? (int)hc : 1;
+  }
+}
+
+Ctx::~Ctx() {
+  for (auto& kv : ktabs) (void)hipFree(kv.second);
+  if (scratch) (void)hipFree(scratch);
+}
+
+float* Ctx::scratch_floats(size_t n, size_t slot) {
+  // Two independent grow-only regions carved from one allocation.
+  size_t need = n * sizeof(float);
+  if (slot >= 2) return nullptr;
+  if (need > scratch_cap[slot]) {
+    size_t total = 0;
+    size_t caps[2] = {scratch_cap[0], scratch_cap[1]};
+    caps[slot] = need + (need >> 2) + 256;
+    total = caps[0] + caps[1];
+    void* p = nullptr;
+    if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, total) != hipSuccess) return nullptr;
+    if (scratch) (void)hipFree(scratch);
+    scratch = p;
+    scratch_cap[0] = caps[0];
+    scratch_cap[1] = caps[1];
+  }
+  char* base = static_cast<char*>(scratch);
+  return reinterpret_cast<float*>(slot == 0 ? base : base + scratch_cap[0]);
+}
+
+const int2* Ctx::ktab(int C, int H, int W, int kh, int kw, int dh, int dw) {
+  auto key = std::make_tuple(C, H, W, kh, kw, dh, dw);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = ktabs.find(key);
+  if (it != ktabs.end()) return it->second;
+  // VirtualIm2Col row offsets (im2col.rs:104-124): row r = (c, ky, kx).
+  std::vector<int2> tab((size_t)C * kh * kw);
+  size_t r = 0;
+  for (int c = 0; c < C; c++)
+    for (int ky = 0; ky < kh; ky++)
+      for (int kx = 0; kx < kw; kx++) {
+        int kyd = ky * dh, kxd = kx * dw;
+        tab[r].x = c * H * W + kyd * W + kxd;
+        tab[r].y = (kyd << 16) | kxd;
+        r++;
+      }
+  int2* d = nullptr;
+  if (hipMalloc(&d, tab.size() * sizeof(int2)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess)
+    return nullptr;
+  ktabs[key] = d;
+  return d;
+}
+
+// calc_output_size_and_padding (src/ops/pooling.rs:27-89).
+rtenhip_status output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h, int64_t k_w,
+                                       int64_t stride_h, int64_t stride_w, int pad_mode,
+                                       const int64_t* pads_in, int64_t dil_y, int64_t dil_x,
+                                       int64_t out_hw[2], int64_t pads[4]) {
+  if (dil_y == 0 || dil_x == 0) return fail(RTENHIP_INVALID_VALUE, "Dilations must be > 0");
+  if (stride_h == 0 || stride_w == 0) return fail(RTENHIP_INVALID_VALUE, "Strides must be > 0");
+  if (pad_mode == 1) {
+    int64_t oh = (in_h + stride_h - 1) / stride_h, ow = (in_w + stride_w - 1) / stride_w;
+    int64_t th = std::max<int64_t>(0, (oh - 1) * stride_h + (k_h - 1) * dil_y + 1 - in_h);
+    int64_t tw = std::max<int64_t>(0, (ow - 1) * stride_w + (k_w - 1) * dil_x + 1 - in_w);
+    pads[0] = th / 2;
+    pads[1] = tw / 2;
+    pads[2] = (th + 1) / 2;
+    pads[3] = (tw + 1) / 2;
+    out_hw[0] = oh;
+    out_hw[1] = ow;
+    return RTENHIP_OK;
+  }
+  if (!pads_in) return fail(RTENHIP_INVALID_VALUE, "Expected 4 padding values");
+  for (int i = 0; i < 4; i++) pads[i] = pads_in[i];
+  int64_t ph = in_h + pads[0] + pads[2], pw = in_w + pads[1] + pads[3];
+  int64_t dkh = k_h + (k_h - 1) * (dil_y - 1), dkw = k_w + (k_w - 1) * (dil_x - 1);
+  if (ph < dkh || pw < dkw) return fail(RTENHIP_INVALID_VALUE, "Input too small for kernel size");
+  out_hw[0] = (ph - dil_y * (k_h - 1) - 1) / stride_h + 1;
+  out_hw[1] = (pw - dil_x * (k_w - 1) - 1) / stride_w + 1;
+  return RTENHIP_OK;
+}
+
+// Resolved conv geometry shared by shape inference and execution.
+struct ConvPlan {
+  int64_t N, C, H, W, O, KC, kh, kw, sh, sw, dh, dw, oh, ow, groups;
+  int64_t pads[4];
+  bool one_d;
+};
+
+static rtenhip_status plan_conv(const rtenhip_tensor* x, const rtenhip_tensor* w, int pad_mode,
+                                const int64_t* pads, const int64_t* strides,
+                                const int64_t* dilations, int64_t groups, ConvPlan& p) {
+  if (!x || !w) return fail(RTENHIP_MISSING_INPUTS, "Missing inputs");
+  p.one_d = x->ndim == 3;
+  int64_t p4[4] = {0, 0, 0, 0};
+  if (p.one_d) {
+    // conv.rs:96-143: 1-D conv as 2-D with H = 1.
+    if (w->ndim != 3) return fail(RTENHIP_INVALID_VALUE, "Expected kernel to have 3 dims");
+    p.N = x->shape[0];
+    p.C = x->shape[1];
+    p.H = 1;
+    p.W = x->shape[2];
+    p.O = w->shape[0];
+    p.KC = w->shape[1];
+    p.kh = 1;
+    p.kw = w->shape[2];
+    p.sh = 1;
+    p.sw = strides ? strides[0] : 1;
+    p.dh = 1;
+    p.dw = dilations ? dilations[0] : 1;
+    if (pads) {
+      p4[1] = pads[0];
+      p4[3] = pads[1];
+    }
+  } else {
+    if (x->ndim != 4) return fail(RTENHIP_INVALID_VALUE, "Expected input to have 4 dims");
+    if (w->ndim != 4) return fail(RTENHIP_INVALID_VALUE, "Expected kernel to have 4 dims");
+    p.N = x->shape[0];
+    p.C = x->shape[1];
+    p.H = x->shape[2];
+    p.W = x->shape[3];
+    p.O = w->shape[0];
+    p.KC = w->shape[1];
+    p.kh = w->shape[2];
+    p.kw = w->shape[3];
+    p.sh = strides ? strides[0] : 1;
+    p.sw = strides ? strides[1] : 1;
+    p.dh = dilations ? dilations[0] : 1;
+    p.dw = dilations ? dilations[1] : 1;
+    if (pads)
+      for (int i = 0; i < 4; i++) p4[i] = pads[i];
+  }
+  p.groups = groups;
+  int64_t ohw[2];
+  rtenhip_status st = output_size_and_padding(p.H, p.W, p.kh, p.kw, p.sh, p.sw, pad_mode, p4, p.dh,
+                                              p.dw, ohw, p.pads);
+  if (st) return st;
+  p.oh = ohw[0];
+  p.ow = ohw[1];
+  if (groups == 0 || p.C / groups != p.KC)
+    return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES,
+                "Input channels (per group) does not match kernel input channels");
+  if (p.C % groups != 0 || p.O % groups != 0)
+    return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES,
+                "Input channels and output channels must be divisible by group count");
+  return RTENHIP_OK;
+}
+
+rtenhip_status conv_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* w,
+                         const float* bias, int pad_mode, const int64_t* pads,
+                         const int64_t* strides, const int64_t* dilations, int64_t groups,
+                         const float* residual, int act, float lo, float hi, rtenhip_tensor* y) {
+  ConvPlan p;
+  rtenhip_status st = plan_conv(x, w, pad_mode, pads, strides, dilations, groups, p);
+  if (st) return st;
+  hipStream_t s = c->stream;
+  if (!is_contiguous(*w)) return fail(RTENHIP_UNSUPPORTED_VALUE, "Conv weights must be contiguous");
+  const float* xd = x->data;
+  if (!is_contiguous(*x)) {
+    float* tmp = c->scratch_floats(numel(*x), 0);
+    if (!tmp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    st = launch_copy_strided(*x, tmp, s);
+    if (st) return st;
+    xd = tmp;
+  }
+  const int64_t P = p.oh * p.ow;
+  const bool has_pad = p.pads[0] || p.pads[1] || p.pads[2] || p.pads[3];
+  if (p.N == 0 || p.O == 0 || P == 0) return RTENHIP_OK;
+
+  if (p.kh == 1 && p.kw == 1 && !has_pad && p.groups == 1 && p.sh == 1 && p.sw == 1 &&
+      p.dh == 1 && p.dw == 1) {
+    // conv_2d_pointwise (conv.rs:24-68): per image W[O,C] @ X_n[C,HW] (+bias).
+    if (p.O == 1) {
+      // A has one row -> the reference takes gemv (gemm.rs:767-780).
+      for (int64_t n = 0; n < p.N; n++) {
+        st = launch_gemv(P, p.C, w->data, xd + n * p.C * P, P, 1, y->data + n * P, 1.f, 0.f, bias,
+                         c->ref_threads, s);
+        if (st) return st;
+      }
+      if (residual || act) {
+        // Rare path: apply fused epilogue as separate elementwise passes.
+        if (residual) {
+          BcastDesc d{};
+          st = launch_binary(RTENHIP_BINARY_ADD, y->data, residual, y->data, p.N * P, d, 0, 1, 1, s);
+          if (st) return st;
+        }
+        if (act == RTENHIP_ACT_RELU) st = launch_unary(RTENHIP_UNARY_RELU, y->data, y->data, p.N * P, 0, 0, s);
+        if (act == RTENHIP_ACT_CLIP) st = launch_unary(RTENHIP_UNARY_CLIP, y->data, y->data, p.N * P, lo, hi, s);
+      }
+      return st;
+    }
+    GemmDesc d{};
+    d.M = (int)p.O;
+    d.N = (int)(p.N * P);
+    d.K = (int)p.C;
+    d.a = w->data;
+    d.a_m = p.C;
+    d.a_k = 1;
+    d.bmode = 2;
+    d.b = xd;
+    d.C = (int)p.C;
+    d.H = (int)p.H;
+    d.W = (int)p.W;
+    d.OW = (int)p.ow;
+    d.P = (int)P;
+    d.x_img = p.C * p.H * p.W;
+    d.omode = 1;
+    d.out = y->data;
+    d.out_img = p.O * P;
+    d.bias = bias;
+    d.residual = residual;
+    d.alpha = 1.f;
+    d.beta = 0.f;
+    d.act = act;
+    d.act_lo = lo;
+    d.act_hi = hi;
+    return launch_gemm(d, s);
+  }
+  if (p.C == p.O && p.groups == p.C) {
+    return launch_depthwise(xd, w->data, bias, y->data, (int)p.N, (int)p.C, (int)p.H, (int)p.W,
+                            (int)p.oh, (int)p.ow, (int)p.kh, (int)p.kw, (int)p.sh, (int)p.sw,
+                            (int)p.dh, (int)p.dw, (int)p.pads[0], (int)p.pads[1], residual, act,
+                            lo, hi, s);
+  }
+  const int64_t opg = p.O / p.groups, ipg = p.C / p.groups;
+  const int64_t K = ipg * p.kh * p.kw;
+  const int2* tab = c->ktab((int)ipg, (int)p.H, (int)p.W, (int)p.kh, (int)p.kw, (int)p.dh,
+                            (int)p.dw);
+  if (!tab) return fail(RTENHIP_HIP_ERROR, "im2col table allocation failed");
+  for (int64_t g = 0; g < p.groups; g++) {
+    GemmDesc d{};
+    d.M = (int)opg;
+    d.N = (int)(p.N * P);
+    d.K = (int)K;
+    d.a = w->data + g * opg * K;
+    d.a_m = K;
+    d.a_k = 1;
+    d.bmode = 1;
+    d.b = xd + g * ipg * p.H * p.W;
+    d.C = (int)ipg;
+    d.H = (int)p.H;
+    d.W = (int)p.W;
+    d.OW = (int)p.ow;
+    d.P = (int)P;
+    d.sh = (int)p.sh;
+    d.sw = (int)p.sw;
+    d.pt = (int)p.pads[0];
+    d.pl = (int)p.pads[1];
+    d.x_img = p.C * p.H * p.W;
+    d.ktab = tab;
+    d.omode = 1;
+    d.out = y->data + g * opg * P;
+    d.out_img = p.O * P;
+    d.bias = bias ? bias + g * opg : nullptr;
+    d.residual = residual ? residual + g * opg * P : nullptr;
+    d.alpha = 1.f;
+    d.beta = 0.f;
+    d.act = act;
+    d.act_lo = lo;
+    d.act_hi = hi;
+    st = launch_gemm(d, s);
+    if (st) return st;
+  }
+  return RTENHIP_OK;
+}
+
+// GemmExecutor::gemm_bias on strided device matrices (gemm.rs:733-930).
+rtenhip_status gemm_impl(Ctx* c, int64_t m, int64_t n, int64_t k, const float* a, int64_t a_rs,
+                         int64_t a_cs, const float* b, int64_t b_rs, int64_t b_cs, float* out,
+                         int64_t out_rs, float alpha, float beta, const float* bias, int act) {
+  hipStream_t s = c->stream;
+  if (m == 0 || n == 0) return RTENHIP_OK;
+  if (m == 1 && k > 0 && act == 0) {
+    return launch_gemv(n, k, a, b, b_rs, b_cs, out, alpha, beta, bias, c->ref_threads, s);
+  }
+  GemmDesc d{};
+  d.M = (int)m;
+  d.N = (int)n;
+  d.K = (int)k;
+  d.a = a;
+  d.a_m = a_rs;
+  d.a_k = a_cs;
+  d.bmode = 0;
+  d.b = b;
+  d.b_k = b_rs;
+  d.b_n = b_cs;
+  d.omode = 0;
+  d.out = out;
+  d.out_m = out_rs;
+  d.bias = bias;
+  d.cin = beta != 0.f ? out : nullptr;
+  d.alpha = alpha;
+  d.beta = beta;
+  d.act = act;
+  if (k == 0) {
+    // gemm.rs:757-765: out = beta * (beta == 0 ? 0 : out), no bias.
+    d.a = nullptr;
+    d.bias = nullptr;
+  }
+  return launch_gemm(d, s);
+}
+
+}  // namespace rtenhip
+
+using namespace rtenhip;
+
+static Ctx* C_(rtenhip_ctx* c) { return reinterpret_cast<Ctx*>(c); }
+
+extern "C" {
+
+rtenhip_ctx* rtenhip_create(int device) {
+  if (hipSetDevice(device) != hipSuccess) {
+    set_error(RTENHIP_HIP_ERROR, "hipSetDevice failed");
+    return nullptr;
+  }
+  return reinterpret_cast<rtenhip_ctx*>(new Ctx(device));
+}
+
+void rtenhip_destroy(rtenhip_ctx* ctx) { delete C_(ctx); }
+
+rtenhip_status rtenhip_set_stream(rtenhip_ctx* ctx, void* stream) {
+  C_(ctx)->stream = reinterpret_cast<hipStream_t>(stream);
+  return RTENHIP_OK;
+}
+void* rtenhip_get_stream(rtenhip_ctx* ctx) { return C_(ctx)->stream; }
+
+const char* rtenhip_last_error_message(void) { return g_err.c_str(); }
+
+rtenhip_status rtenhip_synchronize(rtenhip_ctx* ctx) {
+  RTENHIP_HIP_CHECK(hipStreamSynchronize(C_(ctx)->stream));
+  return RTENHIP_OK;
+}
+
+void* rtenhip_malloc(rtenhip_ctx*, size_t bytes) {
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes ? bytes : 4) != hipSuccess) return nullptr;
+  return p;
+}
+void rtenhip_free(rtenhip_ctx*, void* ptr) {
+  if (ptr) (void)hipFree(ptr);
+}
+rtenhip_status rtenhip_memcpy_h2d(rtenhip_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  RTENHIP_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, C_(ctx)->stream));
+  RTENHIP_HIP_CHECK(hipStreamSynchronize(C_(ctx)->stream));
+  return RTENHIP_OK;
+}
+rtenhip_status rtenhip_memcpy_d2h(rtenhip_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  RTENHIP_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, C_(ctx)->stream));
+  RTENHIP_HIP_CHECK(hipStreamSynchronize(C_(ctx)->stream));
+  return RTENHIP_OK;
+}
+
+const char* rtenhip_build_info(void) { return "rten-hip gfx950 (CDNA4) f32 MFMA backend v0.1"; }
+
+rtenhip_status rtenhip_output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h,
+                                               int64_t k_w, int64_t stride_h, int64_t stride_w,
+                                               int pad_mode, const int64_t pads_in[4],
+                                               int64_t dil_h, int64_t dil_w, int64_t out_hw[2],
+                                               int64_t pads_out[4]) {
+  return output_size_and_padding(in_h, in_w, k_h, k_w, stride_h, stride_w, pad_mode, pads_in,
+                                 dil_h, dil_w, out_hw, pads_out);
+}
+
+rtenhip_status rtenhip_gemm_f32(rtenhip_ctx* ctx, int64_t m, int64_t n, int64_t k,
+                                const float* a, int64_t a_rs, int64_t a_cs, const float* b,
+                                int64_t b_rs, int64_t b_cs, float* out, int64_t out_rs,
+                                float alpha, float beta, const float* bias) {
+  return gemm_impl(C_(ctx), m, n, k, a, a_rs, a_cs, b, b_rs, b_cs, out, out_rs, alpha, beta, bias,
+                   0);
+}
+
+rtenhip_status rtenhip_conv_output_shape(const rtenhip_tensor* x, const rtenhip_tensor* w,
+                                         int pad_mode, const int64_t* pads,
+                                         const int64_t* strides, const int64_t* dilations,
+                                         int64_t groups, int64_t* out_shape, int32_t* out_ndim) {
+  ConvPlan p;
+  rtenhip_status st = plan_conv(x, w, pad_mode, pads, strides, dilations, groups, p);
+  if (st) return st;
+  out_shape[0] = p.N;
+  out_shape[1] = p.O;
+  if (p.one_d) {
+    out_shape[2] = p.ow;
+    *out_ndim = 3;
+  } else {
+    out_shape[2] = p.oh;
+    out_shape[3] = p.ow;
+    *out_ndim = 4;
+  }
+  return RTENHIP_OK;
+}
+
+rtenhip_status rtenhip_conv_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                const rtenhip_tensor* w, const float* bias, int pad_mode,
+                                const int64_t* pads, const int64_t* strides,
+                                const int64_t* dilations, int64_t groups, const float* residual,
+                                int act, float act_lo, float act_hi, rtenhip_tensor* y) {
+  int64_t os[4];
+  int32_t ond;
+  rtenhip_status st =
+      rtenhip_conv_output_shape(x, w, pad_mode, pads, strides, dilations, groups, os, &ond);
+  if (st) return st;
+  if (!y || y->ndim != ond) return fail(RTENHIP_INCORRECT_OUTPUT_TYPE, "Output has wrong rank");
+  for (int i = 0; i < ond; i++)
+    if (y->shape[i] != os[i]) return fail(RTENHIP_INCORRECT_OUTPUT_TYPE, "Output has wrong shape");
+  if (!is_contiguous(*y)) return fail(RTENHIP_UNSUPPORTED_VALUE, "Output must be contiguous");
+  return conv_impl(C_(ctx), x, w, bias, pad_mode, pads, strides, dilations, groups, residual, act,
+                   act_lo, act_hi, y);
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// Internal helpers shared by the HIP kernels and the host runtime.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/rten_hip.h"
+
+namespace rtenhip {
+
+// Thread-local last error (rtenhip_last_error_message).
+void set_error(int code, const std::string& msg);
+rtenhip_status fail(rtenhip_status code, const char* msg);
+rtenhip_status hip_fail(hipError_t e, const char* where);
+
+#define RTENHIP_HIP_CHECK(expr)                              \
+  do {                                                       \
+    hipError_t _e = (expr);                                  \
+    if (_e != hipSuccess) return ::rtenhip::hip_fail(_e, #expr); \
+  } while (0)
+
+// Launch-error check after a kernel launch.
+#define RTENHIP_LAUNCH_CHECK() RTENHIP_HIP_CHECK(hipGetLastError())
+
+inline int64_t numel(const rtenhip_tensor& t) {
+  int64_t n = 1;
+  for (int i = 0; i < t.ndim; i++) n *= t.shape[i];
+  return n;
+}
+
+inline bool is_contiguous(const rtenhip_tensor& t) {
+  int64_t s = 1;
+  for (int i = t.ndim - 1; i >= 0; i--) {
+    if (t.shape[i] != 1 && t.strides[i] != s) return false;
+    s *= t.shape[i];
+  }
+  return true;
+}
+
+inline rtenhip_tensor make_tensor(float* data, const int64_t* shape, int ndim) {
+  rtenhip_tensor t{};
+  t.data = data;
+  t.ndim = ndim;
+  int64_t s = 1;
+  for (int i = ndim - 1; i >= 0; i--) {
+    t.shape[i] = shape[i];
+    t.strides[i] = s;
+    s *= shape[i];
+  }
+  return t;
+}
+
+struct Ctx;
+hipStream_t stream_of(rtenhip_ctx* ctx);
+
+// ---- kernel launchers (implemented in the .hip files) ----
+
+// Implicit-GEMM engine (gemm_mfma.hip).  See GemmDesc.
+struct GemmDesc {
+  int M, N, K;
+  // A[m,k] = a[m*a_m + k*a_k]
+  const float* a;
+  int64_t a_m, a_k;
+  // B source: 0 dense B[k,n] = b[k*b_k + n*b_n]; 1 im2col of NCHW x;
+  // 2 pointwise (1x1 s1 p0) conv of NCHW x.
+  int bmode;
+  const float* b;
+  int64_t b_k, b_n;
+  // conv geometry (bmode 1/2): per-group input [C,H,W] of image stride x_img
+  int C, H, W, OW, P, sh, sw, pt, pl;
+  int64_t x_img;
+  const int2* ktab;  // bmode 1: per k {c*H*W + ky*dh*W + kx*dw, (ky*dh)<<16 | kx*dw}
+  // output: omode 0 dense out[m*out_m + n]; 1 conv out[img*out_img + m*P + p]
+  int omode;
+  float* out;
+  int64_t out_m, out_img;
+  const float* bias;      // [M] or null
+  const float* residual;  // same addressing as out, or null
+  const float* cin;       // dense C input for beta != 0 (BMODE 0 only), or null
+  float alpha, beta;
+  int act;
+  float act_lo, act_hi;
+  // Batched MatMul (dense modes): blockIdx.y = flat batch index over up to 4
+  // broadcast prefix dims; element offsets of a / b / out per prefix dim.
+  int nbatch;  // 0 or 1 = not batched
+  int nbp;
+  int64_t pshape[4], pa[4], pb[4], po[4];
+};
+rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s);
+
+// gemv with the reference's summation order (gemm.rs:651-704, kernels.rs:26-194).
+rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b, int64_t b_rs,
+                           int64_t b_cs, float* out, float alpha, float beta, const float* bias,
+                           int64_t ref_threads, hipStream_t s);
+
+// Elementwise / pooling / normalisation (elementwise.hip, pool.hip, norm.hip).
+rtenhip_status launch_unary(int op, const float* x, float* y, int64_t n, float p0, float p1,
+                            hipStream_t s);
+struct BcastDesc {
+  int ndim;
+  int64_t shape[RTENHIP_MAX_DIMS];
+  int64_t sa[RTENHIP_MAX_DIMS], sb[RTENHIP_MAX_DIMS];
+};
+rtenhip_status launch_binary(int op, const float* a, const float* b, float* y, int64_t n,
+                             const BcastDesc& d, int mode, int64_t inner, int64_t nb,
+                             hipStream_t s);
+rtenhip_status launch_batch_norm(const float* x, float* y, int64_t N, int64_t C, int64_t inner,
+                                 const float* scale, const float* bias, const float* mean,
+                                 const float* var, float eps, hipStream_t s);
+rtenhip_status launch_pool(int is_max, const float* x, float* y, int64_t NC, int H, int W,
+                           int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
+                           int count_include_pad, hipStream_t s);
+rtenhip_status launch_gap(const float* x, float* y, int64_t NC, int64_t HW, hipStream_t s);
+rtenhip_status launch_depthwise(const float* x, const float* w, const float* bias, float* y,
+                                int N, int C, int H, int W, int OH, int OW, int kh, int kw,
+                                int sh, int sw, int dh, int dw, int pt, int pl,
+                                const float* residual, int act, float lo, float hi,
+                                hipStream_t s);
+rtenhip_status launch_softmax(const float* x, float* y, int64_t rows, int64_t len,
+                              hipStream_t s);
+rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
+                                 const float* scale, const float* bias, float eps,
+                                 hipStream_t s);
+rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s);
+
+}  // namespace rtenhip

@@ -1,0 +1,210 @@
+// Elementwise kernels: unary activations (src/ops/unary_elementwise.rs with
+// rten-vecmath numerics), broadcasting binary ops
+// (src/ops/binary_elementwise.rs:158-439), BatchNormalization
+// (src/ops/norm.rs:18-54) and strided copies (make-contiguous).
+//
+// All are HBM-bound streaming kernels: 16-byte vector loads/stores where the
+// layout allows, grid capped at ~2048 blocks and grid-strided.
+#include "common.h"
+#include "vecmath.h"
+
+namespace rtenhip {
+
+template <int OP>
+__device__ __forceinline__ float unary_apply(float v, float p0, float p1) {
+  if constexpr (OP == RTENHIP_UNARY_RELU) return rust_max(v, 0.f);
+  if constexpr (OP == RTENHIP_UNARY_CLIP) return rust_clamp(v, p0, p1);
+  if constexpr (OP == RTENHIP_UNARY_GELU) return vm_gelu(v);
+  if constexpr (OP == RTENHIP_UNARY_ERF) return vm_erf(v);
+  if constexpr (OP == RTENHIP_UNARY_SIGMOID) return vm_sigmoid(v);
+  if constexpr (OP == RTENHIP_UNARY_TANH) return vm_tanh(v);
+  if constexpr (OP == RTENHIP_UNARY_EXP) return vm_exp(v);
+  if constexpr (OP == RTENHIP_UNARY_SILU) return __fmul_rn(v, vm_sigmoid(v));
+  return v;
+}
+
+template <int OP>
+__global__ void unary_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                             float p0, float p1) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool vec = ((((uintptr_t)x) | ((uintptr_t)y)) & 15) == 0;
+  if (vec) {
+    const int64_t n4 = n / 4;
+    for (int64_t v = i; v < n4; v += stride) {
+      float4 a = reinterpret_cast<const float4*>(x)[v];
+      a.x = unary_apply<OP>(a.x, p0, p1);
+      a.y = unary_apply<OP>(a.y, p0, p1);
+      a.z = unary_apply<OP>(a.z, p0, p1);
+      a.w = unary_apply<OP>(a.w, p0, p1);
+      reinterpret_cast<float4*>(y)[v] = a;
+    }
+    for (int64_t t = n4 * 4 + i; t < n; t += stride) y[t] = unary_apply<OP>(x[t], p0, p1);
+  } else {
+    for (int64_t t = i; t < n; t += stride) y[t] = unary_apply<OP>(x[t], p0, p1);
+  }
+}
+
+static dim3 stream_grid(int64_t n, int per_thread = 4) {
+  int64_t blocks = (n / per_thread + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 4096) blocks = 4096;
+  return dim3((unsigned)blocks);
+}
+
+rtenhip_status launch_unary(int op, const float* x, float* y, int64_t n, float p0, float p1,
+                            hipStream_t s) {
+  if (n == 0) return RTENHIP_OK;
+  dim3 g = stream_grid(n), b(256);
+  switch (op) {
+#define CASE(OPV)                                                              \
+  case OPV:                                                                    \
+    hipLaunchKernelGGL(unary_kernel<OPV>, g, b, 0, s, x, y, n, p0, p1);        \
+    break;
+    CASE(RTENHIP_UNARY_RELU)
+    CASE(RTENHIP_UNARY_CLIP)
+    CASE(RTENHIP_UNARY_GELU)
+    CASE(RTENHIP_UNARY_ERF)
+    CASE(RTENHIP_UNARY_SIGMOID)
+    CASE(RTENHIP_UNARY_TANH)
+    CASE(RTENHIP_UNARY_EXP)
+    CASE(RTENHIP_UNARY_SILU)
+#undef CASE
+    default:
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Unsupported unary op");
+  }
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+template <int OP>
+__device__ __forceinline__ float binary_apply(float a, float b) {
+  if constexpr (OP == RTENHIP_BINARY_ADD) return __fadd_rn(a, b);
+  if constexpr (OP == RTENHIP_BINARY_SUB) return __fsub_rn(a, b);
+  if constexpr (OP == RTENHIP_BINARY_MUL) return __fmul_rn(a, b);
+  return __fdiv_rn(a, b);
+}
+
+// mode 0: same shape, contiguous.  mode 1: b repeats every `inner` elements
+// of a (row broadcast, e.g. bias [C] over [..., C]).  mode 2: b constant per
+// run of `inner` elements cycling (e.g. [C,1,1] over [N,C,H,W]): b index =
+// (i / inner) % nb.  mode 3: general strided broadcast.
+template <int OP>
+__global__ void binary_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                              float* __restrict__ y, int64_t n, BcastDesc d, int mode,
+                              int64_t inner, int64_t nb) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float av, bv;
+    if (mode == 0) {
+      av = a[i];
+      bv = b[i];
+    } else if (mode == 1) {
+      av = a[i];
+      bv = b[i % inner];
+    } else if (mode == 2) {
+      av = a[i];
+      bv = b[(i / inner) % nb];
+    } else {
+      int64_t rem = i, oa = 0, ob = 0;
+      for (int k = d.ndim - 1; k >= 0; k--) {
+        int64_t idx = rem % d.shape[k];
+        rem /= d.shape[k];
+        oa += idx * d.sa[k];
+        ob += idx * d.sb[k];
+      }
+      av = a[oa];
+      bv = b[ob];
+    }
+    y[i] = binary_apply<OP>(av, bv);
+  }
+}
+
+rtenhip_status launch_binary(int op, const float* a, const float* b, float* y, int64_t n,
+                             const BcastDesc& d, int mode, int64_t inner, int64_t nb,
+                             hipStream_t s) {
+  if (n == 0) return RTENHIP_OK;
+  dim3 g = stream_grid(n, 1), bl(256);
+  switch (op) {
+    case RTENHIP_BINARY_ADD:
+      hipLaunchKernelGGL(binary_kernel<RTENHIP_BINARY_ADD>, g, bl, 0, s, a, b, y, n, d, mode, inner, nb);
+      break;
+    case RTENHIP_BINARY_SUB:
+      hipLaunchKernelGGL(binary_kernel<RTENHIP_BINARY_SUB>, g, bl, 0, s, a, b, y, n, d, mode, inner, nb);
+      break;
+    case RTENHIP_BINARY_MUL:
+      hipLaunchKernelGGL(binary_kernel<RTENHIP_BINARY_MUL>, g, bl, 0, s, a, b, y, n, d, mode, inner, nb);
+      break;
+    case RTENHIP_BINARY_DIV:
+      hipLaunchKernelGGL(binary_kernel<RTENHIP_BINARY_DIV>, g, bl, 0, s, a, b, y, n, d, mode, inner, nb);
+      break;
+    default:
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Unsupported binary op");
+  }
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+// batch_norm_in_place (norm.rs:18-54): per (n, c) plane,
+// y = (x - mean) * (scale / sqrt(var + eps)) + bias, separate roundings.
+__global__ void batch_norm_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t C,
+                                  int64_t inner, const float* __restrict__ scale,
+                                  const float* __restrict__ bias, const float* __restrict__ mean,
+                                  const float* __restrict__ var, float eps) {
+  const int64_t plane = blockIdx.y;  // n*C + c
+  const int64_t c = plane % C;
+  const float sc = __fdiv_rn(scale[c], sqrt_rn(__fadd_rn(var[c], eps)));
+  const float mu = mean[c], bi = bias[c];
+  const float* xp = x + plane * inner;
+  float* yp = y + plane * inner;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < inner;
+       i += (int64_t)gridDim.x * blockDim.x)
+    yp[i] = __fadd_rn(__fmul_rn(__fsub_rn(xp[i], mu), sc), bi);
+}
+
+rtenhip_status launch_batch_norm(const float* x, float* y, int64_t N, int64_t C, int64_t inner,
+                                 const float* scale, const float* bias, const float* mean,
+                                 const float* var, float eps, hipStream_t s) {
+  if (N * C * inner == 0) return RTENHIP_OK;
+  int64_t bx = (inner + 255) / 256;
+  if (bx > 64) bx = 64;
+  hipLaunchKernelGGL(batch_norm_kernel, dim3((unsigned)bx, (unsigned)(N * C)), dim3(256), 0, s, x,
+                     y, C, inner, scale, bias, mean, var, eps);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+// Strided -> contiguous copy (to_contiguous_in).
+struct CopyDesc {
+  int ndim;
+  int64_t shape[RTENHIP_MAX_DIMS];
+  int64_t strides[RTENHIP_MAX_DIMS];
+};
+__global__ void copy_strided_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n,
+                                    CopyDesc d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t rem = i, off = 0;
+    for (int k = d.ndim - 1; k >= 0; k--) {
+      off += (rem % d.shape[k]) * d.strides[k];
+      rem /= d.shape[k];
+    }
+    y[i] = x[off];
+  }
+}
+
+rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s) {
+  int64_t n = numel(src);
+  if (n == 0) return RTENHIP_OK;
+  CopyDesc d{};
+  d.ndim = src.ndim;
+  for (int i = 0; i < src.ndim; i++) {
+    d.shape[i] = src.shape[i];
+    d.strides[i] = src.strides[i];
+  }
+  hipLaunchKernelGGL(copy_strided_kernel, stream_grid(n, 1), dim3(256), 0, s, src.data, dst, n, d);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+}  // namespace rtenhip

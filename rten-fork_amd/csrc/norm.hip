@@ -1,0 +1,149 @@
+// Softmax and LayerNormalization: one wavefront per row.
+//
+// Both reproduce the reference's summation order so results are bit-exact:
+//  - Softmax = vec_softmax_in_place (rten-vecmath/src/softmax.rs:14-56) on the
+//    AVX2 width (8 lanes): max from f32::MIN, e_i = exp(x_i - max), eight
+//    partial sums over i = j (mod 8) in index order, folded 0 + p0 + ... + p7,
+//    then y_i = e_i / sum.  The exps run on all 64 lanes; only the eight short
+//    chains and the final fold are serial.
+//  - LayerNorm = layer_normalization (src/ops/norm.rs:245-299): mean via
+//    slice_sum (8-element chunks, src/slice_reductions.rs:37-53), x - mean,
+//    1/sqrt(iter_sum(d*d)/n + eps) (iter_sum: groups of 4,
+//    slice_reductions.rs:57-84), then * inv, * scale, + bias.
+#include "common.h"
+#include "vecmath.h"
+
+#include <cfloat>
+
+namespace rtenhip {
+
+constexpr int ROWS_PER_BLOCK = 4;
+
+// rows handled by one wave each; `lds` holds ROWS_PER_BLOCK * len floats.
+__global__ __launch_bounds__(256) void softmax_kernel(const float* __restrict__ x,
+                                                      float* __restrict__ y, int64_t rows,
+                                                      int len, int use_lds) {
+  extern __shared__ float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave;
+  const bool active = row < rows;
+  const float* xr = x + (active ? row : 0) * len;
+  float* yr = y + (active ? row : 0) * len;
+  float* buf = use_lds ? lds + wave * len : yr;
+
+  float m = -FLT_MAX;
+  if (active)
+    for (int i = lane; i < len; i += 64) m = rust_max(m, xr[i]);
+  for (int off = 32; off > 0; off >>= 1) m = rust_max(m, __shfl_xor(m, off));
+  if (active)
+    for (int i = lane; i < len; i += 64) buf[i] = vm_exp(__fsub_rn(xr[i], m));
+  __syncthreads();
+  float part = 0.f;
+  if (active && lane < 8)
+    for (int i = lane; i < len; i += 8) part = __fadd_rn(part, buf[i]);
+  float sum = 0.f;
+  for (int j = 0; j < 8; j++) sum = __fadd_rn(sum, __shfl(part, j));
+  if (active)
+    for (int i = lane; i < len; i += 64) yr[i] = __fdiv_rn(buf[i], sum);
+}
+
+rtenhip_status launch_softmax(const float* x, float* y, int64_t rows, int64_t len,
+                              hipStream_t s) {
+  if (rows == 0 || len == 0) return RTENHIP_OK;
+  const int use_lds = len <= 4096;
+  // Without LDS the exps are staged in y itself; in-place (x == y) is safe
+  // because each row is read fully (max) before any write... except the
+  // exp pass reads x_i and writes y_i at the same index, which is fine.
+  size_t shmem = use_lds ? (size_t)ROWS_PER_BLOCK * len * sizeof(float) : 0;
+  int64_t blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)blocks), dim3(256), shmem, s, x, y, rows,
+                     (int)len, use_lds);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+__global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict__ x,
+                                                         float* __restrict__ y, int64_t rows,
+                                                         int len, const float* __restrict__ scale,
+                                                         const float* __restrict__ bias,
+                                                         float eps) {
+  extern __shared__ float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wave;
+  const bool active = row < rows;
+  const float* xr = x + (active ? row : 0) * len;
+  float* yr = y + (active ? row : 0) * len;
+  // Per-wave scratch: chunk/group partial sums (len/4 + 2 floats max).
+  float* part = lds + wave * (len / 4 + 8);
+
+  // slice_sum: full 8-chunks in parallel, then a serial fold.
+  const int nchunks = len / 8;
+  if (active)
+    for (int c = lane; c < nchunks; c += 64) {
+      const float* p = xr + 8 * c;
+      float z0 = __fadd_rn(p[0], p[4]), z1 = __fadd_rn(p[1], p[5]);
+      float z2 = __fadd_rn(p[2], p[6]), z3 = __fadd_rn(p[3], p[7]);
+      part[c] = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
+    }
+  __syncthreads();
+  float mean = 0.f;
+  if (lane == 0 && active) {
+    float total = 0.f;
+    for (int c = 0; c < nchunks; c++) total = __fadd_rn(total, part[c]);
+    if (nchunks * 8 < len) {
+      float t = 0.f;
+      for (int i = nchunks * 8; i < len; i++) t = __fadd_rn(t, xr[i]);
+      total = __fadd_rn(total, t);
+    }
+    mean = __fdiv_rn(total, (float)len);
+  }
+  mean = __shfl(mean, 0);
+  __syncthreads();
+
+  // iter_sum of squares of d = x - mean: groups of 4 while n > 4, then the tail.
+  const int ngroups = len > 4 ? (len - 1) / 4 : 0;
+  if (active)
+    for (int g = lane; g < ngroups; g += 64) {
+      const float* p = xr + 4 * g;
+      float d0 = __fsub_rn(p[0], mean), d1 = __fsub_rn(p[1], mean);
+      float d2 = __fsub_rn(p[2], mean), d3 = __fsub_rn(p[3], mean);
+      float ab = __fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1));
+      float cd = __fadd_rn(__fmul_rn(d2, d2), __fmul_rn(d3, d3));
+      part[g] = __fadd_rn(ab, cd);
+    }
+  __syncthreads();
+  float inv = 0.f;
+  if (lane == 0 && active) {
+    float sum = 0.f;
+    for (int g = 0; g < ngroups; g++) sum = __fadd_rn(sum, part[g]);
+    for (int i = 4 * ngroups; i < len; i++) {
+      float d = __fsub_rn(xr[i], mean);
+      sum = __fadd_rn(sum, __fmul_rn(d, d));
+    }
+    float ms = __fdiv_rn(sum, (float)len);
+    inv = __fdiv_rn(1.f, sqrt_rn(__fadd_rn(ms, eps)));
+  }
+  inv = __shfl(inv, 0);
+  if (active)
+    for (int i = lane; i < len; i += 64) {
+      float v = __fmul_rn(__fsub_rn(xr[i], mean), inv);
+      v = __fmul_rn(v, scale[i]);
+      if (bias) v = __fadd_rn(v, bias[i]);
+      yr[i] = v;
+    }
+}
+
+rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
+                                 const float* scale, const float* bias, float eps,
+                                 hipStream_t s) {
+  if (rows == 0 || len == 0) return RTENHIP_OK;
+  size_t shmem = (size_t)ROWS_PER_BLOCK * (len / 4 + 8) * sizeof(float);
+  if (shmem > 160 * 1024) return fail(RTENHIP_UNSUPPORTED_VALUE, "LayerNorm row too long");
+  int64_t blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  hipLaunchKernelGGL(layer_norm_kernel, dim3((unsigned)blocks), dim3(256), shmem, s, x, y, rows,
+                     (int)len, scale, bias, eps);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+}  // namespace rtenhip

@@ -12,6 +12,9 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# The reference's gemv column blocking depends on its thread count
+# (src/gemm.rs:673); pin it so the oracle and the GPU path agree.
+os.environ.setdefault("RTEN_NUM_THREADS", "8")
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 PKG_DIR = os.path.join(ROOT, "rten-fork_amd")
 for p in (ORACLE_DIR, PKG_DIR, ROOT):

@@ -1,0 +1,352 @@
+"""GPU parity tests: every HIP operator against the CPU oracle.
+
+The oracle restates RTen's CPU path including its summation order, so the bar
+here is BIT-EXACT equality (compared as uint32 bit patterns) for every op
+whose reference order the kernels reproduce.  Inputs are XorShiftRng streams
+(rten-tensor/src/rng.rs) shifted to [-0.5, 0.5).  Sizes are small enough for
+the oracle to finish in well under a second each; full-size ResNet-50 parity
+lives in test_model_gpu.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def rh():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rten_hip
+
+    rten_hip.default_context()
+    return rten_hip
+
+
+def dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def host(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def rnd(oracle, seed, *shape, scale=1.0, shift=0.5):
+    n = int(np.prod(shape)) if shape else 1
+    v = (oracle.xorshift(seed, n) - np.float32(shift)) * np.float32(scale)
+    return v.astype(np.float32).reshape(shape)
+
+
+def assert_bits(actual, expected, what=""):
+    actual = np.asarray(actual, np.float32)
+    expected = np.asarray(expected, np.float32)
+    assert actual.shape == expected.shape, (what, actual.shape, expected.shape)
+    a = actual.view(np.uint32)
+    e = expected.view(np.uint32)
+    same = (a == e) | (np.isnan(actual) & np.isnan(expected))
+    if not same.all():
+        idx = np.argwhere(~same)[:5]
+        diff = np.abs(actual.astype(np.float64) - expected).max()
+        rel = diff / max(1e-30, np.abs(expected).max())
+        pytest.fail(f"{what}: {int((~same).sum())}/{same.size} differ (max abs {diff:.3g}, "
+                    f"rel {rel:.3g}); first at {idx.tolist()}: "
+                    f"{[actual[tuple(i)] for i in idx]} vs {[expected[tuple(i)] for i in idx]}")
+
+
+# --------------------------------------------------------------------------
+# GEMM engine
+# --------------------------------------------------------------------------
+
+GEMM_SHAPES = [(1, 1, 1), (2, 3, 4), (7, 17, 33), (64, 64, 64), (65, 130, 257), (128, 128, 256),
+               (100, 300, 600), (33, 1025, 300), (257, 129, 1000), (64, 1000, 2048),
+               (16, 16, 0)]
+
+
+@pytest.mark.parametrize("m,n,k", GEMM_SHAPES)
+def test_gemm_bitexact(rh, oracle, m, n, k):
+    a = rnd(oracle, 1, m, k)
+    b = rnd(oracle, 2, k, n)
+    bias = rnd(oracle, 3, m)
+    exp = oracle.gemm(a, b, bias=bias)
+    got = host(rh.gemm(dev(a), dev(b), bias=dev(bias)))
+    assert_bits(got, exp, f"gemm {m}x{n}x{k}")
+
+
+def test_gemm_alpha_beta(rh, oracle):
+    m, n, k = 70, 50, 520
+    a, b = rnd(oracle, 4, m, k), rnd(oracle, 5, k, n)
+    init = rnd(oracle, 6, m, n)
+    for alpha, beta in ((1.0, 1.0), (1.0, 0.0)):
+        exp = oracle.gemm(a, b, alpha, beta, out=init.copy())
+        out = dev(init)
+        rh.gemm(dev(a), dev(b), alpha, beta, out=out)
+        assert_bits(host(out), exp, f"alpha={alpha} beta={beta}")
+
+
+def test_gemm_transposed_views(rh, oracle):
+    """Strided A/B (transposed views, FusedTranspose) read in place."""
+    m, n, k = 45, 70, 300
+    at = rnd(oracle, 7, k, m)
+    bt = rnd(oracle, 8, n, k)
+    exp = oracle.gemm(at.T, bt.T)
+    got = host(rh.gemm(dev(at).t(), dev(bt).t()))
+    assert_bits(got, exp, "transposed")
+
+
+@pytest.mark.parametrize("n,k,transposed", [(1000, 2048, True), (1000, 2048, False), (37, 13, True),
+                                            (300, 700, False), (129, 9, True)])
+def test_gemv_bitexact(rh, oracle, n, k, transposed):
+    """M == 1 takes the reference's gemv path and summation order."""
+    a = rnd(oracle, 9, 1, k)
+    if transposed:
+        b = rnd(oracle, 10, n, k).T  # unit row stride -> simd_gemv_transposed
+    else:
+        b = rnd(oracle, 10, k, n)
+    bias = rnd(oracle, 11, 1)
+    exp = oracle.gemm(a, b, bias=bias)
+    bd = dev(b.T).t() if transposed else dev(b)
+    got = host(rh.gemm(dev(a), bd, bias=dev(bias)))
+    assert_bits(got, exp, "gemv")
+
+
+# --------------------------------------------------------------------------
+# Conv
+# --------------------------------------------------------------------------
+
+CONV_CASES = [
+    # name, (N, C, H, W), (O, kh, kw), pads, strides, dilations, groups
+    ("resnet-conv1", (2, 3, 30, 30), (64, 7, 7), (3, 3, 3, 3), (2, 2), (1, 1), 1),
+    ("3x3-s1", (2, 64, 14, 14), (64, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 1),
+    ("3x3-s2-K1152", (2, 128, 14, 14), (128, 3, 3), (1, 1, 1, 1), (2, 2), (1, 1), 1),
+    ("1x1-pointwise", (2, 256, 7, 7), (128, 1, 1), (0, 0, 0, 0), (1, 1), (1, 1), 1),
+    ("1x1-pointwise-K1024", (3, 1024, 5, 5), (96, 1, 1), (0, 0, 0, 0), (1, 1), (1, 1), 1),
+    ("1x1-s2-im2col", (2, 64, 14, 14), (256, 1, 1), (0, 0, 0, 0), (2, 2), (1, 1), 1),
+    ("3x3-layer4", (2, 512, 7, 7), (512, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 1),
+    ("grouped", (2, 8, 9, 9), (12, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 2),
+    ("dilated", (1, 4, 11, 11), (6, 3, 3), (2, 2, 2, 2), (1, 1), (2, 2), 1),
+    ("uneven-pad", (1, 40, 6, 6), (7, 3, 3), (1, 0, 2, 1), (1, 1), (1, 1), 1),
+    ("strided-1x3", (1, 5, 9, 9), (3, 3, 3), (1, 1, 1, 1), (1, 3), (1, 1), 1),
+    ("depthwise-s1", (2, 32, 12, 12), (32, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 32),
+    ("depthwise-s2", (2, 96, 13, 13), (96, 3, 3), (1, 1, 1, 1), (2, 2), (1, 1), 96),
+    ("depthwise-pad3-s2", (1, 4, 10, 10), (4, 3, 3), (3, 3, 3, 3), (2, 2), (1, 1), 4),
+    ("pointwise-O1-gemv", (2, 20, 6, 6), (1, 1, 1), (0, 0, 0, 0), (1, 1), (1, 1), 1),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv_bitexact(rh, oracle, case):
+    name, xs, (O, kh, kw), pads, strides, dil, groups = case
+    x = rnd(oracle, 21, *xs)
+    w = rnd(oracle, 22, O, xs[1] // groups, kh, kw, scale=0.3)
+    b = rnd(oracle, 23, O)
+    exp = oracle.conv(x, w, b, pads=pads, strides=strides, dilations=dil, groups=groups)
+    got = host(rh.conv(dev(x), dev(w), dev(b), padding=pads, groups=groups, strides=strides,
+                       dilations=dil))
+    assert_bits(got, exp, name)
+
+
+def test_conv_fused_residual_relu(rh, oracle):
+    """Conv -> Add(residual) -> Relu fused epilogue == the three reference ops."""
+    x = rnd(oracle, 31, 2, 64, 14, 14)
+    w = rnd(oracle, 32, 256, 64, 1, 1, scale=0.3)
+    b = rnd(oracle, 33, 256)
+    res = rnd(oracle, 34, 2, 256, 14, 14)
+    exp = oracle.relu(oracle.add(oracle.conv(x, w, b), res))
+    got = host(rh.conv(dev(x), dev(w), dev(b), residual=dev(res), act="relu"))
+    assert_bits(got, exp, "conv+add+relu")
+    exp = oracle.clip(oracle.conv(x, w, b), 0.0, 6.0)
+    got = host(rh.conv(dev(x), dev(w), dev(b), act="clip", act_range=(0.0, 6.0)))
+    assert_bits(got, exp, "conv+clip")
+
+
+def test_conv_1d(rh, oracle):
+    x = rnd(oracle, 41, 2, 6, 30)
+    w = rnd(oracle, 42, 5, 6, 3)
+    exp = oracle.conv(x, w, None, pads=(1, 1), strides=(2,), dilations=(1,))
+    got = host(rh.conv(dev(x), dev(w), None, padding=(1, 1), strides=(2,), dilations=(1,)))
+    assert_bits(got, exp, "conv1d")
+
+
+def test_conv_errors(rh):
+    import torch
+
+    x = torch.zeros(1, 3, 4, 4, device="cuda")
+    with pytest.raises(rh.OpError) as e:
+        rh.conv(x, torch.zeros(2, 2, 3, 3, device="cuda"))
+    assert e.value.kind == "IncompatibleInputShapes"
+    assert "does not match kernel input channels" in str(e.value)
+    with pytest.raises(rh.OpError) as e:
+        rh.conv(x, torch.zeros(2, 3, 5, 5, device="cuda"))
+    assert str(e.value) == "Input too small for kernel size" and e.value.kind == "InvalidValue"
+    with pytest.raises(rh.OpError) as e:
+        rh.conv(x, torch.zeros(2, 3, 3, 3, device="cuda"), strides=(0, 0))
+    assert str(e.value) == "Strides must be > 0"
+
+
+# --------------------------------------------------------------------------
+# Pooling / normalisation / elementwise
+# --------------------------------------------------------------------------
+
+def test_pooling_bitexact(rh, oracle):
+    x = rnd(oracle, 51, 2, 6, 17, 17)
+    assert_bits(host(rh.max_pool(dev(x), (3, 3), (2, 2), (1, 1, 1, 1))),
+                oracle.max_pool(x, (3, 3), (2, 2), (1, 1, 1, 1)), "maxpool")
+    for incl in (False, True):
+        assert_bits(host(rh.average_pool(dev(x), (3, 3), (2, 2), (1, 1, 1, 1), incl)),
+                    oracle.average_pool(x, (3, 3), (2, 2), (1, 1, 1, 1), incl), "avgpool")
+    assert_bits(host(rh.max_pool(dev(x), (2, 2), (2, 2), "same")),
+                oracle.max_pool(x, (2, 2), (2, 2), padding="same"), "maxpool same")
+    g = rnd(oracle, 52, 3, 37, 7, 7)
+    assert_bits(host(rh.global_average_pool(dev(g))), oracle.global_average_pool(g), "gap")
+
+
+def test_batch_norm_bitexact(rh, oracle):
+    x = rnd(oracle, 61, 2, 5, 6, 7)
+    sc, bi, mu = rnd(oracle, 62, 5), rnd(oracle, 63, 5), rnd(oracle, 64, 5)
+    var = oracle.xorshift(65, 5) + np.float32(0.5)
+    assert_bits(host(rh.batch_norm(dev(x), dev(sc), dev(bi), dev(mu), dev(var), 1e-5)),
+                oracle.batch_norm(x, sc, bi, mu, var, 1e-5), "batchnorm")
+
+
+@pytest.mark.parametrize("op", ["Relu", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu"])
+def test_unary_bitexact(rh, oracle, op):
+    x = rnd(oracle, 71, 40001, scale=24.0)
+    x[:8] = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-30, -1e-30, 104.0], np.float32)
+    assert_bits(host(rh.unary(op, dev(x))), oracle.unary(op, x), op)
+
+
+def test_clip_bitexact(rh, oracle):
+    x = rnd(oracle, 72, 1001, scale=20.0)
+    assert_bits(host(rh.clip(dev(x), 0.0, 6.0)), oracle.clip(x, 0.0, 6.0), "clip")
+
+
+@pytest.mark.parametrize("op", ["Add", "Sub", "Mul", "Div"])
+@pytest.mark.parametrize("shapes", [((2, 3, 4, 5), (2, 3, 4, 5)), ((2, 3, 4, 5), (5,)),
+                                    ((2, 3, 4, 5), (3, 1, 1)), ((2, 3, 4, 5), (1,)),
+                                    ((3, 1, 5), (2, 1, 4, 1)), ((32, 12, 128, 128), (32, 1, 1, 128))])
+def test_binary_bitexact(rh, oracle, op, shapes):
+    a = rnd(oracle, 81, *shapes[0])
+    b = rnd(oracle, 82, *shapes[1]) + np.float32(0.75)
+    assert_bits(host(rh.binary(op, dev(a), dev(b))), oracle.binary(op, a, b), f"{op} {shapes}")
+
+
+def test_binary_broadcast_error(rh):
+    import torch
+
+    with pytest.raises(rh.OpError) as e:
+        rh.add(torch.zeros(2, 3, device="cuda"), torch.zeros(4, device="cuda"))
+    assert e.value.kind == "IncompatibleInputShapes"
+
+
+@pytest.mark.parametrize("shape,axis", [((32, 12, 4, 128), -1), ((7, 300), 1), ((5, 6), 0),
+                                        ((3, 5000), -1), ((4, 1, 9), 2)])
+def test_softmax_bitexact(rh, oracle, shape, axis):
+    x = rnd(oracle, 91, *shape, scale=8.0)
+    assert_bits(host(rh.softmax(dev(x), axis)), oracle.softmax(x, axis), f"softmax {shape}")
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 768), (5, 2), (3, 7, 13)])
+def test_layer_norm_bitexact(rh, oracle, shape):
+    x = rnd(oracle, 92, *shape, scale=4.0)
+    sc = rnd(oracle, 93, shape[-1]) + np.float32(1.0)
+    bi = rnd(oracle, 94, shape[-1])
+    assert_bits(host(rh.layer_normalization(dev(x), dev(sc), dev(bi), -1, 1e-12)),
+                oracle.layer_norm(x, sc, bi, -1, 1e-12), f"layernorm {shape}")
+
+
+# --------------------------------------------------------------------------
+# Gemm / MatMul operators
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("batch", [64, 4, 1])
+def test_gemm_op_fc_bitexact(rh, oracle, batch):
+    """ResNet-50 FC: Gemm(transB=1) with broadcast bias C (matmul.rs:27-81)."""
+    a = rnd(oracle, 101, batch, 2048)
+    w = rnd(oracle, 102, 1000, 2048, scale=0.05)
+    c = rnd(oracle, 103, 1000)
+    exp = oracle.gemm_op(a, w, c, trans_b=True)
+    got = host(rh.gemm_op(dev(a), dev(w), dev(c), transpose_b=True))
+    assert_bits(got, exp, f"fc batch {batch}")
+
+
+@pytest.mark.parametrize("sa,sb", [((2, 3, 5, 64), (3, 64, 7)), ((4, 33, 70), (70, 9)),
+                                   ((2, 12, 128, 64), (2, 12, 64, 128)), ((6, 1, 40), (6, 40, 30))])
+def test_matmul_bitexact(rh, oracle, sa, sb):
+    a = rnd(oracle, 111, *sa)
+    b = rnd(oracle, 112, *sb)
+    assert_bits(host(rh.matmul(dev(a), dev(b))), oracle.matmul(a, b), f"matmul {sa}x{sb}")
+
+
+def test_matmul_fused_transpose_view(rh, oracle):
+    """QK^T with K^T as a strided view (FusedTranspose, src/ops/fused.rs:45-80)."""
+    q = rnd(oracle, 121, 2, 4, 128, 64)
+    k = rnd(oracle, 122, 2, 4, 128, 64)
+    exp = oracle.matmul(q, np.ascontiguousarray(np.swapaxes(k, -1, -2)))
+    got = host(rh.matmul(dev(q), dev(k).transpose(-1, -2)))
+    assert_bits(got, exp, "qk^T")
+
+
+# --------------------------------------------------------------------------
+# The reference's known-answer vectors, run on the GPU
+# --------------------------------------------------------------------------
+
+KATS = json.load(open(os.path.join(HERE, "golden", "kats.json")))
+
+
+def test_kats_on_gpu(rh):
+    for case in KATS["conv"]:
+        x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+        w = np.array(case["w"], np.float32).reshape(case["w_shape"])
+        b = dev(case["bias"]) if case["bias"] else None
+        y = host(rh.conv(dev(x), dev(w), b, padding=case["pads"], groups=case["groups"],
+                         strides=case["strides"], dilations=case["dilations"]))
+        exp = ([np.float32(p) + np.float32(q) for p, q in case["y_parts"]] if "y_parts" in case
+               else case["y"])
+        tol = 1e-4 if case["tol"] == "1e4" else 1e-5 * np.abs(np.array(exp)) + 1e-8
+        assert (np.abs(y.ravel() - np.array(exp, np.float32)) <= tol).all(), case["source"]
+    c = KATS["graph_conv_relu"]
+    y = host(rh.relu(rh.conv(dev(np.array(c["x"]).reshape(c["x_shape"])),
+                             dev(np.array(c["w"]).reshape(c["w_shape"])), padding=(1, 1, 1, 1))))
+    assert (np.abs(y.ravel() - np.array(c["y"], np.float32)) <= 1e-4).all()
+    for case in KATS["softmax"]:
+        x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+        if case.get("transpose_input"):
+            xt = dev(x).t()  # strided view, like the reference test's permute
+        else:
+            xt = dev(x)
+        y = host(rh.softmax(xt, case["axis"])).ravel()
+        exp = np.array(case["y"], np.float32)
+        if case["tol"] == "ulp0":
+            assert np.array_equal(y.view(np.uint32), exp.view(np.uint32)), case["source"]
+        else:
+            assert (np.abs(y - exp) <= 1e-4).all(), case["source"]
+    c = KATS["layer_norm"]
+    y = host(rh.layer_normalization(dev(np.array(c["x"]).reshape(c["x_shape"])), dev(c["scale"]),
+                                    dev(c["bias"]), c["axis"], c["epsilon"])).ravel()
+    assert (np.abs(y - np.array(c["y"], np.float32)) <= 1e-4).all()
+    for case in KATS["unary"]:
+        x = np.array([float(v) for v in case["x"]], np.float32)
+        y = host(rh.unary(case["op"], dev(x)))
+        exp = np.array([float(v) for v in case["y"]], np.float32)
+        m = ~np.isnan(exp)
+        assert np.array_equal(np.isnan(y), np.isnan(exp)), case["source"]
+        assert (np.abs(y[m] - exp[m]) <= 1e-8 + 1e-5 * np.abs(exp[m])).all(), case["source"]
+    c = KATS["global_average_pool"]
+    y = host(rh.global_average_pool(dev(np.array(c["x"], np.float32).reshape(c["x_shape"]))))
+    assert np.allclose(y.ravel(), c["y"])
+    for case in KATS["max_pool"][0]["cases"]:
+        x = np.array(KATS["max_pool"][0]["x"], np.float32).reshape(1, 1, 4, 4)
+        y = host(rh.max_pool(dev(x), case["kernel"], case["strides"]))
+        assert np.allclose(y.ravel(), case["y"])
