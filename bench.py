@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: ResNet-50 f32 inference throughput on MI355X (BASELINE.json).
+
+One step = one forward pass of ResNet-50 (f32, batch 64 per GPU, synthetic
+input resident in HBM) through the device graph executor
+(librten_hip.so: fused conv epilogues, hipGraph replay), plus — for N > 1 —
+the RCCL all-gather of every rank's [64, 1000] logits (the one exchange step
+of the batch-sharded path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  ``value`` = images/s of the whole job (all
+ranks' images / max-over-ranks wall time of the K timed steps).  The
+``roofline`` object prices the dominant kernel (the f32 MFMA implicit-GEMM
+engine, all Conv + Gemm launches) from per-launch hipEvent times taken on
+the executor's stream; ``cpu_baseline`` times the CPU oracle (RTen's
+algorithm restated in C++, "port") on a bounded batch-1 sample on the host.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rten-fork_amd"))
+
+F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense f32 matrix peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBPS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=64, help="images per GPU")
+    p.add_argument("--model", default="resnet50", choices=["resnet50", "mobilenet_v2"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--timing-report", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(spec, seconds: float):
+    """Time the CPU oracle (restated RTen CPU path) on ResNet-50 batch 1."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import graph_runner
+    import rten_oracle
+
+    x = np.random.default_rng(99).random((1, 3, 224, 224), dtype=np.float32)
+    graph_runner.run(spec, {"input": x})  # warm-up
+    times = []
+    t_end = time.time() + seconds
+    while time.time() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        graph_runner.run(spec, {"input": x})
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    import platform
+
+    cpu_model = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(1.0 / med, 3),
+        "unit": "images/s",
+        "cores": rten_oracle.num_threads(),
+        "kind": "port",
+        "sample": f"{spec.name} batch 1, {len(times)} runs in ~{seconds:.0f}s, median "
+                  f"{med * 1e3:.1f} ms; restated RTen algorithm (C++ BLIS 6x16 AVX2-FMA, "
+                  f"KC=256), not the Rust binary; host CPU: {cpu_model}",
+    }
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    import rten_hip
+    from rten_hip import models
+
+    ctx = rten_hip.Context(torch.cuda.current_device())
+    spec = models.resnet50() if args.model == "resnet50" else models.mobilenet_v2()
+    g = spec.to_graph(ctx)
+    B = args.batch
+    flops_per_img = models.conv_flops(spec, 1)
+    rng = np.random.default_rng(1234 + rank)
+    x = torch.from_numpy(rng.random((B, 3, 224, 224), dtype=np.float32)).cuda()
+    (out,) = g.run({g.input_ids[0]: x}, g.output_ids)
+    gathered = torch.empty((world * B, out.shape[1]), dtype=torch.float32, device=x.device)
+
+    def step():
+        g.run({g.input_ids[0]: x}, g.output_ids, out=[out])
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device=x.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    # Roofline of the dominant kernel: per-launch hipEvent times of every
+    # Conv/Gemm launch (the MFMA GEMM engine) on the executor's stream, over
+    # the same K steps run eagerly with timing on.
+    g.set_timing(True)
+    conv_ms = 0.0
+    report = ""
+    for _ in range(max(1, min(args.steps, 10))):
+        g.run({g.input_ids[0]: x}, g.output_ids, out=[out])
+        torch.cuda.synchronize()
+        report = g.timing_report()
+        for line in report.splitlines()[1:]:
+            name = line.split()[0]
+            if name.startswith("Conv") or name == "Gemm":
+                conv_ms += float(line.split()[1])
+    n_prof = max(1, min(args.steps, 10))
+    g.set_timing(False)
+    conv_ms /= n_prof
+    gemm_flops = flops_per_img * B
+    achieved = gemm_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+
+    if rank == 0:
+        line = {
+            "metric": "images/sec ResNet-50 f32 batch=64 per GPU" if args.model == "resnet50"
+                      else "images/sec MobileNetV2 f32",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U[0,1) images resident in HBM; seeded He-uniform weights)",
+            "config": {"workload": f"{spec.name} f32 batch={B} per GPU, 224x224 NCHW, BN folded "
+                                   f"(BASELINE.json configs[{1 if B == 64 and world == 1 else 4}])",
+                       "model": spec.name, "global_batch": world * B, "seq_len": None,
+                       "parallelism": f"batch-shard x{world} (replicated weights, RCCL all-gather of logits)"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
+                         "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "gemm_mfma_kernel (all Conv+Gemm launches)",
+                         "flops_per_step": gemm_flops,
+                         "kernel_ms_per_step": round(conv_ms, 4),
+                         "model_frac": round(value / world * flops_per_img / 1e12 /
+                                             F32_MFMA_PEAK_TFLOPS, 4)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
+        if args.timing_report:
+            sys.stderr.write(report + "\n")
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

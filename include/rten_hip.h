@@ -193,6 +193,10 @@ int32_t rtenhip_graph_add_constant(rtenhip_graph* g, const char* name, const flo
 int32_t rtenhip_graph_add_op(rtenhip_graph* g, const char* name, const char* op_type,
                              const char* attrs, const int32_t* inputs, int32_t n_inputs,
                              const int32_t* outputs, int32_t n_outputs);
+/* Declare the model's input / output value ids (Model::input_ids /
+ * output_ids, src/model.rs:616-632); outputs are never fused away. */
+rtenhip_status rtenhip_graph_set_io(rtenhip_graph* g, const int32_t* input_ids, int32_t n_inputs,
+                                    const int32_t* output_ids, int32_t n_outputs);
 /* Load-time optimisation: fuse Conv+Add+Relu/Clip epilogues and fold
  * Flatten/Reshape (metadata).  Numerics are unchanged (bit-identical). */
 rtenhip_status rtenhip_graph_optimize(rtenhip_graph* g);
@@ -203,6 +207,12 @@ rtenhip_status rtenhip_graph_run(rtenhip_graph* g, const int32_t* input_ids,
                                  const rtenhip_tensor* inputs, int32_t n_inputs,
                                  const int32_t* output_ids, rtenhip_tensor* outputs,
                                  int32_t n_outputs);
+/* Plan (or fetch the cached plan) and report the output shapes without
+ * running: shapes[i*RTENHIP_MAX_DIMS + d], ndims[i]. */
+rtenhip_status rtenhip_graph_plan(rtenhip_graph* g, const int32_t* input_ids,
+                                  const rtenhip_tensor* inputs, int32_t n_inputs,
+                                  const int32_t* output_ids, int32_t n_outputs, int64_t* shapes,
+                                  int32_t* ndims);
 /* Output shape of a value after the last run (or -1). */
 int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape);
 /* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled. */

@@ -1,0 +1,962 @@
+// Graph executor for the MI355X backend: restates Graph::run / run_plan
+// (src/graph.rs:733-1073) on the device.
+//
+//  - Planning (create_plan, graph.rs:1256-1345): DFS from the requested outputs
+//    to a topological op list; plans are cached per (inputs, outputs, input
+//    shapes) like get_cached_plan (graph.rs:768-795).
+//  - Memory (TensorPool + refcount frees, graph.rs:844-1037): shapes are
+//    inferred once per plan and every intermediate gets a fixed offset in one
+//    device arena (best-fit reuse of blocks freed when their refcount reaches
+//    zero; unary ops run in place on a sole-consumer input, graph.rs:897-931).
+//    Graph outputs are written straight into the caller's buffers.
+//  - Launch: the first run is eager; later runs replay a hipGraph captured on
+//    the executor's own stream (no per-op host launch cost).
+//  - Timing (RunOptions.timing / RTEN_TIMING, graph.rs:1039-1055): per-op
+//    hipEvent times aggregated by operator type.
+#include "graph.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <set>
+#include <sstream>
+
+namespace rtenhip {
+
+bool parse_attrs(const char* s, Attrs& out) {
+  if (!s) return true;
+  std::string str(s);
+  size_t pos = 0;
+  while (pos < str.size()) {
+    size_t end = str.find(';', pos);
+    if (end == std::string::npos) end = str.size();
+    std::string kv = str.substr(pos, end - pos);
+    pos = end + 1;
+    if (kv.empty()) continue;
+    size_t eq = kv.find('=');
+    if (eq == std::string::npos) return false;
+    std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+    std::vector<double> nums;
+    bool numeric = !v.empty();
+    size_t p = 0;
+    while (numeric && p <= v.size()) {
+      size_t c = v.find(',', p);
+      if (c == std::string::npos) c = v.size();
+      std::string tok = v.substr(p, c - p);
+      char* e = nullptr;
+      double d = strtod(tok.c_str(), &e);
+      if (tok.empty() || *e) numeric = false;
+      nums.push_back(d);
+      p = c + 1;
+    }
+    if (numeric)
+      out.nums[k] = nums;
+    else
+      out.strs[k] = v;
+  }
+  return true;
+}
+
+static int64_t prod(const Shape& s, size_t from = 0, size_t to = SIZE_MAX) {
+  int64_t n = 1;
+  for (size_t i = from; i < std::min(to, s.size()); i++) n *= s[i];
+  return n;
+}
+
+static rtenhip_tensor desc(float* p, const Shape& s) {
+  return make_tensor(p, s.data(), (int)s.size());
+}
+
+Graph::~Graph() {
+  for (auto& pl : plans)
+    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  for (auto& n : nodes)
+    if (n.kind == NodeKind::Constant && n.dev && n.owns_dev) (void)hipFree(n.dev);
+  if (arena) (void)hipFree(arena);
+  if (exec_stream) (void)hipStreamDestroy(exec_stream);
+  if (ev_in) (void)hipEventDestroy(ev_in);
+  if (ev_out) (void)hipEventDestroy(ev_out);
+}
+
+int Graph::add_node(Node n) {
+  int id = (int)nodes.size();
+  if (!n.name.empty()) by_name[n.name] = id;
+  nodes.push_back(std::move(n));
+  // Any structural change invalidates cached plans.
+  for (auto& pl : plans)
+    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  plans.clear();
+  return id;
+}
+
+// Constant scalar from a small host copy (Clip min/max, Reshape shape).
+static bool const_values(const Graph& g, int id, std::vector<float>& out) {
+  if (id < 0 || id >= (int)g.nodes.size()) return false;
+  const Node& n = g.nodes[id];
+  if (n.kind != NodeKind::Constant || n.host_small.empty()) return false;
+  out = n.host_small;
+  return true;
+}
+
+rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& ins,
+                                   std::vector<Shape>& outs) {
+  const Node& op = nodes[op_id];
+  const std::string& t = op.op_type;
+  auto in = [&](size_t i) -> const Shape* { return i < ins.size() ? ins[i] : nullptr; };
+  auto need = [&](size_t i) -> rtenhip_status {
+    if (!in(i)) return fail(RTENHIP_MISSING_INPUTS, "Missing required input");
+    return RTENHIP_OK;
+  };
+  outs.assign(std::max<size_t>(1, op.outputs.size()), Shape());
+  rtenhip_status st = need(0);
+  if (st) return st;
+  const Shape& x = *in(0);
+  if (t == "Conv") {
+    if ((st = need(1))) return st;
+    rtenhip_tensor xd = desc(nullptr, x), wd = desc(nullptr, *in(1));
+    std::string ap = op.attrs.str("auto_pad", "notset");
+    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+    auto pads = op.attrs.ints("pads", x.size() == 3 ? std::vector<int64_t>{0, 0}
+                                                     : std::vector<int64_t>{0, 0, 0, 0});
+    auto strides = op.attrs.ints("strides", x.size() == 3 ? std::vector<int64_t>{1}
+                                                           : std::vector<int64_t>{1, 1});
+    auto dil = op.attrs.ints("dilations", x.size() == 3 ? std::vector<int64_t>{1}
+                                                         : std::vector<int64_t>{1, 1});
+    int64_t os[4];
+    int32_t ond;
+    st = rtenhip_conv_output_shape(&xd, &wd, mode, pads.data(), strides.data(), dil.data(),
+                                   (int64_t)op.attrs.num("groups", 1), os, &ond);
+    if (st) return st;
+    outs[0].assign(os, os + ond);
+  } else if (t == "MaxPool" || t == "AveragePool") {
+    if (x.size() != 4) return fail(RTENHIP_INVALID_VALUE, "Expected input to have 4 dims");
+    auto k = op.attrs.ints("kernel_size", {1, 1});
+    auto s = op.attrs.ints("strides", {1, 1});
+    auto p = op.attrs.ints("pads", {0, 0, 0, 0});
+    std::string ap = op.attrs.str("auto_pad", "notset");
+    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+    int64_t ohw[2], fp[4];
+    st = output_size_and_padding(x[2], x[3], k[0], k[1], s[0], s[1], mode, p.data(), 1, 1, ohw, fp);
+    if (st) return st;
+    outs[0] = {x[0], x[1], ohw[0], ohw[1]};
+  } else if (t == "GlobalAveragePool") {
+    if (x.size() != 4) return fail(RTENHIP_INVALID_VALUE, "Expected input to have 4 dims");
+    outs[0] = {x[0], x[1], 1, 1};
+  } else if (t == "Gemm") {
+    if ((st = need(1))) return st;
+    const Shape& b = *in(1);
+    if (x.size() != 2 || b.size() != 2) return fail(RTENHIP_INVALID_VALUE, "Gemm inputs must be 2-D");
+    bool ta = op.attrs.num("transA", 0) != 0, tb = op.attrs.num("transB", 0) != 0;
+    outs[0] = {ta ? x[1] : x[0], tb ? b[0] : b[1]};
+  } else if (t == "MatMul") {
+    if ((st = need(1))) return st;
+    const Shape& b = *in(1);
+    if (x.size() < 2 || b.size() < 2) return fail(RTENHIP_INVALID_VALUE, "Inputs must have >= 2 dimensions");
+    int64_t pre[RTENHIP_MAX_DIMS];
+    int pn;
+    if (!broadcast_shapes(x.data(), (int)x.size() - 2, b.data(), (int)b.size() - 2, pre, &pn))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast shapes");
+    outs[0].assign(pre, pre + pn);
+    outs[0].push_back(x[x.size() - 2]);
+    outs[0].push_back(b[b.size() - 1]);
+  } else if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div") {
+    if ((st = need(1))) return st;
+    const Shape& b = *in(1);
+    int64_t os[RTENHIP_MAX_DIMS];
+    int on;
+    if (!broadcast_shapes(x.data(), (int)x.size(), b.data(), (int)b.size(), os, &on))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast inputs");
+    outs[0].assign(os, os + on);
+  } else if (t == "Flatten") {
+    int64_t axis = (int64_t)op.attrs.num("axis", 1);
+    if (axis < 0) axis += (int64_t)x.size();
+    if (axis < 0 || axis > (int64_t)x.size()) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+    outs[0] = {prod(x, 0, axis), prod(x, axis)};
+  } else if (t == "Reshape") {
+    std::vector<float> sv;
+    if (!const_values(*this, op.inputs.size() > 1 ? op.inputs[1] : -1, sv))
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Reshape needs a constant shape");
+    Shape s;
+    int infer = -1;
+    int64_t known = 1;
+    for (size_t i = 0; i < sv.size(); i++) {
+      int64_t d = (int64_t)sv[i];
+      if (d == 0 && op.attrs.num("allowzero", 0) == 0) d = i < x.size() ? x[i] : 0;
+      if (d == -1) {
+        infer = (int)i;
+        d = 1;
+      } else {
+        known *= d;
+      }
+      s.push_back(d);
+    }
+    if (infer >= 0) s[infer] = known ? prod(x) / known : 0;
+    if (prod(s) != prod(x)) return fail(RTENHIP_INVALID_VALUE, "Input and output sizes are incompatible");
+    outs[0] = s;
+  } else if (t == "Transpose") {
+    auto perm = op.attrs.ints("perm", {});
+    if (perm.empty())
+      for (int64_t i = (int64_t)x.size() - 1; i >= 0; i--) perm.push_back(i);
+    if (perm.size() != x.size()) return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
+    outs[0].clear();
+    for (auto p : perm) outs[0].push_back(x[p]);
+  } else {
+    // Shape-preserving ops: unary activations, BatchNormalization,
+    // LayerNormalization, Softmax, Identity.
+    static const std::set<std::string> same = {
+        "Relu", "Clip", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu", "BatchNormalization",
+        "LayerNormalization", "Softmax", "Identity"};
+    if (!same.count(t)) {
+      std::string msg = "Unsupported operator type: " + t;
+      set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
+      return RTENHIP_UNSUPPORTED_VALUE;
+    }
+    outs[0] = x;
+  }
+  return RTENHIP_OK;
+}
+
+static bool is_unary(const std::string& t) {
+  return t == "Relu" || t == "Clip" || t == "Gelu" || t == "Erf" || t == "Sigmoid" ||
+         t == "Tanh" || t == "Exp" || t == "Silu";
+}
+
+rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vector<Shape>& in_shapes,
+                                const std::vector<int>& out_ids, Plan& p) {
+  p.input_ids = in_ids;
+  p.output_ids = out_ids;
+  p.input_shapes = in_shapes;
+  // Producer of each value.
+  std::map<int, int> producer;
+  for (int i = 0; i < (int)nodes.size(); i++)
+    if (nodes[i].kind == NodeKind::Operator && !nodes[i].removed)
+      for (int o : nodes[i].outputs) producer[o] = i;
+  std::set<int> available(in_ids.begin(), in_ids.end());
+  // create_plan: DFS from outputs, inputs before consumers.
+  std::set<int> visited;
+  std::function<rtenhip_status(int)> visit_value = [&](int v) -> rtenhip_status {
+    if (v < 0) return RTENHIP_OK;
+    if (available.count(v) || nodes[v].kind == NodeKind::Constant) return RTENHIP_OK;
+    auto it = producer.find(v);
+    if (it == producer.end()) {
+      std::string msg = "Missing input \"" + nodes[v].name + "\"";
+      set_error(RTENHIP_MISSING_INPUTS, msg);
+      return RTENHIP_MISSING_INPUTS;
+    }
+    int op = it->second;
+    if (visited.count(op)) return RTENHIP_OK;
+    visited.insert(op);
+    for (int i : nodes[op].inputs) {
+      rtenhip_status st = visit_value(i);
+      if (st) return st;
+    }
+    if (nodes[op].fused_residual >= 0) {
+      rtenhip_status st = visit_value(nodes[op].fused_residual);
+      if (st) return st;
+    }
+    p.ops.push_back(op);
+    return RTENHIP_OK;
+  };
+  for (int o : out_ids) {
+    rtenhip_status st = visit_value(o);
+    if (st) return st;
+  }
+
+  // Shapes.
+  std::map<int, Shape> shapes;
+  for (size_t i = 0; i < in_ids.size(); i++) shapes[in_ids[i]] = in_shapes[i];
+  auto shape_of = [&](int v) -> const Shape* {
+    if (v < 0) return nullptr;
+    if (nodes[v].kind == NodeKind::Constant) return &nodes[v].shape;
+    auto it = shapes.find(v);
+    return it == shapes.end() ? nullptr : &it->second;
+  };
+  for (int op : p.ops) {
+    std::vector<const Shape*> ins;
+    for (int i : nodes[op].inputs) ins.push_back(shape_of(i));
+    std::vector<Shape> outs;
+    rtenhip_status st = infer_shapes(op, ins, outs);
+    if (st) {
+      std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
+      set_error(st, msg);
+      return st;
+    }
+    for (size_t k = 0; k < nodes[op].outputs.size(); k++) shapes[nodes[op].outputs[k]] = outs[k];
+  }
+
+  // Refcounts over the plan (graph.rs:844-862), counting fused residuals.
+  std::map<int, int> uses;
+  for (int op : p.ops) {
+    for (int i : nodes[op].inputs)
+      if (i >= 0) uses[i]++;
+    if (nodes[op].fused_residual >= 0) uses[nodes[op].fused_residual]++;
+  }
+  std::set<int> outset(out_ids.begin(), out_ids.end());
+
+  // Storage blocks with best-fit reuse; aliases share their base's block.
+  struct Block {
+    size_t off, size;
+    int refs;
+  };
+  std::vector<Block> blocks;
+  std::map<int, int> block_of;  // value -> block index (arena values only)
+  std::vector<std::pair<size_t, size_t>> free_list;  // (off, size)
+  size_t top = 0;
+  auto alloc = [&](size_t bytes) -> size_t {
+    bytes = (bytes + 255) & ~size_t(255);
+    if (bytes == 0) bytes = 256;
+    int best = -1;
+    for (int i = 0; i < (int)free_list.size(); i++)
+      if (free_list[i].second >= bytes && (best < 0 || free_list[i].second < free_list[best].second))
+        best = i;
+    if (best >= 0) {
+      size_t off = free_list[best].first;
+      if (free_list[best].second == bytes)
+        free_list.erase(free_list.begin() + best);
+      else {
+        free_list[best].first += bytes;
+        free_list[best].second -= bytes;
+      }
+      return off;
+    }
+    size_t off = top;
+    top += bytes;
+    return off;
+  };
+  auto release = [&](size_t off, size_t bytes) {
+    bytes = (bytes + 255) & ~size_t(255);
+    if (bytes == 0) bytes = 256;
+    free_list.push_back({off, bytes});
+    std::sort(free_list.begin(), free_list.end());
+    std::vector<std::pair<size_t, size_t>> merged;
+    for (auto& f : free_list) {
+      if (!merged.empty() && merged.back().first + merged.back().second == f.first)
+        merged.back().second += f.second;
+      else
+        merged.push_back(f);
+    }
+    free_list = merged;
+  };
+  auto drop_use = [&](int v) {
+    auto it = block_of.find(v);
+    if (it == block_of.end()) return;
+    Block& b = blocks[it->second];
+    if (--b.refs == 0) release(b.off, b.size);
+  };
+
+  for (int op : p.ops) {
+    Node& n = nodes[op];
+    int out = n.outputs.empty() ? -1 : n.outputs[0];
+    const Shape& os = shapes[out];
+    size_t bytes = (size_t)prod(os) * sizeof(float);
+    Slot s;
+    s.shape = os;
+    bool alias = n.op_type == "Flatten" || n.op_type == "Reshape" || n.op_type == "Identity";
+    n.alias_input0 = alias;
+    int in0 = n.inputs.empty() ? -1 : n.inputs[0];
+    if (outset.count(out)) {
+      // Written straight into the caller's buffer (aliases copy into it).
+      s.ext = nullptr;
+      p.slots[out] = s;
+    } else if (alias && block_of.count(in0)) {
+      Block& b = blocks[block_of[in0]];
+      b.refs += uses[out];
+      block_of[out] = block_of[in0];
+      s.offset = b.off;
+      p.slots[out] = s;
+    } else if (alias) {
+      // Alias of an input/constant: share its pointer at run time.
+      s.offset = SIZE_MAX;
+      p.slots[out] = s;
+    } else if (is_unary(n.op_type) && block_of.count(in0) && blocks[block_of[in0]].refs == 1 &&
+               blocks[block_of[in0]].size >= ((bytes + 255) & ~size_t(255))) {
+      // In place on the sole remaining consumer (graph.rs:897-931).
+      Block& b = blocks[block_of[in0]];
+      b.refs += uses[out];
+      block_of[out] = block_of[in0];
+      s.offset = b.off;
+      p.slots[out] = s;
+    } else {
+      size_t off = alloc(bytes);
+      blocks.push_back({off, bytes, uses[out]});
+      block_of[out] = (int)blocks.size() - 1;
+      s.offset = off;
+      p.slots[out] = s;
+    }
+    for (int i : n.inputs)
+      if (i >= 0) drop_use(i);
+    if (n.fused_residual >= 0) drop_use(n.fused_residual);
+    // An output nobody reads is released right after its producer.
+    if (block_of.count(out) && blocks[block_of[out]].refs == 0) {
+      Block& b = blocks[block_of[out]];
+      b.refs = -1;
+      release(b.off, b.size);
+    }
+    if (n.fused_residual >= 0) {
+      const Shape* rs = shape_of(n.fused_residual);
+      if (!rs || *rs != os)
+        return fail(RTENHIP_UNSUPPORTED_VALUE, "Fused residual must match the Conv output shape");
+    }
+  }
+  p.arena_bytes = top;
+  return RTENHIP_OK;
+}
+
+float* Graph::ptr_of(Plan& p, int v) {
+  if (v < 0) return nullptr;
+  const Node& n = nodes[v];
+  if (n.kind == NodeKind::Constant) return n.dev;
+  for (size_t i = 0; i < p.input_ids.size(); i++)
+    if (p.input_ids[i] == v) return p.bound_in[i];
+  for (size_t i = 0; i < p.output_ids.size(); i++)
+    if (p.output_ids[i] == v) return p.bound_out[i];
+  auto it = p.slots.find(v);
+  if (it == p.slots.end()) return nullptr;
+  if (it->second.offset == SIZE_MAX) {
+    // alias of an input / constant: find the producer's input 0
+    for (int op : p.ops)
+      if (!nodes[op].outputs.empty() && nodes[op].outputs[0] == v) return ptr_of(p, nodes[op].inputs[0]);
+    return nullptr;
+  }
+  return reinterpret_cast<float*>(static_cast<char*>(arena) + it->second.offset);
+}
+
+static const Shape* plan_shape(Graph& g, Plan& p, int v) {
+  if (v < 0) return nullptr;
+  if (g.nodes[v].kind == NodeKind::Constant) return &g.nodes[v].shape;
+  for (size_t i = 0; i < p.input_ids.size(); i++)
+    if (p.input_ids[i] == v) return &p.input_shapes[i];
+  auto it = p.slots.find(v);
+  return it == p.slots.end() ? nullptr : &it->second.shape;
+}
+
+rtenhip_status Graph::exec_op(Plan& p, int op_id) {
+  Node& n = nodes[op_id];
+  const std::string& t = n.op_type;
+  auto T = [&](int v) -> rtenhip_tensor {
+    const Shape* s = plan_shape(*this, p, v);
+    return desc(ptr_of(p, v), s ? *s : Shape());
+  };
+  auto P = [&](size_t i) -> float* { return i < n.inputs.size() ? ptr_of(p, n.inputs[i]) : nullptr; };
+  int out = n.outputs[0];
+  rtenhip_tensor y = T(out);
+  rtenhip_tensor x = T(n.inputs[0]);
+  rtenhip_ctx* c = cptr;
+  if (n.alias_input0) {
+    // Flatten / Reshape / Identity are views; copy only when the output is
+    // a caller buffer.
+    if (y.data != x.data && y.data)
+      RTENHIP_HIP_CHECK(hipMemcpyAsync(y.data, x.data, (size_t)numel(y) * 4,
+                                       hipMemcpyDeviceToDevice, ctx->stream));
+    return RTENHIP_OK;
+  }
+  if (t == "Conv") {
+    rtenhip_tensor w = T(n.inputs[1]);
+    std::string ap = n.attrs.str("auto_pad", "notset");
+    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+    bool one_d = x.ndim == 3;
+    auto pads = n.attrs.ints("pads", one_d ? std::vector<int64_t>{0, 0} : std::vector<int64_t>{0, 0, 0, 0});
+    auto strides = n.attrs.ints("strides", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
+    auto dil = n.attrs.ints("dilations", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
+    return conv_impl(ctx, &x, &w, P(2), mode, pads.data(), strides.data(), dil.data(),
+                     (int64_t)n.attrs.num("groups", 1), ptr_of(p, n.fused_residual), n.fused_act,
+                     n.act_lo, n.act_hi, &y);
+  }
+  if (is_unary(t)) {
+    int op = t == "Relu" ? RTENHIP_UNARY_RELU : t == "Clip" ? RTENHIP_UNARY_CLIP
+           : t == "Gelu" ? RTENHIP_UNARY_GELU : t == "Erf" ? RTENHIP_UNARY_ERF
+           : t == "Sigmoid" ? RTENHIP_UNARY_SIGMOID : t == "Tanh" ? RTENHIP_UNARY_TANH
+           : t == "Exp" ? RTENHIP_UNARY_EXP : RTENHIP_UNARY_SILU;
+    float lo = -3.40282347e38f, hi = 3.40282347e38f;
+    if (op == RTENHIP_UNARY_CLIP) {
+      std::vector<float> v;
+      if (n.inputs.size() > 1 && const_values(*this, n.inputs[1], v)) lo = v[0];
+      if (n.inputs.size() > 2 && const_values(*this, n.inputs[2], v)) hi = v[0];
+      lo = (float)n.attrs.num("min", lo);
+      hi = (float)n.attrs.num("max", hi);
+    }
+    return rtenhip_unary_f32(c, op, &x, lo, hi, &y);
+  }
+  if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div") {
+    rtenhip_tensor b = T(n.inputs[1]);
+    int op = t == "Add" ? RTENHIP_BINARY_ADD : t == "Sub" ? RTENHIP_BINARY_SUB
+           : t == "Mul" ? RTENHIP_BINARY_MUL : RTENHIP_BINARY_DIV;
+    // Commutative ops run with the larger operand first (graph.rs:897-931);
+    // a+b == b+a bitwise, so only the fast broadcast path changes.
+    bool swap = (op == RTENHIP_BINARY_ADD || op == RTENHIP_BINARY_MUL) && numel(b) > numel(x);
+    return swap ? rtenhip_binary_f32(c, op, &b, &x, &y) : rtenhip_binary_f32(c, op, &x, &b, &y);
+  }
+  if (t == "MaxPool" || t == "AveragePool") {
+    auto k = n.attrs.ints("kernel_size", {1, 1});
+    auto s = n.attrs.ints("strides", {1, 1});
+    auto pads = n.attrs.ints("pads", {0, 0, 0, 0});
+    std::string ap = n.attrs.str("auto_pad", "notset");
+    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+    if (t == "MaxPool") return rtenhip_max_pool_f32(c, &x, k.data(), s.data(), mode, pads.data(), &y);
+    return rtenhip_average_pool_f32(c, &x, k.data(), s.data(), mode, pads.data(),
+                                    (int)n.attrs.num("count_include_pad", 0), &y);
+  }
+  if (t == "GlobalAveragePool") return rtenhip_global_average_pool_f32(c, &x, &y);
+  if (t == "Gemm") {
+    rtenhip_tensor b = T(n.inputs[1]);
+    rtenhip_tensor cc{};
+    bool has_c = n.inputs.size() > 2 && n.inputs[2] >= 0;
+    if (has_c) cc = T(n.inputs[2]);
+    return rtenhip_gemm_op_f32(c, &x, &b, has_c ? &cc : nullptr, (float)n.attrs.num("alpha", 1.0),
+                               (float)n.attrs.num("beta", 1.0), (int)n.attrs.num("transA", 0),
+                               (int)n.attrs.num("transB", 0), &y);
+  }
+  if (t == "MatMul") {
+    rtenhip_tensor b = T(n.inputs[1]);
+    return rtenhip_matmul_f32(c, &x, &b, &y);
+  }
+  if (t == "BatchNormalization") {
+    return rtenhip_batch_norm_f32(c, &x, P(1), P(2), P(3), P(4), (float)n.attrs.num("epsilon", 1e-5), &y);
+  }
+  if (t == "LayerNormalization") {
+    rtenhip_tensor sc = T(n.inputs[1]);
+    rtenhip_tensor bi{};
+    bool has_b = n.inputs.size() > 2 && n.inputs[2] >= 0;
+    if (has_b) bi = T(n.inputs[2]);
+    return rtenhip_layer_norm_f32(c, &x, &sc, has_b ? &bi : nullptr, (int64_t)n.attrs.num("axis", -1),
+                                  (float)n.attrs.num("epsilon", 1e-5), &y);
+  }
+  if (t == "Softmax") return rtenhip_softmax_f32(c, &x, (int64_t)n.attrs.num("axis", -1), &y);
+  if (t == "Transpose") {
+    auto perm = n.attrs.ints("perm", {});
+    if (perm.empty())
+      for (int64_t i = x.ndim - 1; i >= 0; i--) perm.push_back(i);
+    rtenhip_tensor v = x;
+    for (int i = 0; i < x.ndim; i++) {
+      v.shape[i] = x.shape[perm[i]];
+      v.strides[i] = x.strides[perm[i]];
+    }
+    return launch_copy_strided(v, y.data, ctx->stream);
+  }
+  std::string msg = "Unsupported operator type: " + t;
+  set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
+  return RTENHIP_UNSUPPORTED_VALUE;
+}
+
+rtenhip_status Graph::find_plan(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
+                                const int32_t* out_ids, int n_out, Plan** out) {
+  std::vector<int> iv(in_ids, in_ids + n_in), ov(out_ids, out_ids + n_out);
+  std::vector<Shape> ishapes;
+  for (int i = 0; i < n_in; i++) {
+    if (iv[i] < 0 || iv[i] >= (int)nodes.size()) return fail(RTENHIP_INVALID_VALUE, "Invalid input id");
+    if (!is_contiguous(ins[i])) return fail(RTENHIP_UNSUPPORTED_VALUE, "Graph inputs must be contiguous");
+    ishapes.emplace_back(ins[i].shape, ins[i].shape + ins[i].ndim);
+  }
+  for (int o : ov)
+    if (o < 0 || o >= (int)nodes.size()) return fail(RTENHIP_INVALID_VALUE, "Invalid output id");
+  for (auto& pl : plans)
+    if (pl->input_ids == iv && pl->output_ids == ov && pl->input_shapes == ishapes) {
+      *out = pl.get();
+      return RTENHIP_OK;
+    }
+  auto np = std::make_unique<Plan>();
+  rtenhip_status st = make_plan(iv, ishapes, ov, *np);
+  if (st) return st;
+  plans.push_back(std::move(np));
+  *out = plans.back().get();
+  return RTENHIP_OK;
+}
+
+rtenhip_status Graph::plan_shapes(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
+                                  const int32_t* out_ids, int n_out, int64_t* shapes,
+                                  int32_t* ndims) {
+  Plan* plan = nullptr;
+  rtenhip_status st = find_plan(in_ids, ins, n_in, out_ids, n_out, &plan);
+  if (st) return st;
+  for (int i = 0; i < n_out; i++) {
+    const Shape* s = nullptr;
+    if (nodes[out_ids[i]].kind == NodeKind::Constant) s = &nodes[out_ids[i]].shape;
+    for (int k = 0; !s && k < n_in; k++)
+      if (in_ids[k] == out_ids[i]) s = &plan->input_shapes[k];
+    if (!s) s = &plan->slots[out_ids[i]].shape;
+    ndims[i] = (int32_t)s->size();
+    for (size_t d = 0; d < s->size(); d++) shapes[i * RTENHIP_MAX_DIMS + d] = (*s)[d];
+  }
+  return RTENHIP_OK;
+}
+
+rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
+                          const int32_t* out_ids, rtenhip_tensor* outs, int n_out) {
+  Plan* plan = nullptr;
+  {
+    rtenhip_status st = find_plan(in_ids, ins, n_in, out_ids, n_out, &plan);
+    if (st) return st;
+  }
+  std::vector<int> ov(out_ids, out_ids + n_out);
+  // Check the caller's output buffers (RunError::OutputMismatch).
+  for (int i = 0; i < n_out; i++) {
+    const Shape& s = plan->slots[ov[i]].shape;
+    if (outs[i].ndim != (int)s.size() || !is_contiguous(outs[i]))
+      return fail(RTENHIP_INCORRECT_OUTPUT_TYPE, "Output buffer has the wrong shape");
+    for (size_t d = 0; d < s.size(); d++)
+      if (outs[i].shape[d] != s[d]) return fail(RTENHIP_INCORRECT_OUTPUT_TYPE, "Output buffer has the wrong shape");
+  }
+  hipStream_t caller = ctx->stream;
+  if (!exec_stream) {
+    RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&exec_stream, hipStreamNonBlocking));
+    RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
+    RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
+  }
+  if (plan->arena_bytes > arena_cap) {
+    RTENHIP_HIP_CHECK(hipStreamSynchronize(caller));
+    RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
+    for (auto& pl : plans)
+      if (pl->exec) {
+        (void)hipGraphExecDestroy(pl->exec);
+        pl->exec = nullptr;
+      }
+    if (arena) RTENHIP_HIP_CHECK(hipFree(arena));
+    arena = nullptr;
+    RTENHIP_HIP_CHECK(hipMalloc(&arena, plan->arena_bytes));
+    arena_cap = plan->arena_bytes;
+  }
+  std::vector<float*> bin, bout;
+  for (int i = 0; i < n_in; i++) bin.push_back(ins[i].data);
+  for (int i = 0; i < n_out; i++) bout.push_back(outs[i].data);
+  bool same_binding = plan->exec && bin == plan->bound_in && bout == plan->bound_out;
+  plan->bound_in = bin;
+  plan->bound_out = bout;
+
+  RTENHIP_HIP_CHECK(hipEventRecord(ev_in, caller));
+  RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, ev_in, 0));
+  ctx->stream = exec_stream;
+  rtenhip_status st = RTENHIP_OK;
+  const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
+  if (replay) {
+    if (!same_binding) {
+      if (plan->exec) {
+        (void)hipGraphExecDestroy(plan->exec);
+        plan->exec = nullptr;
+      }
+      hipGraph_t g = nullptr;
+      hipError_t e = hipStreamBeginCapture(exec_stream, hipStreamCaptureModeThreadLocal);
+      if (e == hipSuccess) {
+        for (int op : plan->ops) {
+          st = exec_op(*plan, op);
+          if (st) break;
+        }
+        hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
+        if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&plan->exec, g, nullptr, nullptr, 0);
+        if (g) (void)hipGraphDestroy(g);
+        if (!st && e2 != hipSuccess) st = hip_fail(e2, "hipGraph capture");
+      } else {
+        st = hip_fail(e, "hipStreamBeginCapture");
+      }
+    }
+    if (!st) {
+      hipError_t e = hipGraphLaunch(plan->exec, exec_stream);
+      if (e != hipSuccess) st = hip_fail(e, "hipGraphLaunch");
+    }
+  } else {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    for (int op : plan->ops) {
+      hipEvent_t a = nullptr, b = nullptr;
+      if (timing) {
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        (void)hipEventRecord(a, exec_stream);
+      }
+      st = exec_op(*plan, op);
+      if (timing) {
+        (void)hipEventRecord(b, exec_stream);
+        evs.push_back({a, b});
+      }
+      if (st) {
+        std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
+        set_error(st, msg);
+        break;
+      }
+    }
+    plan->eager_runs++;
+    if (timing && !st) {
+      (void)hipStreamSynchronize(exec_stream);
+      std::map<std::string, std::pair<double, int>> tot;
+      double total = 0;
+      for (size_t i = 0; i < evs.size(); i++) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
+        const Node& n = nodes[plan->ops[i]];
+        std::string key = n.op_type;
+        if (n.op_type == "Conv" && (n.fused_residual >= 0 || n.fused_act)) key = "Conv(fused)";
+        tot[key].first += ms;
+        tot[key].second++;
+        total += ms;
+      }
+      for (auto& e : evs) {
+        (void)hipEventDestroy(e.first);
+        (void)hipEventDestroy(e.second);
+      }
+      std::vector<std::pair<double, std::string>> rows;
+      for (auto& kv : tot) rows.push_back({kv.second.first, kv.first});
+      std::sort(rows.rbegin(), rows.rend());
+      std::ostringstream os;
+      char buf[256];
+      snprintf(buf, sizeof buf, "Graph run of %zu ops finished in %.3f ms (device time)\n",
+               plan->ops.size(), total);
+      os << buf;
+      for (auto& r : rows) {
+        snprintf(buf, sizeof buf, "%-22s %10.3f ms (%5.2f%%)  x%d\n", r.second.c_str(), r.first,
+                 total > 0 ? 100.0 * r.first / total : 0.0, tot[r.second].second);
+        os << buf;
+      }
+      timing_report = os.str();
+    }
+  }
+  ctx->stream = caller;
+  RTENHIP_HIP_CHECK(hipEventRecord(ev_out, exec_stream));
+  RTENHIP_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
+  return st;
+}
+
+// Load-time fusion (cf. GraphOptimizer, src/optimize.rs:286-297, which fuses
+// only activations; here Conv epilogues are fused too).  Conv -> Add(other)
+// -> Relu|Clip and Conv -> Relu|Clip collapse into the Conv node when each
+// intermediate value has exactly one consumer.  Results are bit-identical:
+// the epilogue applies the same f32 add and max/clamp to the same values.
+rtenhip_status Graph::optimize() {
+  std::map<int, std::vector<int>> consumers;
+  for (int i = 0; i < (int)nodes.size(); i++)
+    if (nodes[i].kind == NodeKind::Operator && !nodes[i].removed)
+      for (int v : nodes[i].inputs)
+        if (v >= 0) consumers[v].push_back(i);
+  std::set<int> outputs(model_outputs.begin(), model_outputs.end());
+  auto sole = [&](int v) -> int {
+    if (outputs.count(v)) return -1;
+    auto it = consumers.find(v);
+    if (it == consumers.end() || it->second.size() != 1) return -1;
+    return it->second[0];
+  };
+  auto act_of = [&](int op, int& act, float& lo, float& hi) -> bool {
+    Node& n = nodes[op];
+    if (n.op_type == "Relu") {
+      act = RTENHIP_ACT_RELU;
+      return true;
+    }
+    if (n.op_type == "Clip") {
+      std::vector<float> v;
+      lo = -3.40282347e38f;
+      hi = 3.40282347e38f;
+      if (n.inputs.size() > 1 && n.inputs[1] >= 0) {
+        if (!const_values(*this, n.inputs[1], v)) return false;
+        lo = v[0];
+      }
+      if (n.inputs.size() > 2 && n.inputs[2] >= 0) {
+        if (!const_values(*this, n.inputs[2], v)) return false;
+        hi = v[0];
+      }
+      lo = (float)n.attrs.num("min", lo);
+      hi = (float)n.attrs.num("max", hi);
+      act = RTENHIP_ACT_CLIP;
+      return true;
+    }
+    return false;
+  };
+  int fused = 0;
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& conv = nodes[i];
+    if (conv.kind != NodeKind::Operator || conv.removed || conv.op_type != "Conv") continue;
+    if (conv.outputs.size() != 1 || conv.fused_act || conv.fused_residual >= 0) continue;
+    int v = conv.outputs[0];
+    int nxt = sole(v);
+    if (nxt < 0 || nodes[nxt].removed) continue;
+    Node& a = nodes[nxt];
+    if (a.op_type == "Add" && a.inputs.size() == 2 && a.outputs.size() == 1) {
+      int other = a.inputs[0] == v ? a.inputs[1] : a.inputs[0];
+      if (other == v) continue;
+      // Residual must have the conv output's shape: checked at plan time by
+      // the broadcast rules; require non-constant same-rank value here.
+      conv.fused_residual = other;
+      a.removed = true;
+      int out = a.outputs[0];
+      conv.outputs[0] = out;
+      fused++;
+      int nn = sole(out);
+      int act;
+      float lo, hi;
+      if (nn >= 0 && !nodes[nn].removed && act_of(nn, act, lo, hi)) {
+        conv.fused_act = act;
+        conv.act_lo = lo;
+        conv.act_hi = hi;
+        nodes[nn].removed = true;
+        conv.outputs[0] = nodes[nn].outputs[0];
+        fused++;
+      }
+      continue;
+    }
+    int act;
+    float lo, hi;
+    if (act_of(nxt, act, lo, hi)) {
+      conv.fused_act = act;
+      conv.act_lo = lo;
+      conv.act_hi = hi;
+      a.removed = true;
+      conv.outputs[0] = a.outputs[0];
+      fused++;
+    }
+  }
+  for (auto& pl : plans)
+    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  plans.clear();
+  (void)fused;
+  return RTENHIP_OK;
+}
+
+}  // namespace rtenhip
+
+using namespace rtenhip;
+
+static Graph* G_(rtenhip_graph* g) { return reinterpret_cast<Graph*>(g); }
+
+extern "C" {
+
+rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
+  Graph* g = new Graph();
+  g->ctx = reinterpret_cast<Ctx*>(ctx);
+  g->cptr = ctx;
+  if (const char* s = getenv("RTEN_TIMING")) g->timing = s[0] != 0 && s[0] != '0';
+  if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
+  return reinterpret_cast<rtenhip_graph*>(g);
+}
+
+void rtenhip_graph_destroy(rtenhip_graph* g) { delete G_(g); }
+
+int32_t rtenhip_graph_add_value(rtenhip_graph* g, const char* name) {
+  Node n;
+  n.kind = NodeKind::Value;
+  n.name = name ? name : "";
+  return G_(g)->add_node(std::move(n));
+}
+
+int32_t rtenhip_graph_add_constant(rtenhip_graph* g, const char* name, const float* host_data,
+                                   const int64_t* shape, int32_t ndim) {
+  Node n;
+  n.kind = NodeKind::Constant;
+  n.name = name ? name : "";
+  n.shape.assign(shape, shape + ndim);
+  size_t count = (size_t)prod(n.shape);
+  if (hipMalloc(&n.dev, std::max<size_t>(4, count * 4)) != hipSuccess) {
+    set_error(RTENHIP_HIP_ERROR, "hipMalloc failed for constant");
+    return -1;
+  }
+  if (count && hipMemcpy(n.dev, host_data, count * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    set_error(RTENHIP_HIP_ERROR, "hipMemcpy failed for constant");
+    (void)hipFree(n.dev);
+    return -1;
+  }
+  if (count <= 64) n.host_small.assign(host_data, host_data + count);
+  return G_(g)->add_node(std::move(n));
+}
+
+int32_t rtenhip_graph_add_op(rtenhip_graph* g, const char* name, const char* op_type,
+                             const char* attrs, const int32_t* inputs, int32_t n_inputs,
+                             const int32_t* outputs, int32_t n_outputs) {
+  Graph* G = G_(g);
+  Node n;
+  n.kind = NodeKind::Operator;
+  n.name = name ? name : "";
+  n.op_type = op_type ? op_type : "";
+  if (!parse_attrs(attrs, n.attrs)) {
+    set_error(RTENHIP_INVALID_VALUE, "Malformed attribute string");
+    return -1;
+  }
+  for (int i = 0; i < n_inputs; i++) {
+    if (inputs[i] >= (int)G->nodes.size()) {
+      set_error(RTENHIP_INVALID_VALUE, "Invalid input id");
+      return -1;
+    }
+    n.inputs.push_back(inputs[i]);
+  }
+  for (int i = 0; i < n_outputs; i++) {
+    if (outputs[i] < 0 || outputs[i] >= (int)G->nodes.size() ||
+        G->nodes[outputs[i]].kind != NodeKind::Value) {
+      set_error(RTENHIP_INVALID_VALUE, "Invalid output id");
+      return -1;
+    }
+    n.outputs.push_back(outputs[i]);
+  }
+  if (n.outputs.empty()) {
+    set_error(RTENHIP_INVALID_VALUE, "Operator has no outputs");
+    return -1;
+  }
+  return G->add_node(std::move(n));
+}
+
+rtenhip_status rtenhip_graph_optimize(rtenhip_graph* g) { return G_(g)->optimize(); }
+
+rtenhip_status rtenhip_graph_set_io(rtenhip_graph* g, const int32_t* input_ids, int32_t n_inputs,
+                                    const int32_t* output_ids, int32_t n_outputs) {
+  Graph* G = G_(g);
+  for (int i = 0; i < n_inputs; i++)
+    if (input_ids[i] < 0 || input_ids[i] >= (int)G->nodes.size())
+      return fail(RTENHIP_INVALID_VALUE, "Invalid input id");
+  for (int i = 0; i < n_outputs; i++)
+    if (output_ids[i] < 0 || output_ids[i] >= (int)G->nodes.size())
+      return fail(RTENHIP_INVALID_VALUE, "Invalid output id");
+  G->model_inputs.assign(input_ids, input_ids + n_inputs);
+  G->model_outputs.assign(output_ids, output_ids + n_outputs);
+  return RTENHIP_OK;
+}
+
+rtenhip_status rtenhip_graph_plan(rtenhip_graph* g, const int32_t* input_ids,
+                                  const rtenhip_tensor* inputs, int32_t n_inputs,
+                                  const int32_t* output_ids, int32_t n_outputs, int64_t* shapes,
+                                  int32_t* ndims) {
+  return G_(g)->plan_shapes(input_ids, inputs, n_inputs, output_ids, n_outputs, shapes, ndims);
+}
+
+rtenhip_status rtenhip_graph_run(rtenhip_graph* g, const int32_t* input_ids,
+                                 const rtenhip_tensor* inputs, int32_t n_inputs,
+                                 const int32_t* output_ids, rtenhip_tensor* outputs,
+                                 int32_t n_outputs) {
+  return G_(g)->run(input_ids, inputs, n_inputs, output_ids, outputs, n_outputs);
+}
+
+int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape) {
+  Graph* G = G_(g);
+  if (id < 0 || id >= (int)G->nodes.size()) return -1;
+  if (G->nodes[id].kind == NodeKind::Constant) {
+    for (size_t i = 0; i < G->nodes[id].shape.size(); i++) shape[i] = G->nodes[id].shape[i];
+    return (int32_t)G->nodes[id].shape.size();
+  }
+  for (auto it = G->plans.rbegin(); it != G->plans.rend(); ++it) {
+    auto s = (*it)->slots.find(id);
+    if (s != (*it)->slots.end()) {
+      for (size_t i = 0; i < s->second.shape.size(); i++) shape[i] = s->second.shape[i];
+      return (int32_t)s->second.shape.size();
+    }
+  }
+  return -1;
+}
+
+rtenhip_status rtenhip_graph_set_timing(rtenhip_graph* g, int enabled) {
+  G_(g)->timing = enabled != 0;
+  return RTENHIP_OK;
+}
+
+const char* rtenhip_graph_timing_report(rtenhip_graph* g) { return G_(g)->timing_report.c_str(); }
+
+int32_t rtenhip_graph_node_id(rtenhip_graph* g, const char* name) {
+  auto it = G_(g)->by_name.find(name ? name : "");
+  return it == G_(g)->by_name.end() ? -1 : it->second;
+}
+
+int32_t rtenhip_model_input_ids(rtenhip_graph* g, int32_t* ids, int32_t cap) {
+  auto& v = G_(g)->model_inputs;
+  for (int i = 0; i < (int)v.size() && i < cap; i++) ids[i] = v[i];
+  return (int32_t)v.size();
+}
+
+int32_t rtenhip_model_output_ids(rtenhip_graph* g, int32_t* ids, int32_t cap) {
+  auto& v = G_(g)->model_outputs;
+  for (int i = 0; i < (int)v.size() && i < cap; i++) ids[i] = v[i];
+  return (int32_t)v.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+// Graph IR and executor state behind rtenhip_graph (restates the semantics of
+// src/graph.rs: value/constant/operator nodes, DFS execution plan, refcount
+// frees, in-place reuse, timing).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "ctx.h"
+
+namespace rtenhip {
+
+using Shape = std::vector<int64_t>;
+
+struct Attrs {
+  std::map<std::string, std::vector<double>> nums;
+  std::map<std::string, std::string> strs;
+  bool has(const std::string& k) const { return nums.count(k) || strs.count(k); }
+  double num(const std::string& k, double dflt) const {
+    auto it = nums.find(k);
+    return it == nums.end() || it->second.empty() ? dflt : it->second[0];
+  }
+  std::vector<int64_t> ints(const std::string& k, std::vector<int64_t> dflt) const {
+    auto it = nums.find(k);
+    if (it == nums.end()) return dflt;
+    std::vector<int64_t> r;
+    for (double v : it->second) r.push_back((int64_t)v);
+    return r;
+  }
+  std::string str(const std::string& k, const std::string& dflt) const {
+    auto it = strs.find(k);
+    return it == strs.end() ? dflt : it->second;
+  }
+};
+
+// Parse "key=v1,v2;key2=text".
+bool parse_attrs(const char* s, Attrs& out);
+
+enum class NodeKind { Value, Constant, Operator };
+
+struct Node {
+  NodeKind kind = NodeKind::Value;
+  std::string name;
+  // Constant: device data + host copy for small tensors (scalar attrs).
+  float* dev = nullptr;
+  Shape shape;
+  std::vector<float> host_small;
+  bool owns_dev = true;
+  // Operator
+  std::string op_type;
+  Attrs attrs;
+  std::vector<int> inputs;   // -1 = absent optional input
+  std::vector<int> outputs;
+  // Load-time fusion (rtenhip_graph_optimize): Conv epilogue.
+  int fused_residual = -1;   // value id added after the bias
+  int fused_act = 0;         // RTENHIP_ACT_*
+  float act_lo = 0.f, act_hi = 0.f;
+  bool removed = false;      // op folded into another
+  bool alias_input0 = false; // output is a view of input 0 (Flatten/Reshape)
+};
+
+struct Slot {
+  size_t offset = 0;  // bytes into the arena, or external pointer when ext
+  float* ext = nullptr;
+  Shape shape;
+};
+
+struct Plan {
+  std::vector<int> ops;               // topological order
+  std::map<int, Slot> slots;          // value id -> storage
+  size_t arena_bytes = 0;
+  std::vector<int> input_ids, output_ids;
+  std::vector<Shape> input_shapes;
+  // hipGraph replay state: valid for these exact input/output pointers.
+  hipGraphExec_t exec = nullptr;
+  std::vector<float*> bound_in, bound_out;
+  int eager_runs = 0;
+};
+
+struct Graph {
+  Ctx* ctx = nullptr;
+  rtenhip_ctx* cptr = nullptr;
+  std::vector<Node> nodes;
+  std::map<std::string, int> by_name;
+  std::vector<int> model_inputs, model_outputs;
+  std::vector<std::unique_ptr<Plan>> plans;
+  void* arena = nullptr;
+  size_t arena_cap = 0;
+  hipStream_t exec_stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  bool timing = false;
+  bool use_hip_graph = true;
+  std::string timing_report;
+  std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
+
+  ~Graph();
+  int add_node(Node n);
+  rtenhip_status run(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
+                     const int32_t* out_ids, rtenhip_tensor* outs, int n_out);
+  rtenhip_status optimize();
+  rtenhip_status plan_shapes(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
+                             const int32_t* out_ids, int n_out, int64_t* shapes, int32_t* ndims);
+
+ private:
+  rtenhip_status find_plan(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
+                           const int32_t* out_ids, int n_out, Plan** out);
+  rtenhip_status make_plan(const std::vector<int>& in_ids, const std::vector<Shape>& in_shapes,
+                           const std::vector<int>& out_ids, Plan& p);
+  rtenhip_status infer_shapes(int op_id, const std::vector<const Shape*>& ins,
+                              std::vector<Shape>& outs);
+  rtenhip_status exec_op(Plan& p, int op_id);
+  float* ptr_of(Plan& p, int value_id);
+};
+
+}  // namespace rtenhip

@@ -1,0 +1,190 @@
+"""Graph / Model surface (src/graph.rs, src/model.rs) over the C ABI.
+
+``Graph`` mirrors RTen's ``Graph`` builder + ``run`` (graph.rs:509-1073): value,
+constant and operator nodes; ``run(inputs, outputs)`` plans, executes on the
+GPU and returns device tensors.  ``ModelSpec`` is a plain description of a
+model (the content a ``.rten`` file carries) that can be instantiated as a
+``Graph`` on the device — or, in tests, evaluated by the CPU oracle.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import MAX_DIMS, OpError, Tensor, _torch, check, default_context, describe, lib
+
+
+def _attr_str(attrs: dict) -> str:
+    parts = []
+    for k, v in attrs.items():
+        if isinstance(v, str):
+            parts.append(f"{k}={v}")
+        elif isinstance(v, (list, tuple)):
+            parts.append(f"{k}=" + ",".join(repr(float(x)) if isinstance(x, float) else str(int(x)) for x in v))
+        elif isinstance(v, bool):
+            parts.append(f"{k}={int(v)}")
+        elif isinstance(v, float):
+            parts.append(f"{k}={v!r}")
+        else:
+            parts.append(f"{k}={int(v)}")
+    return ";".join(parts)
+
+
+class Graph:
+    """Device graph (rtenhip_graph)."""
+
+    def __init__(self, ctx=None):
+        self.ctx = ctx or default_context()
+        self.ptr = lib().rtenhip_graph_create(C.c_void_p(self.ctx.ptr))
+        self.names: Dict[str, int] = {}
+        self.input_ids: List[int] = []
+        self.output_ids: List[int] = []
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib().rtenhip_graph_destroy(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ret(self, nid: int, name: str) -> int:
+        if nid < 0:
+            raise OpError(5, lib().rtenhip_last_error_message().decode())
+        if name:
+            self.names[name] = nid
+        return nid
+
+    def add_value(self, name: str) -> int:
+        return self._ret(lib().rtenhip_graph_add_value(C.c_void_p(self.ptr), name.encode()), name)
+
+    def add_constant(self, name: str, data: np.ndarray) -> int:
+        data = np.ascontiguousarray(data, dtype=np.float32)
+        shape = (C.c_int64 * max(1, data.ndim))(*data.shape)
+        nid = lib().rtenhip_graph_add_constant(C.c_void_p(self.ptr), name.encode(),
+                                              data.ctypes.data_as(C.POINTER(C.c_float)), shape,
+                                              C.c_int32(data.ndim))
+        return self._ret(nid, name)
+
+    def add_op(self, name: str, op_type: str, inputs: Sequence[Optional[int]],
+               outputs: Sequence[int], attrs: Optional[dict] = None) -> int:
+        ins = [(-1 if i is None else int(i)) for i in inputs]
+        ia = (C.c_int32 * max(1, len(ins)))(*ins)
+        oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
+        nid = lib().rtenhip_graph_add_op(C.c_void_p(self.ptr), name.encode(), op_type.encode(),
+                                         _attr_str(attrs or {}).encode(), ia, C.c_int32(len(ins)),
+                                         oa, C.c_int32(len(outputs)))
+        return self._ret(nid, name)
+
+    def optimize(self):
+        check(lib().rtenhip_graph_optimize(C.c_void_p(self.ptr)))
+
+    def node_id(self, name: str) -> int:
+        return self.names[name]
+
+    def set_timing(self, enabled: bool):
+        check(lib().rtenhip_graph_set_timing(C.c_void_p(self.ptr), C.c_int(int(enabled))))
+
+    def timing_report(self) -> str:
+        return lib().rtenhip_graph_timing_report(C.c_void_p(self.ptr)).decode()
+
+    def output_shapes(self, inputs: Dict[int, object], outputs: Sequence[int]):
+        in_ids = list(inputs.keys())
+        descs = (Tensor * max(1, len(in_ids)))(*[describe(inputs[i]) for i in in_ids])
+        ia = (C.c_int32 * max(1, len(in_ids)))(*in_ids)
+        oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
+        shapes = (C.c_int64 * (MAX_DIMS * max(1, len(outputs))))()
+        ndims = (C.c_int32 * max(1, len(outputs)))()
+        check(lib().rtenhip_graph_plan(C.c_void_p(self.ptr), ia, descs, C.c_int32(len(in_ids)), oa,
+                                       C.c_int32(len(outputs)), shapes, ndims))
+        return [tuple(shapes[i * MAX_DIMS + d] for d in range(ndims[i])) for i in range(len(outputs))]
+
+    def run(self, inputs: Dict[int, object], outputs: Sequence[int], out=None):
+        """Graph::run: inputs {value id: device tensor}; returns device tensors."""
+        torch = _torch()
+        self.ctx.sync_stream()
+        in_ids = list(inputs.keys())
+        if out is None:
+            shapes = self.output_shapes(inputs, outputs)
+            dev = next(iter(inputs.values())).device if inputs else torch.device("cuda")
+            out = [torch.empty(s, dtype=torch.float32, device=dev) for s in shapes]
+        descs = (Tensor * max(1, len(in_ids)))(*[describe(inputs[i]) for i in in_ids])
+        odescs = (Tensor * max(1, len(out)))(*[describe(t) for t in out])
+        ia = (C.c_int32 * max(1, len(in_ids)))(*in_ids)
+        oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
+        check(lib().rtenhip_graph_run(C.c_void_p(self.ptr), ia, descs, C.c_int32(len(in_ids)), oa,
+                                      odescs, C.c_int32(len(outputs))))
+        return out
+
+
+@dataclass
+class Node:
+    kind: str                      # "value" | "const" | "op"
+    name: str
+    data: Optional[np.ndarray] = None
+    op_type: str = ""
+    attrs: dict = field(default_factory=dict)
+    inputs: List[Optional[str]] = field(default_factory=list)
+    outputs: List[str] = field(default_factory=list)
+
+
+class ModelSpec:
+    """A model as data: the node list a .rten file holds (schema.fbs Graph)."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.nodes: List[Node] = []
+        self.inputs: List[str] = []
+        self.outputs: List[str] = []
+        self._n = 0
+
+    def value(self, name: str) -> str:
+        self.nodes.append(Node("value", name))
+        return name
+
+    def const(self, name: str, data: np.ndarray) -> str:
+        self.nodes.append(Node("const", name, data=np.ascontiguousarray(data, np.float32)))
+        return name
+
+    def op(self, op_type: str, inputs: Sequence[Optional[str]], attrs: Optional[dict] = None,
+           name: Optional[str] = None, n_outputs: int = 1) -> str:
+        self._n += 1
+        name = name or f"{op_type.lower()}_{self._n}"
+        outs = [self.value(f"{name}_out" if n_outputs == 1 else f"{name}_out{i}")
+                for i in range(n_outputs)]
+        self.nodes.append(Node("op", name, op_type=op_type, attrs=dict(attrs or {}),
+                               inputs=list(inputs), outputs=outs))
+        return outs[0]
+
+    def n_params(self) -> int:
+        return sum(n.data.size for n in self.nodes if n.kind == "const")
+
+    def to_graph(self, ctx=None, optimize: bool = True) -> Graph:
+        """Instantiate on the device (constants uploaded once)."""
+        g = Graph(ctx)
+        ids: Dict[str, int] = {}
+        for n in self.nodes:
+            if n.kind == "value":
+                ids[n.name] = g.add_value(n.name)
+            elif n.kind == "const":
+                ids[n.name] = g.add_constant(n.name, n.data)
+        for n in self.nodes:
+            if n.kind == "op":
+                g.add_op(n.name, n.op_type, [None if i is None else ids[i] for i in n.inputs],
+                         [ids[o] for o in n.outputs], n.attrs)
+        g.input_ids = [ids[i] for i in self.inputs]
+        g.output_ids = [ids[o] for o in self.outputs]
+        # The optimizer must know the model outputs (never fuse them away).
+        ia = (C.c_int32 * max(1, len(g.input_ids)))(*g.input_ids)
+        oa = (C.c_int32 * max(1, len(g.output_ids)))(*g.output_ids)
+        check(lib().rtenhip_graph_set_io(C.c_void_p(g.ptr), ia, C.c_int32(len(g.input_ids)), oa,
+                                         C.c_int32(len(g.output_ids))))
+        if optimize:
+            g.optimize()
+        return g

@@ -1,0 +1,167 @@
+"""Synthetic model definitions for the benchmark configs (BASELINE.json).
+
+No checkpoints or network exist here, so models are built with seeded
+random weights of the real architectures, in the operator mix RTen receives
+from an ONNX export with BatchNorm folded into Conv (tools/export-timm-model.py
+exports with torch.onnx constant folding):
+
+- ResNet-50 v1.5 (timm/torchvision ``resnet50``): Conv(+bias) / Relu / MaxPool
+  / Add / GlobalAveragePool / Flatten / Gemm.  He-uniform weights
+  U(+-sqrt(6/fan_in)), biases U(+-0.01), the last conv of every bottleneck
+  scaled by 0.2 so activations stay O(1) through 16 residual blocks
+  (SURVEY.md §8d).
+- MobileNetV2 (width 1.0): Conv / depthwise Conv / Clip(0, 6) / Add /
+  GlobalAveragePool / Flatten / Gemm.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .graph import ModelSpec
+
+RESNET50_GFLOP_PER_IMAGE = 8.178  # 2*MACs over 53 convs + FC
+MOBILENETV2_GFLOP_PER_IMAGE = 0.6015
+
+
+class _Init:
+    def __init__(self, seed: int):
+        self.rng = np.random.default_rng(seed)
+
+    def conv(self, cout, cin, kh, kw, scale=1.0):
+        fan_in = cin * kh * kw
+        lim = np.sqrt(6.0 / fan_in) * scale
+        w = self.rng.uniform(-lim, lim, size=(cout, cin, kh, kw)).astype(np.float32)
+        b = self.rng.uniform(-0.01, 0.01, size=(cout,)).astype(np.float32)
+        return w, b
+
+    def fc(self, cout, cin):
+        lim = np.sqrt(6.0 / cin)
+        w = self.rng.uniform(-lim, lim, size=(cout, cin)).astype(np.float32)
+        b = self.rng.uniform(-0.01, 0.01, size=(cout,)).astype(np.float32)
+        return w, b
+
+
+def _conv(m: ModelSpec, init: _Init, name, x, cin, cout, k, stride=1, pad=0, groups=1,
+          scale=1.0):
+    w, b = init.conv(cout, cin // groups, k, k, scale)
+    wn = m.const(f"{name}.weight", w)
+    bn = m.const(f"{name}.bias", b)
+    return m.op("Conv", [x, wn, bn], {"pads": [pad] * 4, "strides": [stride, stride],
+                                      "dilations": [1, 1], "groups": groups}, name=name)
+
+
+def resnet50(num_classes: int = 1000, seed: int = 4321) -> ModelSpec:
+    """ResNet-50 v1.5 (stride on the 3x3 conv), BN folded, NCHW input [N,3,224,224]."""
+    m = ModelSpec("resnet50")
+    init = _Init(seed)
+    x = m.value("input")
+    m.inputs = ["input"]
+    h = _conv(m, init, "conv1", x, 3, 64, 7, stride=2, pad=3)
+    h = m.op("Relu", [h], name="relu1")
+    h = m.op("MaxPool", [h], {"kernel_size": [3, 3], "strides": [2, 2], "pads": [1, 1, 1, 1]},
+             name="maxpool")
+    cin = 64
+    for li, (width, blocks, stride) in enumerate([(64, 3, 1), (128, 4, 2), (256, 6, 2),
+                                                  (512, 3, 2)]):
+        for bi in range(blocks):
+            s = stride if bi == 0 else 1
+            pre = f"layer{li + 1}.{bi}"
+            cout = width * 4
+            t = _conv(m, init, f"{pre}.conv1", h, cin, width, 1)
+            t = m.op("Relu", [t], name=f"{pre}.relu1")
+            t = _conv(m, init, f"{pre}.conv2", t, width, width, 3, stride=s, pad=1)
+            t = m.op("Relu", [t], name=f"{pre}.relu2")
+            t = _conv(m, init, f"{pre}.conv3", t, width, cout, 1, scale=0.2)
+            if bi == 0:
+                ident = _conv(m, init, f"{pre}.downsample", h, cin, cout, 1, stride=s)
+            else:
+                ident = h
+            t = m.op("Add", [t, ident], name=f"{pre}.add")
+            h = m.op("Relu", [t], name=f"{pre}.relu3")
+            cin = cout
+    h = m.op("GlobalAveragePool", [h], name="avgpool")
+    h = m.op("Flatten", [h], {"axis": 1}, name="flatten")
+    w, b = init.fc(num_classes, 2048)
+    h = m.op("Gemm", [h, m.const("fc.weight", w), m.const("fc.bias", b)],
+             {"alpha": 1.0, "beta": 1.0, "transA": 0, "transB": 1}, name="fc")
+    m.outputs = [h]
+    return m
+
+
+def mobilenet_v2(num_classes: int = 1000, seed: int = 4321) -> ModelSpec:
+    """MobileNetV2 1.0 (torchvision layout), BN folded, ReLU6 = Clip(0, 6)."""
+    m = ModelSpec("mobilenet_v2")
+    init = _Init(seed)
+    x = m.value("input")
+    m.inputs = ["input"]
+    zero = m.const("clip.min", np.array(0.0, np.float32))
+    six = m.const("clip.max", np.array(6.0, np.float32))
+
+    def relu6(t, name):
+        return m.op("Clip", [t, zero, six], name=name)
+
+    h = relu6(_conv(m, init, "features.0", x, 3, 32, 3, stride=2, pad=1), "features.0.relu6")
+    cin = 32
+    cfg = [(1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 96, 3, 1),
+           (6, 160, 3, 2), (6, 320, 1, 1)]
+    idx = 1
+    for t_exp, c, n, s in cfg:
+        for i in range(n):
+            stride = s if i == 0 else 1
+            pre = f"features.{idx}"
+            hidden = cin * t_exp
+            y = h
+            if t_exp != 1:
+                y = relu6(_conv(m, init, f"{pre}.expand", y, cin, hidden, 1), f"{pre}.expand.relu6")
+            y = relu6(_conv(m, init, f"{pre}.dw", y, hidden, hidden, 3, stride=stride, pad=1,
+                            groups=hidden), f"{pre}.dw.relu6")
+            y = _conv(m, init, f"{pre}.project", y, hidden, c, 1, scale=0.5)
+            if stride == 1 and cin == c:
+                y = m.op("Add", [y, h], name=f"{pre}.add")
+            h = y
+            cin = c
+            idx += 1
+    h = relu6(_conv(m, init, "features.18", h, 320, 1280, 1), "features.18.relu6")
+    h = m.op("GlobalAveragePool", [h], name="avgpool")
+    h = m.op("Flatten", [h], {"axis": 1}, name="flatten")
+    w, b = init.fc(num_classes, 1280)
+    h = m.op("Gemm", [h, m.const("classifier.weight", w), m.const("classifier.bias", b)],
+             {"alpha": 1.0, "beta": 1.0, "transA": 0, "transB": 1}, name="classifier")
+    m.outputs = [h]
+    return m
+
+
+def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
+    """2*MAC count of every Conv and Gemm in ``spec`` at input [batch,3,hw,hw]
+    (used for the roofline figure; cross-checked against SURVEY.md App. A)."""
+    shapes = {spec.inputs[0]: (batch, 3, hw, hw)}
+    consts = {n.name: n.data.shape for n in spec.nodes if n.kind == "const"}
+    total = 0.0
+    for n in spec.nodes:
+        if n.kind != "op":
+            continue
+        xs = shapes.get(n.inputs[0]) if n.inputs and n.inputs[0] in shapes else None
+        if n.op_type == "Conv":
+            o, ci, kh, kw = consts[n.inputs[1]]
+            N, C, H, W = xs
+            p, s = n.attrs["pads"], n.attrs["strides"]
+            oh = (H + p[0] + p[2] - kh) // s[0] + 1
+            ow = (W + p[1] + p[3] - kw) // s[1] + 1
+            total += 2.0 * N * o * oh * ow * ci * kh * kw
+            shapes[n.outputs[0]] = (N, o, oh, ow)
+        elif n.op_type == "MaxPool":
+            N, C, H, W = xs
+            k, s, p = n.attrs["kernel_size"], n.attrs["strides"], n.attrs["pads"]
+            shapes[n.outputs[0]] = (N, C, (H + p[0] + p[2] - k[0]) // s[0] + 1,
+                                    (W + p[1] + p[3] - k[1]) // s[1] + 1)
+        elif n.op_type == "GlobalAveragePool":
+            shapes[n.outputs[0]] = (xs[0], xs[1], 1, 1)
+        elif n.op_type == "Flatten":
+            shapes[n.outputs[0]] = (xs[0], int(np.prod(xs[1:])))
+        elif n.op_type == "Gemm":
+            o, k = consts[n.inputs[1]]
+            total += 2.0 * xs[0] * o * k
+            shapes[n.outputs[0]] = (xs[0], o)
+        else:
+            shapes[n.outputs[0]] = xs
+    return total

@@ -1,0 +1,91 @@
+"""Whole-model parity on the GPU: the device graph executor (fused, hipGraph
+replayed) against the CPU oracle running the same ModelSpec op by op with
+RTen's semantics.  Bar: bit-exact logits.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rh():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rten_hip
+
+    rten_hip.default_context()
+    return rten_hip
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def _run_both(rh, spec, batch, optimize=True, runs=3, seed=1234):
+    import torch
+    import graph_runner
+
+    x = np.random.default_rng(seed).random((batch, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {"input": x})[spec.outputs[0]]
+    g = spec.to_graph(optimize=optimize)
+    xd = torch.from_numpy(x).cuda()
+    outs = []
+    out = None
+    for _ in range(runs):  # run 1 eager, later runs replay the captured hipGraph
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        outs.append(out[0].cpu().numpy())
+    return exp, outs
+
+
+@pytest.mark.parametrize("optimize", [True, False])
+def test_resnet50_bitexact(rh, optimize):
+    from rten_hip import models
+
+    exp, outs = _run_both(rh, models.resnet50(), batch=2, optimize=optimize)
+    for o in outs:
+        if not _bits_equal(o, exp):
+            d = np.abs(o.astype(np.float64) - exp)
+            pytest.fail(f"ResNet-50 logits differ: max abs {d.max():.3g}, "
+                        f"rel {d.max() / np.abs(exp).max():.3g}, {(d > 0).sum()} elems")
+
+
+def test_mobilenet_v2_bitexact(rh):
+    from rten_hip import models
+
+    exp, outs = _run_both(rh, models.mobilenet_v2(), batch=2)
+    for o in outs:
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+
+
+def test_resnet50_batch64_full_size(rh):
+    """BASELINE config 2 (ResNet-50 f32, batch 64) end to end, bit-exact."""
+    from rten_hip import models
+
+    exp, outs = _run_both(rh, models.resnet50(), batch=64, runs=2, seed=7)
+    assert np.isfinite(exp).all()
+    for o in outs:
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+
+
+def test_graph_errors(rh):
+    import torch
+    from rten_hip.graph import Graph
+
+    g = Graph()
+    x = g.add_value("x")
+    w = g.add_constant("w", np.zeros((4, 3, 3, 3), np.float32))
+    y = g.add_value("y")
+    g.add_op("conv", "Conv", [x, w], [y], {"pads": [0, 0, 0, 0], "strides": [1, 1]})
+    with pytest.raises(rh.OpError) as e:
+        g.run({x: torch.zeros(1, 3, 2, 2, device="cuda")}, [y])
+    assert "Input too small for kernel size" in str(e.value)
+    z = g.add_value("z")
+    with pytest.raises(rh.OpError) as e:
+        g.run({}, [y])
+    assert e.value.kind == "MissingInputs"
