@@ -14,6 +14,7 @@
 
 #include "common.h"
 #include "ctx.h"
+#include "gemm_dma.h"
 
 namespace rtenhip {
 
@@ -47,28 +48,104 @@ Ctx::Ctx(int dev) : device(dev) {
 
 Ctx::~Ctx() {
   for (auto& kv : ktabs) (void)hipFree(kv.second);
-  if (scratch) (void)hipFree(scratch);
+  for (auto& kv : dtabs) (void)hipFree(kv.second);
+  for (auto& kv : packed_cache) (void)hipFree(kv.second);
+  for (int i = 0; i < NSLOTS; i++)
+    if (slots[i]) (void)hipFree(slots[i]);
 }
 
 float* Ctx::scratch_floats(size_t n, size_t slot) {
-  // Two independent grow-only regions carved from one allocation.
   size_t need = n * sizeof(float);
-  if (slot >= 2) return nullptr;
-  if (need > scratch_cap[slot]) {
-    size_t total = 0;
-    size_t caps[2] = {scratch_cap[0], scratch_cap[1]};
-    caps[slot] = need + (need >> 2) + 256;
-    total = caps[0] + caps[1];
+  if (slot >= (size_t)NSLOTS) return nullptr;
+  if (need > slot_cap[slot] || !slots[slot]) {
     void* p = nullptr;
+    size_t cap = need + (need >> 2) + 256;
     if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
-    if (hipMalloc(&p, total) != hipSuccess) return nullptr;
-    if (scratch) (void)hipFree(scratch);
-    scratch = p;
-    scratch_cap[0] = caps[0];
-    scratch_cap[1] = caps[1];
+    if (hipMalloc(&p, cap) != hipSuccess) return nullptr;
+    if (slots[slot]) (void)hipFree(slots[slot]);
+    slots[slot] = p;
+    slot_cap[slot] = cap;
   }
-  char* base = static_cast<char*>(scratch);
-  return reinterpret_cast<float*>(slot == 0 ? base : base + scratch_cap[0]);
+  return static_cast<float*>(slots[slot]);
+}
+
+const int* Ctx::dtab(int C, int H, int W, int kh, int kw, int dh, int dw) {
+  auto key = std::make_tuple(C, H, W, kh, kw, dh, dw);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = dtabs.find(key);
+  if (it != dtabs.end()) return it->second;
+  // Byte offsets, padded with out-of-range entries to a whole number of the
+  // largest K tile so the kernel never bounds-checks k.
+  const size_t K = (size_t)C * kh * kw;
+  std::vector<int> tab((K + DMA_KTAB_PAD - 1) / DMA_KTAB_PAD * DMA_KTAB_PAD, (int)DMA_OOB);
+  size_t r = 0;
+  for (int c = 0; c < C; c++)
+    for (int ky = 0; ky < kh; ky++)
+      for (int kx = 0; kx < kw; kx++) tab[r++] = (c * H * W + ky * dh * W + kx * dw) * 4;
+  int* d = nullptr;
+  if (hipMalloc(&d, tab.size() * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+    return nullptr;
+  dtabs[key] = d;
+  return d;
+}
+
+bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, int64_t groups,
+                       int64_t K) {
+  // 32-bit buffer offsets: the whole (padded) input must stay below 2 GiB.
+  const int64_t x_elems = N * C * Hp * Wp;
+  return x_elems < (int64_t(1) << 29) && K >= 1 && O / groups >= 1;
+}
+
+rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
+  const int64_t opg = a.O / a.groups, ipg = a.C / a.groups;
+  const int64_t K = ipg * a.kh * a.kw, P = a.oh * a.ow;
+  const int cfg = a.cfg >= 0 ? a.cfg : dma_default_cfg((int)opg, (int)(a.N * P), (int)K);
+  const DmaTile tile = dma_cfg_tile(cfg);
+  const int* tab = c->dtab((int)ipg, (int)a.Hp, (int)a.Wp, (int)a.kh, (int)a.kw, (int)a.dh,
+                           (int)a.dw);
+  if (!tab) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
+  const int64_t per_group = packed_a_floats((int)opg, (int)K, tile);
+  const int64_t x_total = a.N * a.C * a.Hp * a.Wp;
+  for (int64_t g = 0; g < a.groups; g++) {
+    DmaDesc d{};
+    d.M = (int)opg;
+    d.N = (int)(a.N * P);
+    d.K = (int)K;
+    d.tile = tile;
+    d.apk = a.packed_w + g * per_group;
+    d.x = a.xin + g * ipg * a.Hp * a.Wp;
+    d.x_bytes = (uint32_t)((x_total - g * ipg * a.Hp * a.Wp) * 4);
+    d.x_img = a.C * a.Hp * a.Wp;
+    d.ystride = a.sh * a.Wp;
+    d.xstride = a.sw;
+    d.OW = (int)a.ow;
+    d.P = (int)P;
+    d.ktab4 = tab;
+    d.out = a.y + g * opg * P;
+    d.out_img = a.y_img;
+    d.out_c = P;  // channel stride of an unpadded output plane
+    d.out_row = a.ow;
+    d.out_off = 0;
+    if (a.y_row) {
+      // padded output planes: (oh + 2*pad) x y_row, interior at y_off
+      d.out_c = a.y_img / a.O;
+      d.out_row = a.y_row;
+      d.out_off = a.y_off;
+    }
+    d.residual = a.residual ? a.residual + g * opg * P : nullptr;
+    d.res_img = a.O * P;
+    d.res_c = P;
+    d.bias = a.bias ? a.bias + g * opg : nullptr;
+    d.alpha = 1.f;
+    d.beta = 0.f;
+    d.act = a.act;
+    d.act_lo = a.lo;
+    d.act_hi = a.hi;
+    rtenhip_status st = launch_gemm_dma(d, cfg, c->stream);
+    if (st) return st;
+  }
+  return RTENHIP_OK;
 }
 
 const int2* Ctx::ktab(int C, int H, int W, int kh, int kw, int dh, int dw) {
@@ -124,14 +201,7 @@ rtenhip_status output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h, 
   return RTENHIP_OK;
 }
 
-// Resolved conv geometry shared by shape inference and execution.
-struct ConvPlan {
-  int64_t N, C, H, W, O, KC, kh, kw, sh, sw, dh, dw, oh, ow, groups;
-  int64_t pads[4];
-  bool one_d;
-};
-
-static rtenhip_status plan_conv(const rtenhip_tensor* x, const rtenhip_tensor* w, int pad_mode,
+rtenhip_status plan_conv(const rtenhip_tensor* x, const rtenhip_tensor* w, int pad_mode,
                                 const int64_t* pads, const int64_t* strides,
                                 const int64_t* dilations, int64_t groups, ConvPlan& p) {
   if (!x || !w) return fail(RTENHIP_MISSING_INPUTS, "Missing inputs");
@@ -190,6 +260,33 @@ static rtenhip_status plan_conv(const rtenhip_tensor* x, const rtenhip_tensor* w
   return RTENHIP_OK;
 }
 
+bool conv_takes_dma(const ConvPlan& p) {
+  const bool has_pad = p.pads[0] || p.pads[1] || p.pads[2] || p.pads[3];
+  const bool pointwise = p.kh == 1 && p.kw == 1 && !has_pad && p.groups == 1 && p.sh == 1 &&
+                         p.sw == 1 && p.dh == 1 && p.dw == 1;
+  const bool depthwise = p.C == p.O && p.groups == p.C;
+  const int64_t Hp = p.H + p.pads[0] + p.pads[2], Wp = p.W + p.pads[1] + p.pads[3];
+  return !depthwise && !(pointwise && p.O == 1) && p.N * p.oh * p.ow > 0 &&
+         conv_dma_eligible(p.N, p.C, Hp, Wp, p.O, p.groups, (p.C / p.groups) * p.kh * p.kw);
+}
+
+rtenhip_status pack_conv_weights(Ctx* c, const float* w, const ConvPlan& p, int cfg, float* out) {
+  const int64_t opg = p.O / p.groups, K = (p.C / p.groups) * p.kh * p.kw;
+  const DmaTile tile = dma_cfg_tile(cfg);
+  const int64_t per_group = packed_a_floats((int)opg, (int)K, tile);
+  for (int64_t g = 0; g < p.groups; g++) {
+    rtenhip_status st =
+        launch_pack_a(w + g * opg * K, K, (int)opg, (int)K, tile, out + g * per_group, c->stream);
+    if (st) return st;
+  }
+  return RTENHIP_OK;
+}
+
+int64_t packed_conv_weight_floats(const ConvPlan& p, int cfg) {
+  const int64_t opg = p.O / p.groups, K = (p.C / p.groups) * p.kh * p.kw;
+  return packed_a_floats((int)opg, (int)K, dma_cfg_tile(cfg)) * p.groups;
+}
+
 rtenhip_status conv_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* w,
                          const float* bias, int pad_mode, const int64_t* pads,
                          const int64_t* strides, const int64_t* dilations, int64_t groups,
@@ -210,6 +307,70 @@ rtenhip_status conv_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* 
   const int64_t P = p.oh * p.ow;
   const bool has_pad = p.pads[0] || p.pads[1] || p.pads[2] || p.pads[3];
   if (p.N == 0 || p.O == 0 || P == 0) return RTENHIP_OK;
+
+  const int64_t Hp = p.H + p.pads[0] + p.pads[2], Wp = p.W + p.pads[1] + p.pads[3];
+  if (c->use_dma && conv_takes_dma(p)) {
+    // Fast path: zero-bordered input + packed weights + LDS-DMA GEMM.
+    const float* xin = xd;
+    if (has_pad) {
+      float* xp = c->scratch_floats((size_t)(p.N * p.C * Hp * Wp), 1);
+      if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+      st = launch_pad_nchw(xd, xp, p.N * p.C, (int)p.H, (int)p.W, (int)p.pads[0], (int)p.pads[1],
+                           (int)p.pads[2], (int)p.pads[3], s);
+      if (st) return st;
+      xin = xp;
+    }
+    const int64_t opg = p.O / p.groups, K = (p.C / p.groups) * p.kh * p.kw;
+    const int cfg = dma_default_cfg((int)opg, (int)(p.N * P), (int)K);
+    const DmaTile tile = dma_cfg_tile(cfg);
+    const int64_t per_group = packed_a_floats((int)opg, (int)K, tile);
+    float* wp = nullptr;
+    auto key = std::make_tuple((const void*)w->data, opg * p.groups, K, tile.bm, tile.bk, tile.il);
+    if (c->trust_weight_cache) {
+      auto it = c->packed_cache.find(key);
+      if (it != c->packed_cache.end()) wp = it->second;
+    }
+    if (!wp) {
+      if (c->trust_weight_cache) {
+        if (hipMalloc(&wp, (size_t)(per_group * p.groups) * 4) != hipSuccess)
+          return fail(RTENHIP_HIP_ERROR, "hipMalloc failed");
+        c->packed_cache[key] = wp;
+      } else {
+        wp = c->scratch_floats((size_t)(per_group * p.groups), 2);
+        if (!wp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+      }
+      for (int64_t g = 0; g < p.groups; g++) {
+        st = launch_pack_a(w->data + g * opg * K, K, (int)opg, (int)K, tile, wp + g * per_group, s);
+        if (st) return st;
+      }
+    }
+    ConvDmaArgs a{};
+    a.xin = xin;
+    a.N = p.N;
+    a.C = p.C;
+    a.Hp = Hp;
+    a.Wp = Wp;
+    a.O = p.O;
+    a.kh = p.kh;
+    a.kw = p.kw;
+    a.sh = p.sh;
+    a.sw = p.sw;
+    a.dh = p.dh;
+    a.dw = p.dw;
+    a.oh = p.oh;
+    a.ow = p.ow;
+    a.groups = p.groups;
+    a.packed_w = wp;
+    a.bias = bias;
+    a.residual = residual;
+    a.act = act;
+    a.lo = lo;
+    a.hi = hi;
+    a.y = y->data;
+    a.y_img = p.O * P;
+    a.cfg = cfg;
+    return conv_dma(c, a);
+  }
 
   if (p.kh == 1 && p.kw == 1 && !has_pad && p.groups == 1 && p.sh == 1 && p.sw == 1 &&
       p.dh == 1 && p.dw == 1) {
@@ -395,6 +556,13 @@ rtenhip_status rtenhip_memcpy_d2h(rtenhip_ctx* ctx, void* dst, const void* src, 
 }
 
 const char* rtenhip_build_info(void) { return "rten-hip gfx950 (CDNA4) f32 MFMA backend v0.1"; }
+
+// Tuning / test knob: route convs through the LDS-DMA GEMM (default) or the
+// register-staged general kernel.  Both produce bit-identical results.
+void rtenhip_debug_set_dma(rtenhip_ctx* ctx, int enabled) { C_(ctx)->use_dma = enabled != 0; }
+void rtenhip_debug_trust_weight_cache(rtenhip_ctx* ctx, int enabled) {
+  C_(ctx)->trust_weight_cache = enabled != 0;
+}
 
 rtenhip_status rtenhip_output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h,
                                                int64_t k_w, int64_t stride_h, int64_t stride_w,

@@ -124,5 +124,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s);
 rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s);
+rtenhip_status launch_pad_nchw(const float* x, float* y, int64_t planes, int H, int W, int pt,
+                               int pl, int pb, int pr, hipStream_t s);
 
 }  // namespace rtenhip

@@ -20,17 +20,61 @@ struct Ctx {
   int ref_threads = 0;
   std::mutex mu;
   std::map<std::tuple<int, int, int, int, int, int, int>, int2*> ktabs;
-  void* scratch = nullptr;
-  size_t scratch_cap[2] = {0, 0};
+  std::map<std::tuple<int, int, int, int, int, int, int>, int*> dtabs;
+  static constexpr int NSLOTS = 4;
+  void* slots[NSLOTS] = {nullptr, nullptr, nullptr, nullptr};
+  size_t slot_cap[NSLOTS] = {0, 0, 0, 0};
+  bool use_dma = true;
+  // Packed-weight cache keyed by (weights pointer, M, K, bm, bk, il).  Only valid
+  // when the caller guarantees weights are immutable (graph constants); the
+  // public per-op API packs on every call unless a tuning tool opts in.
+  bool trust_weight_cache = false;
+  std::map<std::tuple<const void*, int64_t, int64_t, int, int, int>, float*> packed_cache;
 
   explicit Ctx(int dev);
   ~Ctx();
-  // Grow-only device scratch (two independent slots).  Synchronizes the
+  // Grow-only device scratch (independent slots: 0 contiguous copies,
+  // 1 softmax / padded inputs, 2 packed weights, 3 spare).  Synchronizes the
   // stream when it has to grow, so callers must not be capturing.
   float* scratch_floats(size_t n, size_t slot);
   // Device table of VirtualIm2Col row offsets for one conv geometry.
   const int2* ktab(int C, int H, int W, int kh, int kw, int dh, int dw);
+  // Device table of per-k input offsets c*H*W + ky*dh*W + kx*dw (DMA GEMM).
+  const int* dtab(int C, int H, int W, int kh, int kw, int dh, int dw);
 };
+
+// Conv through the DMA GEMM with caller-managed inputs: xin is the (padded)
+// input [N, C, Hp, Wp]; packed_w the weights packed for (bm, bk) per group.
+struct ConvDmaArgs {
+  const float* xin;
+  int64_t N, C, Hp, Wp, O, kh, kw, sh, sw, dh, dw, oh, ow, groups;
+  const float* packed_w;  // groups * packed_a_floats(opg, K)
+  const float* bias;
+  const float* residual;
+  int act;
+  float lo, hi;
+  float* y;
+  int64_t y_img, y_row, y_off;  // output addressing (padded outputs allowed)
+  int cfg;                      // DMA kernel configuration, -1 = default
+};
+rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
+bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, int64_t groups,
+                       int64_t K);
+
+// Resolved conv geometry shared by shape inference and execution.
+struct ConvPlan {
+  int64_t N, C, H, W, O, KC, kh, kw, sh, sw, dh, dw, oh, ow, groups;
+  int64_t pads[4];
+  bool one_d;
+};
+rtenhip_status plan_conv(const rtenhip_tensor* x, const rtenhip_tensor* w, int pad_mode,
+                         const int64_t* pads, const int64_t* strides, const int64_t* dilations,
+                         int64_t groups, ConvPlan& p);
+// Whether the conv runs on the LDS-DMA GEMM (vs depthwise / gemv / general).
+bool conv_takes_dma(const ConvPlan& p);
+// Weights packed for DMA configuration cfg (all groups).
+int64_t packed_conv_weight_floats(const ConvPlan& p, int cfg);
+rtenhip_status pack_conv_weights(Ctx* c, const float* w, const ConvPlan& p, int cfg, float* out);
 
 rtenhip_status output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h, int64_t k_w,
                                        int64_t stride_h, int64_t stride_w, int pad_mode,

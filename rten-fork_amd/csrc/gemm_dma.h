@@ -1,0 +1,60 @@
+// LDS-DMA GEMM fast path (gemm_dma.hip).
+#pragma once
+
+#include "common.h"
+
+namespace rtenhip {
+
+// Buffer offset past num_records: the hardware returns 0 for such loads.
+constexpr uint32_t DMA_OOB = 0x80000000u;
+// K tables are padded with DMA_OOB entries to a multiple of this (>= any BK).
+constexpr int DMA_KTAB_PAD = 64;
+
+// Tile shape of a DMA launch.  A is packed per tile as [bk][bm] with the rows
+// of each wave's 32*il-row slab interleaved (row mi*32+l -> position l*il+mi)
+// so a lane reads its il A values with one LDS instruction.
+struct DmaTile {
+  int bm, bk, il;
+  bool operator==(const DmaTile& o) const { return bm == o.bm && bk == o.bk && il == o.il; }
+};
+
+// C[M,N] = epilogue(alpha * A @ B) with
+//   A: packed [tiles_m][tiles_k][bk][bm] (launch_pack_a, interleaved by il),
+//   B[k][n] = x[colbase(n) + koff(k)] with no bounds checks, where for
+//     n = img*P + oy*OW + ox:  colbase = img*x_img + oy*ystride + ox*xstride
+//     and koff = ktab4[k] / 4 (ktab4 holds byte offsets, DMA_OOB past K,
+//     padded to a multiple of DMA_KTAB_PAD entries),
+//   out index  = img*out_img + m*out_c + oy*out_row + ox + out_off,
+//   residual   = img*res_img + m*res_c + (oy*OW + ox).
+struct DmaDesc {
+  int M, N, K;
+  DmaTile tile;             // tile shape A was packed for
+  const float* apk;
+  const float* x;
+  uint32_t x_bytes;         // buffer size in bytes (num_records)
+  int64_t x_img;
+  int64_t ystride, xstride;
+  int OW, P;
+  const int* ktab4;
+  float* out;
+  int64_t out_img, out_c, out_row, out_off;
+  const float* residual;
+  int64_t res_img, res_c;
+  const float* bias;
+  const float* cin;         // beta != 0 (dense outputs only; out_c = row stride)
+  float alpha, beta;
+  int act;
+  float act_lo, act_hi;
+  int dbg;                  // tuning experiments only: 1 = no K-loop DMA, 2 = no MFMA
+};
+
+// Kernel configurations (all bit-identical; see gemm_dma.hip).
+int dma_num_cfgs();
+int dma_default_cfg(int M, int N, int K);
+DmaTile dma_cfg_tile(int cfg);
+int64_t packed_a_floats(int M, int K, const DmaTile& t);
+rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const DmaTile& t,
+                             float* out, hipStream_t s);
+rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s);
+
+}  // namespace rtenhip

@@ -1,0 +1,451 @@
+// f32 MFMA GEMM with LDS-DMA staging for gfx950 — the fast path of the
+// implicit-GEMM engine (see gemm_mfma.hip for the general kernel and the
+// summation-order contract it shares: KC = 256 blocks, fma chains from +0,
+// bias after block 0, src/gemm.rs:733-1050).
+//
+// Why a second kernel: v_mfma_f32_32x32x2_f32 issues at the f32 VALU rate and
+// PMC counters show it never co-executes with VALU instructions
+// (SQ_VALU_MFMA_COEXEC_CYCLES = 0), so every address/bounds instruction of a
+// register-staged im2col gather is taken straight out of MFMA time.  This
+// kernel issues NO per-element VALU work in its K loop:
+//   - A (weights) is pre-packed once into [tiles_m][tiles_k][BK][BM] tiles
+//     (zero padded), copied into LDS by buffer_load_dwordx4 ... lds;
+//   - B is gathered with buffer_load_dword ... lds where each lane's VGPR
+//     offset (its output pixel's input corner) is fixed for the whole kernel
+//     and the k-dependent part is a scalar offset from a per-k table.  This
+//     is exact for convolutions whose input needs no bounds checks: pointwise
+//     and unpadded strided convs, and padded convs whose input the graph
+//     executor materialised with its zero border.  Out-of-range n / k are
+//     pushed past the buffer's num_records and read as 0 by the hardware.
+#include <type_traits>
+
+#include "common.h"
+#include "gemm_dma.h"
+
+namespace rtenhip {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+// Constant address space: uniform loads through it become s_load (SMEM,
+// lgkmcnt) instead of vector loads that would drain vmcnt and with it the
+// whole DMA pipeline.
+typedef __attribute__((address_space(4))) const int const_int_t;
+
+constexpr int DKC = 256;
+
+// One block computes a BM x BN tile with WAVES_M x WAVES_N waves, each owning
+// a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA accumulators.
+template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES,
+          bool MULTI_KB>
+__global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles_m, int tiles_n) {
+  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
+  constexpr int NW = NT / 64;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
+  constexpr int MI = WM / 32, NI = WN / 32;
+  // A tile copy: dwordx4 per lane when there is enough data for every wave,
+  // else dword.
+  constexpr int A_LB = BM * BK * 4 >= NT * 16 ? 16 : 4;  // bytes per lane
+  constexpr int A_CHUNK = 64 * A_LB;                     // bytes per wave-instruction
+  constexpr int A_INSTR = BM * BK * 4 / A_CHUNK;
+  constexpr int B_INSTR = BK * (BN / 64);    // dword wave-instructions per B tile
+  constexpr int A_PER_W = A_INSTR / NW;
+  constexpr int B_PER_W = B_INSTR / NW;
+  constexpr int STAGE = (BM + BN) * BK;      // floats per stage
+  constexpr int KSTEPS = BK / 2;
+  static_assert(WAVES_M * WAVES_N == NW, "wave grid");
+  static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "even DMA split");
+  static_assert(BN % 64 == 0 && DKC % BK == 0 && BK <= DMA_KTAB_PAD, "tile shape");
+  static_assert(MI >= 1 && NI >= 1, "wave tile");
+
+  __shared__ float lds[STAGES * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (wave / WAVES_N) * WM;
+  const int wn = (wave % WAVES_N) * WN;
+
+  // XCD-aware bijective remap (see gemm_mfma.hip).
+  const int nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tmi = wg % tiles_m;
+  const int tm = tmi * BM;
+  const int tn = (wg / tiles_m) * BN;
+  const int M = d.M, N = d.N, K = d.K;
+  const int tiles_k = (K + BK - 1) / BK;
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, d.x_bytes, 0x00020000);
+
+  // Per-lane B offsets: one per 64-column group this wave loads.
+  constexpr int NG = BN / 64;
+  uint32_t vb[NG];
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    // LDS position p of a B row holds column wn' + ni*32 + l where p = wn' + l*NI + ni,
+    // so a lane's NI B values for one k are adjacent (one ds_read).
+    const int pos = g * 64 + lane;
+    const int q = pos % WN;
+    const int n = tn + (pos - q) + (q % NI) * 32 + q / NI;
+    uint32_t off = DMA_OOB;
+    if (n < N) {
+      const int img = n / d.P;
+      const int p = n - img * d.P;
+      const int oy = p / d.OW;
+      const int ox = p - oy * d.OW;
+      off = (uint32_t)(((int64_t)img * d.x_img + (int64_t)oy * d.ystride + (int64_t)ox * d.xstride) * 4);
+    }
+    vb[g] = off;
+  }
+  const uint32_t va = (uint32_t)(wave * A_PER_W * A_CHUNK + lane * A_LB);
+  const uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
+  const_int_t* ktab4 = (const_int_t*)d.ktab4;
+
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    float* As = lds + stage * STAGE;
+    float* Bs = As + BM * BK;
+    const uint32_t a_soff = a_row_base + (uint32_t)kt * (BM * BK * 4);
+#pragma unroll
+    for (int i = 0; i < A_PER_W; i++) {
+      lds_void_t* dst = (lds_void_t*)(As + (wave * A_PER_W + i) * (A_CHUNK / 4));
+      if constexpr (A_LB == 16)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, va + i * A_CHUNK, a_soff, 0, 0);
+      else
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 4, va + i * A_CHUNK, a_soff, 0, 0);
+    }
+    const_int_t* kt4 = ktab4 + kt * BK;
+#pragma unroll
+    for (int i = 0; i < B_PER_W; i++) {
+      const int gi = wave * B_PER_W + i;  // wave-uniform
+      const int kl = gi / NG, g = gi % NG;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(Bs + kl * BN + g * 64), 4, vb[g],
+                                               (uint32_t)kt4[kl], 0, 0);
+    }
+  };
+
+  f32x16 acc[MI][NI];
+#pragma unroll
+  for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+    for (int ni = 0; ni < NI; ni++) acc[mi][ni] = (f32x16){0};
+
+  const int half = lane >> 5;
+  const int l32 = lane & 31;
+  const int m_lim = M - 1 - tm;
+  const int n_lim = N - 1 - tn;
+  auto lrow = [&](int mi, int j) __attribute__((always_inline)) { return wm + mi * 32 + (j & 3) + 8 * (j >> 2) + 4 * half; };
+
+  // End of K block 0: v = alpha*acc (+ beta*C) + bias (gemm.rs:1004-1050).
+  auto first_block = [&](f32x16& v, const f32x16& a, int mi, int ni) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int ml = min(lrow(mi, j), m_lim);
+      float x;
+      if (d.cin) {
+        const int nl = min(wn + ni * 32 + l32, n_lim);
+        const float c = d.cin[(int64_t)(tm + ml) * d.out_c + tn + nl];
+        x = __fmaf_rn(a[j], d.alpha, __fmul_rn(c, d.beta));
+      } else {
+        x = __fmul_rn(a[j], d.alpha);
+      }
+      if (d.bias) x = __fadd_rn(x, d.bias[tm + ml]);
+      v[j] = x;
+    }
+  };
+
+  // LDS read offsets of this lane (floats, relative to a stage): its MI A
+  // values and NI B values of one k row are contiguous (see pack_a_kernel and
+  // the B column permutation above).
+  const int a_lane = half * BM + wm + l32 * MI;
+  const int b_lane = BM * BK + half * BN + wn + l32 * NI;
+
+  // Software pipeline over K tiles.  A tile's operands are read from LDS
+  // into one of two register sets in a single burst; the next tile's burst is
+  // issued before the last two MFMA steps of the current one, so LDS latency
+  // hides behind MFMAs.  As soon as every wave holds its operands of tile kt
+  // (barrier), tile kt's stage is refilled with tile kt+STAGES.  Waits are
+  // counted and the barrier is a raw s_barrier, so later tiles' DMAs stay in
+  // flight across it (__syncthreads would drain vmcnt).
+  constexpr int PER_TILE = A_PER_W + B_PER_W;
+  typedef float va_t __attribute__((ext_vector_type(MI)));
+  typedef float vb_t __attribute__((ext_vector_type(NI)));
+  va_t av[2][KSTEPS];
+  vb_t bv[2][KSTEPS];
+
+  auto wait_dma = [&](int allowed_tiles) __attribute__((always_inline)) {
+    if (STAGES >= 4 && allowed_tiles >= 3) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * 3) : "memory");
+    } else if (STAGES >= 3 && allowed_tiles >= 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * 2) : "memory");
+    } else if (allowed_tiles >= 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  };
+  auto read_tile = [&](auto set_tag, int stage) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_tag)::value;
+    const float* As = lds + stage * STAGE + a_lane;
+    const float* Bs = lds + stage * STAGE + b_lane;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; s++) {
+      av[SET][s] = *(const va_t*)(As + 2 * s * BM);
+      bv[SET][s] = *(const vb_t*)(Bs + 2 * s * BN);
+    }
+  };
+  auto mfma_steps = [&](auto set_tag, auto s0_tag, auto s1_tag) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_tag)::value;
+    if (d.dbg & 2) return;
+#pragma unroll
+    for (int s = decltype(s0_tag)::value; s < decltype(s1_tag)::value; s++)
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[SET][s][mi], bv[SET][s][ni],
+                                                             acc[mi][ni], 0, 0, 0);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  constexpr int TAIL = KSTEPS >= 4 ? 2 : 1;
+  using IMid = std::integral_constant<int, KSTEPS - TAIL>;
+  using IEnd = std::integral_constant<int, KSTEPS>;
+
+  int stage = 0;  // stage holding tile kt
+  auto body = [&](auto set_tag, int kt) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_tag)::value;
+    mfma_steps(set_tag, I0{}, IMid{});
+    if (kt + 1 < tiles_k) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wait_dma(min(STAGES - 2, tiles_k - kt - 2));
+      __builtin_amdgcn_s_barrier();
+      if (kt + STAGES < tiles_k && !(d.dbg & 1)) issue(stage, kt + STAGES);
+      stage = stage + 1 == STAGES ? 0 : stage + 1;
+      read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
+    }
+    mfma_steps(set_tag, IMid{}, IEnd{});
+  };
+  // Tiles [kt0, kt1) with kt0 even (register set = tile parity).
+  auto run = [&](int kt0, int kt1) __attribute__((always_inline)) {
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      body(I0{}, kt);
+      if (kt + 1 < kt1) body(I1{}, kt + 1);
+    }
+  };
+
+  // Prologue: fill every stage, wait for tile 0, read it.
+#pragma unroll
+  for (int s = 0; s < STAGES; s++)
+    if (s < tiles_k) issue(s, s);
+  wait_dma(min(STAGES, tiles_k) - 1);
+  __builtin_amdgcn_s_barrier();
+  read_tile(I0{}, 0);
+
+  f32x16 sum[MULTI_KB ? MI : 1][MULTI_KB ? NI : 1];
+  if constexpr (!MULTI_KB) {
+    run(0, tiles_k);
+  } else {
+    // K > DKC: block 0 is peeled so the bias/beta fold sits outside the loop.
+    constexpr int TPB = DKC / BK;
+    static_assert(TPB % 2 == 0, "register-set parity across K blocks");
+    run(0, TPB);
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++) {
+        first_block(sum[mi][ni], acc[mi][ni], mi, ni);
+        acc[mi][ni] = (f32x16){0};
+      }
+    for (int kt = TPB; kt < tiles_k; kt += TPB) {
+      run(kt, min(kt + TPB, tiles_k));
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++) {
+#pragma unroll
+          for (int j = 0; j < 16; j++) sum[mi][ni][j] = __fmaf_rn(acc[mi][ni][j], d.alpha, sum[mi][ni][j]);
+          acc[mi][ni] = (f32x16){0};
+        }
+    }
+  }
+
+  // ---- epilogue ----
+  const bool full_tile = m_lim >= BM - 1 && n_lim >= BN - 1;
+#pragma unroll
+  for (int ni = 0; ni < NI; ni++) {
+    const int nl = wn + ni * 32 + l32;
+    const bool ncol_ok = nl <= n_lim;
+    const int n = tn + min(nl, n_lim);
+    const int img = n / d.P;
+    const int p = n - img * d.P;
+    const int oy = p / d.OW;
+    const int ox = p - oy * d.OW;
+    const int64_t obase = (int64_t)img * d.out_img + (int64_t)oy * d.out_row + ox + d.out_off;
+    const int64_t rbase = (int64_t)img * d.res_img + p;
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++) {
+      f32x16 v;
+      if constexpr (MULTI_KB) {
+        v = sum[mi][ni];
+      } else {
+        first_block(v, acc[mi][ni], mi, ni);
+      }
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int ml = lrow(mi, j);
+        const bool ok = full_tile || (ncol_ok && ml <= m_lim);
+        float x = v[j];
+        if (d.residual) x = __fadd_rn(x, d.residual[ok ? rbase + (int64_t)(tm + ml) * d.res_c : 0]);
+        if (d.act == RTENHIP_ACT_RELU) {
+          x = fmaxf(x, 0.f);
+        } else if (d.act == RTENHIP_ACT_CLIP) {
+          x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+        }
+        if (ok) d.out[obase + (int64_t)(tm + ml) * d.out_c] = x;
+      }
+    }
+  }
+}
+
+template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES>
+static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
+  const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
+  dim3 grid(tiles_m * tiles_n), block(NT);
+  if (d.K > DKC)
+    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true>), grid,
+                       block, 0, s, d, tiles_m, tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false>), grid,
+                       block, 0, s, d, tiles_m, tiles_n);
+}
+
+// DMA tile configurations:
+//   X(id, threads, BM, BN, BK, WAVES_M, WAVES_N, min waves/SIMD, stages)
+// The wave tile is (BM/WAVES_M) x (BN/WAVES_N).  All configurations produce
+// bit-identical results (same KC-block summation order), so the choice is
+// purely a performance one: dma_default_cfg below, or plan-time tuning.
+#define RTENHIP_DMA_CONFIGS(X)          \
+  X(0, 512, 128, 128, 16, 4, 2, 2, 3)   \
+  X(1, 256, 128, 128, 16, 2, 2, 2, 3)   \
+  X(2, 256, 64, 256, 16, 1, 4, 2, 3)    \
+  X(3, 128, 128, 64, 16, 2, 1, 2, 3)    \
+  X(4, 128, 64, 128, 16, 1, 2, 2, 3)    \
+  X(5, 64, 64, 64, 16, 1, 1, 2, 3)      \
+  X(6, 512, 256, 128, 16, 4, 2, 2, 3)   \
+  X(7, 256, 64, 64, 16, 2, 2, 4, 3)     \
+  X(8, 128, 64, 64, 16, 2, 1, 3, 3)     \
+  X(9, 256, 128, 64, 16, 4, 1, 3, 3)    \
+  X(10, 256, 64, 128, 16, 2, 2, 3, 3)   \
+  X(11, 512, 128, 128, 16, 4, 2, 2, 4)  \
+  X(12, 256, 128, 128, 16, 2, 2, 2, 4)  \
+  X(13, 256, 64, 64, 32, 2, 2, 4, 2)    \
+  X(14, 256, 64, 64, 16, 2, 2, 4, 4)    \
+  X(15, 512, 128, 64, 16, 4, 2, 4, 3)   \
+  X(16, 512, 64, 128, 16, 2, 4, 4, 3)   \
+  X(17, 128, 32, 64, 16, 1, 2, 4, 3)    \
+  X(18, 1024, 128, 128, 16, 4, 4, 4, 3)
+
+struct DmaCfgInfo {
+  int nt, bm, bn, bk, waves_m, waves_n;
+};
+static const DmaCfgInfo kDmaCfgs[] = {
+#define RTENHIP_DMA_INFO(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) {NT, BM, BN, BK, WMW, WNW},
+    RTENHIP_DMA_CONFIGS(RTENHIP_DMA_INFO)
+#undef RTENHIP_DMA_INFO
+};
+constexpr int kNumDmaCfgs = sizeof(kDmaCfgs) / sizeof(kDmaCfgs[0]);
+static int g_dma_cfg = -1;
+static int g_dma_dbg = 0;
+
+int dma_num_cfgs() { return kNumDmaCfgs; }
+
+DmaTile dma_cfg_tile(int cfg) {
+  const DmaCfgInfo& c = kDmaCfgs[cfg];
+  return DmaTile{c.bm, c.bk, c.bm / c.waves_m / 32};
+}
+
+int dma_default_cfg(int M, int N, int K) {
+  (void)K;
+  if (g_dma_cfg >= 0 && g_dma_cfg < kNumDmaCfgs) return g_dma_cfg;
+  // Largest tile that still gives every CU about two blocks.
+  auto tiles = [&](int c) {
+    return (int64_t)((M + kDmaCfgs[c].bm - 1) / kDmaCfgs[c].bm) *
+           ((N + kDmaCfgs[c].bn - 1) / kDmaCfgs[c].bn);
+  };
+  if (M <= 64) return tiles(2) >= 512 ? 2 : (tiles(4) >= 512 ? 4 : 7);
+  if (tiles(1) >= 512) return 1;
+  if (tiles(3) >= 512) return 3;
+  return 7;
+}
+
+rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
+  if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty DMA GEMM");
+  if (cfg < 0 || cfg >= kNumDmaCfgs) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
+  if (!(dma_cfg_tile(cfg) == d.tile))
+    return fail(RTENHIP_INVALID_VALUE, "A packed for another tile shape");
+  DmaDesc dd = d;
+  dd.dbg = g_dma_dbg;
+  switch (cfg) {
+#define RTENHIP_DMA_CASE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) \
+  case id:                                                    \
+    launch_dma_cfg<NT, BM, BN, BK, WMW, WNW, MINW, ST>(dd, s); \
+    break;
+    RTENHIP_DMA_CONFIGS(RTENHIP_DMA_CASE)
+#undef RTENHIP_DMA_CASE
+    default:
+      return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
+  }
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+}  // namespace rtenhip
+
+extern "C" void rtenhip_debug_set_dma_config(int cfg) { rtenhip::g_dma_cfg = cfg; }
+extern "C" void rtenhip_debug_set_dma_mode(int mode) { rtenhip::g_dma_dbg = mode; }
+
+namespace rtenhip {
+
+// Pack A[M, K] (row stride lda, unit column stride) into
+// [tiles_m][tiles_k][BK][BM] tiles, zero padded, rows of each 32*il slab
+// interleaved: position l*il + mi holds row mi*32 + l.
+__global__ void pack_a_kernel(const float* __restrict__ a, int64_t lda, int M, int K, int BM,
+                              int BK, int il, int tiles_k, float* __restrict__ out, int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int pos = (int)(i % BM);
+    const int64_t t = i / BM;
+    const int kk = (int)(t % BK);
+    const int64_t tile = t / BK;
+    const int kt = (int)(tile % tiles_k);
+    const int mt = (int)(tile / tiles_k);
+    const int slab = 32 * il;
+    const int q = pos % slab;
+    const int mm = (pos - q) + (q % il) * 32 + q / il;
+    const int m = mt * BM + mm, k = kt * BK + kk;
+    out[i] = (m < M && k < K) ? a[(int64_t)m * lda + k] : 0.f;
+  }
+}
+
+int64_t packed_a_floats(int M, int K, const DmaTile& t) {
+  const int64_t tm = (M + t.bm - 1) / t.bm, tk = (K + t.bk - 1) / t.bk;
+  return tm * tk * t.bm * t.bk;
+}
+
+rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const DmaTile& t,
+                             float* out, hipStream_t s) {
+  const int tiles_k = (K + t.bk - 1) / t.bk;
+  const int64_t total = packed_a_floats(M, K, t);
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, lda, M, K, t.bm,
+                     t.bk, t.il, tiles_k, out, total);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+}  // namespace rtenhip

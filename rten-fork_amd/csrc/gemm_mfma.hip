@@ -28,17 +28,19 @@ namespace rtenhip {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 16;       // K-tile depth (divides KC = 256)
 constexpr int KC = 256;      // reference depth block (gemm.rs:546-548)
 constexpr int PAD = 4;       // LDS row pad (floats): 2-way at worst on writes
 
-constexpr int NT = 512;      // threads per block (8 waves)
-
+// NT threads (NT/64 waves in a WAVES_M x WAVES_N grid), BM x BN output tile,
+// BK-deep K tiles (BK divides KC), MINW = min waves per SIMD for the
+// register allocator.
 // BMODE 0: dense B, dense output out[m*out_m + n] (GEMM / MatMul).
 // BMODE 1: im2col B, NCHW output.  BMODE 2: pointwise-conv B, NCHW output.
 // All offsets inside one operand are 32-bit (the host checks sizes).
-template <int BM, int BN, int WAVES_M, int WAVES_N, int BMODE, bool MULTI_KB>
-__global__ __launch_bounds__(NT, 2) void gemm_mfma_kernel(GemmDesc d, int tiles_m, int tiles_n) {
+template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int BMODE,
+          bool MULTI_KB>
+__global__ __launch_bounds__(NT, MINW) void gemm_mfma_kernel(GemmDesc d, int tiles_m, int tiles_n) {
+  static_assert(KC % BK == 0, "BK divides KC");
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
   constexpr int MI = WM / 32, NI = WN / 32;
   constexpr int APT = BM * BK / NT;  // A elements staged per thread
@@ -302,24 +304,48 @@ __global__ __launch_bounds__(NT, 2) void gemm_mfma_kernel(GemmDesc d, int tiles_
   }
 }
 
-template <int BM, int BN, int WM_, int WN_, int BMODE>
+template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int BMODE>
 static void launch_cfg(const GemmDesc& d, hipStream_t s) {
   int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
   dim3 grid(tiles_m * tiles_n, d.nbatch > 1 ? d.nbatch : 1), block(NT);
   if (d.K > KC)
-    hipLaunchKernelGGL((gemm_mfma_kernel<BM, BN, WM_, WN_, BMODE, true>), grid, block, 0, s, d,
-                       tiles_m, tiles_n);
+    hipLaunchKernelGGL((gemm_mfma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, BMODE, true>), grid,
+                       block, 0, s, d, tiles_m, tiles_n);
   else
-    hipLaunchKernelGGL((gemm_mfma_kernel<BM, BN, WM_, WN_, BMODE, false>), grid, block, 0, s, d,
-                       tiles_m, tiles_n);
+    hipLaunchKernelGGL((gemm_mfma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, BMODE, false>), grid,
+                       block, 0, s, d, tiles_m, tiles_n);
 }
+
+// Tile configurations (id -> template); RTENHIP_GEMM_CFG forces one (tuning).
+static int g_forced_cfg = -2;
+static int forced_cfg() {
+  if (g_forced_cfg == -2) {
+    const char* s = getenv("RTENHIP_GEMM_CFG");
+    g_forced_cfg = s ? atoi(s) : -1;
+  }
+  return g_forced_cfg;
+}
+
+}  // namespace rtenhip
+
+extern "C" void rtenhip_debug_set_gemm_config(int cfg) { rtenhip::g_forced_cfg = cfg; }
+
+namespace rtenhip {
 
 template <int BMODE>
 static void launch_mode(const GemmDesc& d, hipStream_t s) {
-  if (d.M <= 64)
-    launch_cfg<64, 128, 2, 4, BMODE>(d, s);
-  else
-    launch_cfg<128, 128, 4, 2, BMODE>(d, s);
+  int cfg = forced_cfg();
+  if (cfg < 0) cfg = d.M <= 64 ? 1 : 0;
+  switch (cfg) {
+    case 1: launch_cfg<512, 64, 128, 16, 2, 4, 2, BMODE>(d, s); break;
+    case 2: launch_cfg<256, 128, 128, 16, 2, 2, 2, BMODE>(d, s); break;
+    case 3: launch_cfg<256, 128, 128, 32, 2, 2, 2, BMODE>(d, s); break;
+    case 4: launch_cfg<512, 128, 256, 16, 2, 4, 1, BMODE>(d, s); break;
+    case 5: launch_cfg<256, 64, 128, 16, 2, 2, 2, BMODE>(d, s); break;
+    case 6: launch_cfg<256, 128, 64, 16, 2, 2, 2, BMODE>(d, s); break;
+    case 7: launch_cfg<512, 128, 128, 32, 4, 2, 2, BMODE>(d, s); break;
+    default: launch_cfg<512, 128, 128, 16, 4, 2, 2, BMODE>(d, s); break;
+  }
 }
 
 // K == 0 (gemm.rs:757-765): out = beta * (beta == 0 ? 0 : out); no bias.

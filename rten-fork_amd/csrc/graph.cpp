@@ -14,6 +14,7 @@
 //  - Timing (RunOptions.timing / RTEN_TIMING, graph.rs:1039-1055): per-op
 //    hipEvent times aggregated by operator type.
 #include "graph.h"
+#include "gemm_dma.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -67,6 +68,30 @@ static int64_t prod(const Shape& s, size_t from = 0, size_t to = SIZE_MAX) {
 
 static rtenhip_tensor desc(float* p, const Shape& s) {
   return make_tensor(p, s.data(), (int)s.size());
+}
+
+Plan::~Plan() {
+  for (auto& kv : convs)
+    if (kv.second.packed) (void)hipFree(kv.second.packed);
+  for (auto& kv : padded)
+    if (kv.second.base) (void)hipFree(kv.second.base);
+}
+
+// Conv attributes as conv_impl takes them.
+struct ConvAttrs {
+  int mode;
+  std::vector<int64_t> pads, strides, dil;
+  int64_t groups;
+};
+static ConvAttrs conv_attrs(const Node& n, bool one_d) {
+  ConvAttrs a;
+  std::string ap = n.attrs.str("auto_pad", "notset");
+  a.mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+  a.pads = n.attrs.ints("pads", one_d ? std::vector<int64_t>{0, 0} : std::vector<int64_t>{0, 0, 0, 0});
+  a.strides = n.attrs.ints("strides", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
+  a.dil = n.attrs.ints("dilations", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
+  a.groups = (int64_t)n.attrs.num("groups", 1);
+  return a;
 }
 
 Graph::~Graph() {
@@ -295,6 +320,63 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   }
   std::set<int> outset(out_ids.begin(), out_ids.end());
 
+  // Convs that run on the DMA GEMM.
+  for (int op : p.ops) {
+    const Node& n = nodes[op];
+    if (n.op_type != "Conv" || n.inputs.size() < 2) continue;
+    const Shape* xs = shape_of(n.inputs[0]);
+    const Shape* ws = shape_of(n.inputs[1]);
+    if (!xs || !ws || nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
+    const bool one_d = xs->size() == 3;
+    ConvAttrs ca = conv_attrs(n, one_d);
+    rtenhip_tensor xt = desc(nullptr, *xs), wt = desc(nullptr, *ws);
+    ConvExec ce;
+    if (plan_conv(&xt, &wt, ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(), ca.groups,
+                  ce.g) != RTENHIP_OK)
+      continue;
+    if (!ce.g.one_d && conv_takes_dma(ce.g)) p.convs[op] = ce;
+  }
+  // Values produced by a DMA conv and read only (as input 0) by padded DMA
+  // convs that agree on the padding get a persistent zero-bordered buffer.
+  {
+    std::map<int, std::vector<int>> readers;  // value -> ops reading it (any role)
+    for (int op : p.ops) {
+      for (int i : nodes[op].inputs)
+        if (i >= 0) readers[i].push_back(op);
+      if (nodes[op].fused_residual >= 0) readers[nodes[op].fused_residual].push_back(op);
+    }
+    for (auto& kv : p.convs) {
+      const int v = nodes[kv.first].outputs[0];
+      if (outset.count(v) || !readers.count(v)) continue;
+      bool ok = true;
+      const int64_t* pads = nullptr;
+      for (int r : readers[v]) {
+        auto it = p.convs.find(r);
+        const Node& rn = nodes[r];
+        if (it == p.convs.end() || rn.inputs[0] != v || rn.fused_residual == v) {
+          ok = false;
+          break;
+        }
+        for (size_t k = 1; k < rn.inputs.size(); k++)
+          if (rn.inputs[k] == v) ok = false;
+        const int64_t* rp = it->second.g.pads;
+        if (!(rp[0] || rp[1] || rp[2] || rp[3])) ok = false;
+        if (pads && !std::equal(pads, pads + 4, rp)) ok = false;
+        pads = rp;
+        if (!ok) break;
+      }
+      if (!ok || !pads) continue;
+      const Shape& ls = shapes[v];
+      PaddedValue pv;
+      std::copy(pads, pads + 4, pv.pads);
+      pv.phys = {ls[0], ls[1], ls[2] + pads[0] + pads[2], ls[3] + pads[1] + pads[3]};
+      const size_t bytes = (size_t)prod(pv.phys) * sizeof(float);
+      RTENHIP_HIP_CHECK(hipMalloc(&pv.base, bytes));
+      RTENHIP_HIP_CHECK(hipMemset(pv.base, 0, bytes));
+      p.padded[v] = pv;
+    }
+  }
+
   // Storage blocks with best-fit reuse; aliases share their base's block.
   struct Block {
     size_t off, size;
@@ -356,7 +438,11 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     bool alias = n.op_type == "Flatten" || n.op_type == "Reshape" || n.op_type == "Identity";
     n.alias_input0 = alias;
     int in0 = n.inputs.empty() ? -1 : n.inputs[0];
-    if (outset.count(out)) {
+    if (p.padded.count(out)) {
+      // Persistent zero-bordered storage (PaddedValue), not in the arena.
+      s.offset = SIZE_MAX - 1;
+      p.slots[out] = s;
+    } else if (outset.count(out)) {
       // Written straight into the caller's buffer (aliases copy into it).
       s.ext = nullptr;
       p.slots[out] = s;
@@ -412,6 +498,8 @@ float* Graph::ptr_of(Plan& p, int v) {
     if (p.input_ids[i] == v) return p.bound_in[i];
   for (size_t i = 0; i < p.output_ids.size(); i++)
     if (p.output_ids[i] == v) return p.bound_out[i];
+  auto pit = p.padded.find(v);
+  if (pit != p.padded.end()) return pit->second.base;
   auto it = p.slots.find(v);
   if (it == p.slots.end()) return nullptr;
   if (it->second.offset == SIZE_MAX) {
@@ -453,16 +541,14 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     return RTENHIP_OK;
   }
   if (t == "Conv") {
+    auto cit = p.convs.find(op_id);
+    if (cit != p.convs.end() && ctx->use_dma) return exec_conv_dma(p, op_id, cit->second);
+    if (p.padded.count(n.inputs[0]) || p.padded.count(out))
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "zero-bordered value needs the DMA conv path");
     rtenhip_tensor w = T(n.inputs[1]);
-    std::string ap = n.attrs.str("auto_pad", "notset");
-    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
-    bool one_d = x.ndim == 3;
-    auto pads = n.attrs.ints("pads", one_d ? std::vector<int64_t>{0, 0} : std::vector<int64_t>{0, 0, 0, 0});
-    auto strides = n.attrs.ints("strides", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
-    auto dil = n.attrs.ints("dilations", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
-    return conv_impl(ctx, &x, &w, P(2), mode, pads.data(), strides.data(), dil.data(),
-                     (int64_t)n.attrs.num("groups", 1), ptr_of(p, n.fused_residual), n.fused_act,
-                     n.act_lo, n.act_hi, &y);
+    ConvAttrs ca = conv_attrs(n, x.ndim == 3);
+    return conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(),
+                     ca.groups, ptr_of(p, n.fused_residual), n.fused_act, n.act_lo, n.act_hi, &y);
   }
   if (is_unary(t)) {
     int op = t == "Relu" ? RTENHIP_UNARY_RELU : t == "Clip" ? RTENHIP_UNARY_CLIP
@@ -538,6 +624,118 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   std::string msg = "Unsupported operator type: " + t;
   set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
   return RTENHIP_UNSUPPORTED_VALUE;
+}
+
+// DMA conv with plan-owned packed weights and zero-bordered inputs/outputs.
+// On the plan's first (eager) run the kernel configuration is chosen by
+// timing the candidates on the real operands; all configurations give
+// bit-identical results, so this only affects speed.
+rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
+  const Node& n = nodes[op_id];
+  const ConvPlan& g = ce.g;
+  hipStream_t s = ctx->stream;
+  const int64_t P = g.oh * g.ow;
+  ConvDmaArgs a{};
+  // Input: zero-bordered by its producer, padded here, or used as is.
+  const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
+  auto pin = p.padded.find(n.inputs[0]);
+  if (pin != p.padded.end()) {
+    a.xin = pin->second.base;
+    a.Hp = pin->second.phys[2];
+    a.Wp = pin->second.phys[3];
+  } else if (has_pad) {
+    a.Hp = g.H + g.pads[0] + g.pads[2];
+    a.Wp = g.W + g.pads[1] + g.pads[3];
+    float* xp = ctx->scratch_floats((size_t)(g.N * g.C * a.Hp * a.Wp), 1);
+    if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    rtenhip_status st = launch_pad_nchw(ptr_of(p, n.inputs[0]), xp, g.N * g.C, (int)g.H, (int)g.W,
+                                        (int)g.pads[0], (int)g.pads[1], (int)g.pads[2],
+                                        (int)g.pads[3], s);
+    if (st) return st;
+    a.xin = xp;
+  } else {
+    a.xin = ptr_of(p, n.inputs[0]);
+    a.Hp = g.H;
+    a.Wp = g.W;
+  }
+  a.N = g.N;
+  a.C = g.C;
+  a.O = g.O;
+  a.kh = g.kh;
+  a.kw = g.kw;
+  a.sh = g.sh;
+  a.sw = g.sw;
+  a.dh = g.dh;
+  a.dw = g.dw;
+  a.oh = g.oh;
+  a.ow = g.ow;
+  a.groups = g.groups;
+  a.bias = n.inputs.size() > 2 ? ptr_of(p, n.inputs[2]) : nullptr;
+  a.residual = ptr_of(p, n.fused_residual);
+  a.act = n.fused_act;
+  a.lo = n.act_lo;
+  a.hi = n.act_hi;
+  const int out = n.outputs[0];
+  auto pout = p.padded.find(out);
+  if (pout != p.padded.end()) {
+    const PaddedValue& pv = pout->second;
+    a.y = pv.base;
+    a.y_img = pv.phys[1] * pv.phys[2] * pv.phys[3];
+    a.y_row = pv.phys[3];
+    a.y_off = pv.pads[0] * pv.phys[3] + pv.pads[1];
+  } else {
+    a.y = ptr_of(p, out);
+    a.y_img = g.O * P;
+  }
+  const float* w = ptr_of(p, n.inputs[1]);
+  if (ce.cfg < 0) {
+    const int64_t opg = g.O / g.groups, K = (g.C / g.groups) * g.kh * g.kw;
+    int chosen = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cs);
+    if (autotune && cs == hipStreamCaptureStatusNone) {
+      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10};
+      hipEvent_t e0, e1;
+      RTENHIP_HIP_CHECK(hipEventCreate(&e0));
+      RTENHIP_HIP_CHECK(hipEventCreate(&e1));
+      float best_ms = 1e30f;
+      std::vector<float*> bufs;
+      for (int cfg : kCandidates) {
+        if (cfg >= dma_num_cfgs()) continue;
+        float* pk = nullptr;
+        RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)packed_conv_weight_floats(g, cfg) * 4));
+        bufs.push_back(pk);
+        rtenhip_status st = pack_conv_weights(ctx, w, g, cfg, pk);
+        if (st) return st;
+        a.packed_w = pk;
+        a.cfg = cfg;
+        st = conv_dma(ctx, a);  // warm-up
+        if (st) return st;
+        RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
+        for (int r = 0; r < 2 && !st; r++) st = conv_dma(ctx, a);
+        if (st) return st;
+        RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
+        RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        RTENHIP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best_ms) {
+          best_ms = ms;
+          chosen = cfg;
+        }
+      }
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
+      for (float* b : bufs) (void)hipFree(b);
+    }
+    RTENHIP_HIP_CHECK(hipMalloc(&ce.packed, (size_t)packed_conv_weight_floats(g, chosen) * 4));
+    rtenhip_status st = pack_conv_weights(ctx, w, g, chosen, ce.packed);
+    if (st) return st;
+    ce.cfg = chosen;
+  }
+  a.packed_w = ce.packed;
+  a.cfg = ce.cfg;
+  return conv_dma(ctx, a);
 }
 
 rtenhip_status Graph::find_plan(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
@@ -679,9 +877,11 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       (void)hipStreamSynchronize(exec_stream);
       std::map<std::string, std::pair<double, int>> tot;
       double total = 0;
+      std::vector<float> per_op(evs.size(), 0.f);
       for (size_t i = 0; i < evs.size(); i++) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
+        per_op[i] = ms;
         const Node& n = nodes[plan->ops[i]];
         std::string key = n.op_type;
         if (n.op_type == "Conv" && (n.fused_residual >= 0 || n.fused_act)) key = "Conv(fused)";
@@ -704,6 +904,20 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       for (auto& r : rows) {
         snprintf(buf, sizeof buf, "%-22s %10.3f ms (%5.2f%%)  x%d\n", r.second.c_str(), r.first,
                  total > 0 ? 100.0 * r.first / total : 0.0, tot[r.second].second);
+        os << buf;
+      }
+      // Per-op rows (RTEN_TIMING "by-shape" analogue): name, type, output shape.
+      os << "--- per op ---\n";
+      for (size_t i = 0; i < evs.size(); i++) {
+        const Node& n = nodes[plan->ops[i]];
+        const float ms = per_op[i];
+        std::string shp;
+        auto it = plan->slots.find(n.outputs[0]);
+        if (it != plan->slots.end())
+          for (size_t d = 0; d < it->second.shape.size(); d++)
+            shp += (d ? "x" : "") + std::to_string(it->second.shape[d]);
+        snprintf(buf, sizeof buf, "op %-28s %-12s %-20s %9.4f ms\n", n.name.c_str(),
+                 n.op_type.c_str(), shp.c_str(), ms);
         os << buf;
       }
       timing_report = os.str();
@@ -822,6 +1036,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   g->cptr = ctx;
   if (const char* s = getenv("RTEN_TIMING")) g->timing = s[0] != 0 && s[0] != '0';
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
+  if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

@@ -70,8 +70,28 @@ struct Slot {
   Shape shape;
 };
 
+// A Conv the plan runs on the LDS-DMA GEMM (see exec_op).
+struct ConvExec {
+  ConvPlan g;
+  int cfg = -1;             // kernel configuration (chosen on the first run)
+  float* packed = nullptr;  // weights packed for cfg, owned by the plan
+};
+
+// A value stored with a zero border so the DMA convs reading it need no
+// per-run padding copy: physical [N, C, H + pt + pb, W + pl + pr], written by
+// its producer (a DMA conv) into the interior.  Persistent, outside the arena,
+// so the border stays zero.
+struct PaddedValue {
+  float* base = nullptr;
+  int64_t pads[4] = {0, 0, 0, 0};
+  Shape phys;
+};
+
 struct Plan {
+  ~Plan();
   std::vector<int> ops;               // topological order
+  std::map<int, ConvExec> convs;      // op id -> DMA conv state
+  std::map<int, PaddedValue> padded;  // value id -> zero-bordered storage
   std::map<int, Slot> slots;          // value id -> storage
   size_t arena_bytes = 0;
   std::vector<int> input_ids, output_ids;
@@ -95,6 +115,7 @@ struct Graph {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
   bool use_hip_graph = true;
+  bool autotune = true;  // time DMA conv configurations on a plan's first run
   std::string timing_report;
   std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
 
@@ -114,6 +135,7 @@ struct Graph {
   rtenhip_status infer_shapes(int op_id, const std::vector<const Shape*>& ins,
                               std::vector<Shape>& outs);
   rtenhip_status exec_op(Plan& p, int op_id);
+  rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
   float* ptr_of(Plan& p, int value_id);
 };
 

@@ -350,3 +350,18 @@ def test_kats_on_gpu(rh):
         x = np.array(KATS["max_pool"][0]["x"], np.float32).reshape(1, 1, 4, 4)
         y = host(rh.max_pool(dev(x), case["kernel"], case["strides"]))
         assert np.allclose(y.ravel(), case["y"])
+
+
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv_bitexact_general_kernel(rh, oracle, case):
+    """The register-staged general kernel (DMA path off) is bit-exact too."""
+    import ctypes
+
+    lib = rh.lib()
+    lib.rtenhip_debug_set_dma.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx = rh.default_context()
+    lib.rtenhip_debug_set_dma(ctypes.c_void_p(ctx.ptr), 0)
+    try:
+        test_conv_bitexact(rh, oracle, case)
+    finally:
+        lib.rtenhip_debug_set_dma(ctypes.c_void_p(ctx.ptr), 1)
