@@ -91,7 +91,8 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_add_constant", "rtenhip_graph_add_op", "rtenhip_graph_optimize",
     "rtenhip_graph_run", "rtenhip_graph_value_shape", "rtenhip_graph_set_timing",
     "rtenhip_graph_timing_report", "rtenhip_model_load", "rtenhip_model_input_ids",
-    "rtenhip_model_output_ids", "rtenhip_graph_node_id",
+    "rtenhip_model_output_ids", "rtenhip_graph_node_id", "rtenhip_graph_set_io",
+    "rtenhip_graph_plan",
 ]
 
 

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--dmamode", type=int, default=0,
                     help="timing experiment: 1 = no K-loop DMA, 2 = no MFMA (wrong results)")
     ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--shape", action="append", default=[],
+                    help="extra conv N,C,H,W,O,k,stride,pad (repeatable); replaces the model's layers")
     args = ap.parse_args()
     lib = rten_hip.lib()
     lib.rtenhip_debug_set_gemm_config.argtypes = [ctypes.c_int]
@@ -60,6 +62,11 @@ def main():
             shapes[n.outputs[0]] = (xs[0], xs[1], 1, 1)
         else:
             shapes[n.outputs[0]] = xs
+    if args.shape:
+        layers = {}
+        for sh in args.shape:
+            N, Cc, H, W, O, k, st, pd = [int(v) for v in sh.split(",")]
+            layers[((N, Cc, H, W), (O, Cc, k, k), (pd,) * 4, (st, st), 1)] = [1, f"custom{len(layers)}"]
     cfgs = args.cfgs.split(",")
     rng = np.random.default_rng(0)
     total = {c: 0.0 for c in cfgs}
