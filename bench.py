@@ -84,6 +84,20 @@ def cpu_baseline(spec, seconds: float):
     }
 
 
+def traffic_bytes(model, batch):
+    """HBM bytes per step of the conv GEMM kernels, from the committed
+    rocprofv3 PMC summary (scripts/gpu_traffic.sh -> tools/pmc_traffic.py):
+    FETCH_SIZE x2 (gfx950) + WRITE_SIZE.  None when no summary exists for
+    this workload."""
+    path = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+    if model != "resnet50" or batch != 64 or not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path))["conv_gemm_bytes_per_forward"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def main():
     args = parse()
     import numpy as np
@@ -111,13 +125,20 @@ def main():
     flops_per_img = models.conv_flops(spec, 1)
     rng = np.random.default_rng(1234 + rank)
     x = torch.from_numpy(rng.random((B, 3, 224, 224), dtype=np.float32)).cuda()
-    (out,) = g.run({g.input_ids[0]: x}, g.output_ids)
-    gathered = torch.empty((world * B, out.shape[1]), dtype=torch.float32, device=x.device)
+    (out,) = g.run({g.input_ids[0]: x}, g.output_ids)  # plans + tunes conv kernels
+
+    from rten_hip.parallel import BatchShardRunner
+
+    def forward(xb):
+        g.run({g.input_ids[0]: xb}, g.output_ids, out=[out])
+        return out
+
+    # Rank r holds images [r*B, (r+1)*B) of the world*B job; the only
+    # exchange is the all-gather of logits (RCCL) inside runner.run.
+    runner = BatchShardRunner(forward)
 
     def step():
-        g.run({g.input_ids[0]: x}, g.output_ids, out=[out])
-        if dist is not None:
-            dist.all_gather_into_tensor(gathered, out)
+        runner.run(x, world * B)
 
     for _ in range(args.warmup):
         step()
@@ -181,8 +202,9 @@ def main():
                        "parallelism": f"batch-shard x{world} (replicated weights, RCCL all-gather of logits)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                          "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                         "kernel": "gemm_mfma_kernel (all Conv+Gemm launches)",
+                         "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                         "traffic": traffic_bytes(args.model, B),
+                         "kernel": "gemm_dma_kernel (all 53 Conv launches) + FC Gemm",
                          "flops_per_step": gemm_flops,
                          "kernel_ms_per_step": round(conv_ms, 4),
                          "model_frac": round(value / world * flops_per_img / 1e12 /
