@@ -139,6 +139,11 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     d.bias = a.bias ? a.bias + g * opg : nullptr;
     d.alpha = 1.f;
     d.beta = 0.f;
+    d.vec4 = (P % 4 == 0 && d.out_c == P && d.out_row == a.ow && d.out_off == 0 &&
+              d.out_img % 4 == 0 && d.res_img % 4 == 0 && g * opg * P % 4 == 0 &&
+              ((uintptr_t)a.y % 16) == 0 && (!a.residual || ((uintptr_t)a.residual % 16) == 0))
+                 ? 1
+                 : 0;
     d.act = a.act;
     d.act_lo = a.lo;
     d.act_hi = a.hi;

@@ -45,6 +45,8 @@ struct DmaDesc {
   float alpha, beta;
   int act;
   float act_lo, act_hi;
+  int vec4;                 // outputs/residual row-contiguous with P % 4 == 0, unpadded:
+                            // 16-byte epilogue accesses (no cin)
   int dbg;                  // tuning experiments only: 1 = no K-loop DMA, 2 = no MFMA
 };
 

@@ -274,6 +274,67 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   }
 
   // ---- epilogue ----
+  auto apply_act = [&](float x) __attribute__((always_inline)) {
+    if (d.act == RTENHIP_ACT_RELU) {
+      x = fmaxf(x, 0.f);
+    } else if (d.act == RTENHIP_ACT_CLIP) {
+      x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+    }
+    return x;
+  };
+  constexpr bool VEC_FITS = NW * 1024 <= STAGES * STAGE;
+  if (VEC_FITS && d.vec4) {
+    // Row-contiguous outputs (P % 4 == 0, unpadded): each 32x32 accumulator
+    // block is transposed through this wave's LDS slot so every lane stores
+    // (and loads the residual as) 16-byte row segments: 4 dwordx4 per block
+    // instead of 16 dword accesses.  Same per-element arithmetic as below.
+    __syncthreads();  // every wave is done reading the K stages
+    float* slot = lds + wave * 1024;
+    const int rr = lane >> 3;        // row within an 8-row group
+    const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++) {
+        f32x16 v;
+        if constexpr (MULTI_KB) {
+          v = sum[mi][ni];
+        } else {
+          first_block(v, acc[mi][ni], mi, ni);
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) slot[((j & 3) + 8 * (j >> 2) + 4 * half) * 32 + l32] = v[j];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int n = tn + wn + ni * 32 + c4;
+        const bool ncol_ok = n <= N - 1;  // N % 4 == 0: the whole segment is in range
+        const int nn = ncol_ok ? n : 0;
+        const int img = nn / d.P;
+        const int p = nn - img * d.P;
+        const int64_t obase = (int64_t)img * d.out_img + p;
+        const int64_t rbase = (int64_t)img * d.res_img + p;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          const int row = i * 8 + rr;
+          const int m = tm + wm + mi * 32 + row;
+          const bool ok = ncol_ok && m < M;
+          float4 x = *(const float4*)(slot + row * 32 + c4);
+          if (d.residual && ok) {
+            const float4 r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
+            x.x = __fadd_rn(x.x, r.x);
+            x.y = __fadd_rn(x.y, r.y);
+            x.z = __fadd_rn(x.z, r.z);
+            x.w = __fadd_rn(x.w, r.w);
+          }
+          x.x = apply_act(x.x);
+          x.y = apply_act(x.y);
+          x.z = apply_act(x.z);
+          x.w = apply_act(x.w);
+          if (ok) *(float4*)(d.out + obase + (int64_t)m * d.out_c) = x;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    return;
+  }
   const bool full_tile = m_lim >= BM - 1 && n_lim >= BN - 1;
 #pragma unroll
   for (int ni = 0; ni < NI; ni++) {
@@ -300,11 +361,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         const bool ok = full_tile || (ncol_ok && ml <= m_lim);
         float x = v[j];
         if (d.residual) x = __fadd_rn(x, d.residual[ok ? rbase + (int64_t)(tm + ml) * d.res_c : 0]);
-        if (d.act == RTENHIP_ACT_RELU) {
-          x = fmaxf(x, 0.f);
-        } else if (d.act == RTENHIP_ACT_CLIP) {
-          x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
-        }
+        x = apply_act(x);
         if (ok) d.out[obase + (int64_t)(tm + ml) * d.out_c] = x;
       }
     }
