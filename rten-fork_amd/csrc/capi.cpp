@@ -507,6 +507,11 @@ rtenhip_status gemm_impl(Ctx* c, int64_t m, int64_t n, int64_t k, const float* a
     d.a = nullptr;
     d.bias = nullptr;
   }
+  if (gemm_smallm_eligible(d)) {
+    float* ws = c->scratch_floats((size_t)gemm_smallm_ws_floats(d), 3);
+    if (!ws) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    return launch_gemm_smallm(d, ws, s);
+  }
   return launch_gemm(d, s);
 }
 

@@ -88,6 +88,10 @@ struct GemmDesc {
   int nbp;
   int64_t pshape[4], pa[4], pb[4], po[4];
 };
+// Small-M GEMM split at KC blocks (workspace = gemm_smallm_ws_floats).
+bool gemm_smallm_eligible(const GemmDesc& d);
+int64_t gemm_smallm_ws_floats(const GemmDesc& d);
+rtenhip_status launch_gemm_smallm(const GemmDesc& d, float* ws, hipStream_t s);
 rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s);
 
 // gemv with the reference's summation order (gemm.rs:651-704, kernels.rs:26-194).

@@ -359,8 +359,111 @@ __global__ void gemm_k0_kernel(float* out, int64_t out_m, int M, int N, float be
   }
 }
 
+// Small-M dense GEMM (the FC layer: M = batch <= 64, N = 1000, K = 2048).
+// MFMA tiles would leave most CUs idle at this size, so the K blocks are
+// split across workgroups instead -- exactly at the reference's KC = 256
+// boundaries, which keeps the arithmetic identical: kernel 1 computes each
+// block's fma chain from +0 in k order (one lane per row m, four columns per
+// wave, B read as wave-uniform scalar loads) into a workspace; kernel 2 folds
+// the block chains in order: fma(c0, alpha, beta*cin) or alpha*c0, + bias[m],
+// then fma(c_b, alpha, sum) (gemm.rs:1004-1050).
+typedef __attribute__((address_space(4))) const float const_float_t;
+
+template <bool UNIT>  // a_k == 1 and b_k == 1 (row-major A, B = W^T view)
+__global__ __launch_bounds__(256) void gemm_kblock_kernel(GemmDesc d, float* __restrict__ ws) {
+  constexpr int COLS = 4;  // columns per wave
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int kb = blockIdx.y;
+  const int n0 = blockIdx.x * (4 * COLS) + w * COLS;
+  const int m = min(lane, d.M - 1);
+  const int k0 = kb * 256, k1 = min(d.K, k0 + 256);
+  const float* ap = d.a + (int64_t)m * d.a_m;
+  const_float_t* bp = (const_float_t*)d.b;
+  const int64_t ak = UNIT ? 1 : d.a_k, bk = UNIT ? 1 : d.b_k;
+  float c[COLS];
+#pragma unroll
+  for (int j = 0; j < COLS; j++) c[j] = 0.f;
+  int nn[COLS];
+#pragma unroll
+  for (int j = 0; j < COLS; j++) nn[j] = min(n0 + j, d.N - 1);
+  // Chunks of 16 k: all loads of a chunk are issued before its fma chain.
+  int k = k0;
+  for (; k + 16 <= k1; k += 16) {
+    float av[16], bv[16][COLS];
+#pragma unroll
+    for (int t = 0; t < 16; t++) av[t] = ap[(int64_t)(k + t) * ak];
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+#pragma unroll
+      for (int j = 0; j < COLS; j++) bv[t][j] = bp[(int64_t)(k + t) * bk + (int64_t)nn[j] * d.b_n];
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+#pragma unroll
+      for (int j = 0; j < COLS; j++) c[j] = __fmaf_rn(av[t], bv[t][j], c[j]);
+  }
+  for (; k < k1; k++) {
+    const float av = ap[(int64_t)k * d.a_k];
+#pragma unroll
+    for (int j = 0; j < COLS; j++)
+      c[j] = __fmaf_rn(av, bp[(int64_t)k * d.b_k + (int64_t)nn[j] * d.b_n], c[j]);
+  }
+  if (lane >= d.M) return;
+#pragma unroll
+  for (int j = 0; j < COLS; j++)
+    if (n0 + j < d.N) ws[((int64_t)kb * d.M + lane) * d.N + n0 + j] = c[j];
+}
+
+__global__ __launch_bounds__(256) void gemm_kfold_kernel(GemmDesc d, const float* __restrict__ ws,
+                                                         int nkb) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t MN = (int64_t)d.M * d.N;
+  if (i >= MN) return;
+  const int m = (int)(i / d.N), n = (int)(i - (int64_t)m * d.N);
+  const float c0 = ws[i];
+  float x;
+  if (d.cin) {
+    x = __fmaf_rn(c0, d.alpha, __fmul_rn(d.cin[(int64_t)m * d.out_m + n], d.beta));
+  } else {
+    x = __fmul_rn(c0, d.alpha);
+  }
+  if (d.bias) x = __fadd_rn(x, d.bias[m]);
+  for (int kb = 1; kb < nkb; kb++) x = __fmaf_rn(ws[kb * MN + i], d.alpha, x);
+  if (d.act == RTENHIP_ACT_RELU) {
+    x = fmaxf(x, 0.f);
+  } else if (d.act == RTENHIP_ACT_CLIP) {
+    x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+  }
+  d.out[(int64_t)m * d.out_m + n] = x;
+}
+
+bool gemm_smallm_eligible(const GemmDesc& d) {
+  return d.K > 0 && d.bmode == 0 && d.nbatch <= 1 && !d.residual && d.M <= 64 && d.N >= 64 &&
+         (int64_t)d.M * d.N <= (int64_t(1) << 20) && g_forced_cfg < 0;
+}
+
+int64_t gemm_smallm_ws_floats(const GemmDesc& d) {
+  return (int64_t)((d.K + 255) / 256) * d.M * d.N;
+}
+
+rtenhip_status launch_gemm_smallm(const GemmDesc& d, float* ws, hipStream_t s) {
+  const int nkb = (d.K + 255) / 256;
+  dim3 grid((d.N + 15) / 16, nkb);
+  if (d.a_k == 1 && d.b_k == 1)
+    hipLaunchKernelGGL(gemm_kblock_kernel<true>, grid, dim3(256), 0, s, d, ws);
+  else
+    hipLaunchKernelGGL(gemm_kblock_kernel<false>, grid, dim3(256), 0, s, d, ws);
+  RTENHIP_LAUNCH_CHECK();
+  const int64_t MN = (int64_t)d.M * d.N;
+  hipLaunchKernelGGL(gemm_kfold_kernel, dim3((unsigned)((MN + 255) / 256)), dim3(256), 0, s, d,
+                     (const float*)ws, nkb);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s) {
   if (d.M <= 0 || d.N <= 0) return RTENHIP_OK;
+
   if (d.K <= 0) {
     // The tiled kernel issues clamped loads and needs K >= 1.
     if (d.bmode != 0) return RTENHIP_OK;

@@ -75,6 +75,10 @@ Plan::~Plan() {
     if (kv.second.packed) (void)hipFree(kv.second.packed);
   for (auto& kv : padded)
     if (kv.second.base) (void)hipFree(kv.second.base);
+  for (auto& kv : side_events) {
+    if (kv.second.first) (void)hipEventDestroy(kv.second.first);
+    if (kv.second.second) (void)hipEventDestroy(kv.second.second);
+  }
 }
 
 // Conv attributes as conv_impl takes them.
@@ -101,6 +105,7 @@ Graph::~Graph() {
     if (n.kind == NodeKind::Constant && n.dev && n.owns_dev) (void)hipFree(n.dev);
   if (arena) (void)hipFree(arena);
   if (exec_stream) (void)hipStreamDestroy(exec_stream);
+  if (side_stream) (void)hipStreamDestroy(side_stream);
   if (ev_in) (void)hipEventDestroy(ev_in);
   if (ev_out) (void)hipEventDestroy(ev_out);
 }
@@ -377,6 +382,65 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     }
   }
 
+  // Independent branches: a DMA conv whose inputs were ready two or more ops
+  // before its plan position (the ResNet downsample conv: DFS visits it right
+  // before the conv3 that consumes it) moves up to just after its last
+  // producer and runs on the side stream, concurrently with the main chain;
+  // its first consumer joins it.  Only convs that need no ctx scratch.
+  if (use_side_stream) {
+    std::map<int, int> producer_op;
+    for (int op : p.ops)
+      for (int o : nodes[op].outputs) producer_op[o] = op;
+    std::vector<int> order = p.ops;
+    for (size_t i = 0; i < order.size(); i++) {
+      const int op = order[i];
+      auto cit = p.convs.find(op);
+      if (cit == p.convs.end()) continue;
+      const Node& n = nodes[op];
+      const ConvPlan& g = cit->second.g;
+      const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
+      if (has_pad && !p.padded.count(n.inputs[0])) continue;
+      int last = -1;
+      std::vector<int> deps(n.inputs.begin(), n.inputs.end());
+      if (n.fused_residual >= 0) deps.push_back(n.fused_residual);
+      for (int v : deps) {
+        if (v < 0) continue;
+        auto pit = producer_op.find(v);
+        if (pit == producer_op.end()) continue;
+        for (size_t j = 0; j < i; j++)
+          if (order[j] == pit->second) last = std::max(last, (int)j);
+      }
+      if ((int)i - last < 3) continue;
+      order.erase(order.begin() + i);
+      order.insert(order.begin() + last + 1, op);
+      p.side.insert(op);
+    }
+    p.ops = order;
+    for (int d : p.side) {
+      const int v = nodes[d].outputs[0];
+      bool joined = false;
+      bool after = false;
+      for (int op : p.ops) {
+        if (op == d) {
+          after = true;
+          continue;
+        }
+        if (!after) continue;
+        const Node& n = nodes[op];
+        bool reads = n.fused_residual == v;
+        for (int i : n.inputs) reads = reads || i == v;
+        if (reads) {
+          p.joins[op].push_back(d);
+          joined = true;
+          break;
+        }
+      }
+      if (!joined) p.joins[-1].push_back(d);  // graph output: joined at the end of run
+    }
+  }
+  // Inputs of a side op stay allocated until its join.
+  std::map<int, std::vector<int>> deferred_drops;  // join op -> values
+
   // Storage blocks with best-fit reuse; aliases share their base's block.
   struct Block {
     size_t off, size;
@@ -471,9 +535,24 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       s.offset = off;
       p.slots[out] = s;
     }
-    for (int i : n.inputs)
-      if (i >= 0) drop_use(i);
-    if (n.fused_residual >= 0) drop_use(n.fused_residual);
+    if (p.side.count(op)) {
+      int join = -1;
+      for (auto& kv : p.joins)
+        for (int d : kv.second)
+          if (d == op) join = kv.first;
+      for (int i : n.inputs)
+        if (i >= 0) deferred_drops[join].push_back(i);
+      if (n.fused_residual >= 0) deferred_drops[join].push_back(n.fused_residual);
+    } else {
+      for (int i : n.inputs)
+        if (i >= 0) drop_use(i);
+      if (n.fused_residual >= 0) drop_use(n.fused_residual);
+    }
+    auto dd = deferred_drops.find(op);
+    if (dd != deferred_drops.end()) {
+      for (int v : dd->second) drop_use(v);
+      deferred_drops.erase(dd);
+    }
     // An output nobody reads is released right after its producer.
     if (block_of.count(out) && blocks[block_of[out]].refs == 0) {
       Block& b = blocks[block_of[out]];
@@ -799,6 +878,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   hipStream_t caller = ctx->stream;
   if (!exec_stream) {
     RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&exec_stream, hipStreamNonBlocking));
+    RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
     RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
   }
@@ -822,10 +902,46 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   plan->bound_in = bin;
   plan->bound_out = bout;
 
+  for (int d : plan->side) {
+    auto& ev = plan->side_events[d];
+    if (!ev.first) RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev.first, hipEventDisableTiming));
+    if (!ev.second) RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev.second, hipEventDisableTiming));
+  }
   RTENHIP_HIP_CHECK(hipEventRecord(ev_in, caller));
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, ev_in, 0));
   ctx->stream = exec_stream;
   rtenhip_status st = RTENHIP_OK;
+  // Launch one op on its stream: side ops fork from the main stream and
+  // record completion; a join op first waits for the side ops it reads.
+  auto stream_of = [&](int op) { return plan->side.count(op) ? side_stream : exec_stream; };
+  auto before_op = [&](int op) -> rtenhip_status {
+    if (plan->side.count(op)) {
+      auto& ev = plan->side_events[op];
+      RTENHIP_HIP_CHECK(hipEventRecord(ev.first, exec_stream));
+      RTENHIP_HIP_CHECK(hipStreamWaitEvent(side_stream, ev.first, 0));
+      ctx->stream = side_stream;
+    } else {
+      auto j = plan->joins.find(op);
+      if (j != plan->joins.end())
+        for (int d : j->second)
+          RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, plan->side_events[d].second, 0));
+    }
+    return RTENHIP_OK;
+  };
+  auto after_op = [&](int op) -> rtenhip_status {
+    if (plan->side.count(op)) {
+      RTENHIP_HIP_CHECK(hipEventRecord(plan->side_events[op].second, side_stream));
+      ctx->stream = exec_stream;
+    }
+    return RTENHIP_OK;
+  };
+  auto join_all = [&]() -> rtenhip_status {
+    auto j = plan->joins.find(-1);
+    if (j != plan->joins.end())
+      for (int d : j->second)
+        RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, plan->side_events[d].second, 0));
+    return RTENHIP_OK;
+  };
   const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
   if (replay) {
     if (!same_binding) {
@@ -837,9 +953,13 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       hipError_t e = hipStreamBeginCapture(exec_stream, hipStreamCaptureModeThreadLocal);
       if (e == hipSuccess) {
         for (int op : plan->ops) {
-          st = exec_op(*plan, op);
+          st = before_op(op);
+          if (!st) st = exec_op(*plan, op);
+          if (!st) st = after_op(op);
           if (st) break;
         }
+        if (!st) st = join_all();
+        ctx->stream = exec_stream;
         hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
         if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&plan->exec, g, nullptr, nullptr, 0);
         if (g) (void)hipGraphDestroy(g);
@@ -856,22 +976,27 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
     for (int op : plan->ops) {
       hipEvent_t a = nullptr, b = nullptr;
+      st = before_op(op);
+      if (st) break;
       if (timing) {
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
-        (void)hipEventRecord(a, exec_stream);
+        (void)hipEventRecord(a, stream_of(op));
       }
       st = exec_op(*plan, op);
       if (timing) {
-        (void)hipEventRecord(b, exec_stream);
+        (void)hipEventRecord(b, stream_of(op));
         evs.push_back({a, b});
       }
+      if (!st) st = after_op(op);
       if (st) {
         std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
         set_error(st, msg);
         break;
       }
     }
+    ctx->stream = exec_stream;
+    if (!st) st = join_all();
     plan->eager_runs++;
     if (timing && !st) {
       (void)hipStreamSynchronize(exec_stream);
@@ -1037,6 +1162,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTEN_TIMING")) g->timing = s[0] != 0 && s[0] != '0';
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
+  if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->use_side_stream = s[0] != '0';
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <vector>
@@ -92,6 +93,11 @@ struct Plan {
   std::vector<int> ops;               // topological order
   std::map<int, ConvExec> convs;      // op id -> DMA conv state
   std::map<int, PaddedValue> padded;  // value id -> zero-bordered storage
+  // Ops launched on the side stream (independent branches such as the
+  // ResNet downsample conv), and for each op the side ops it must wait for.
+  std::set<int> side;
+  std::map<int, std::vector<int>> joins;
+  std::map<int, std::pair<hipEvent_t, hipEvent_t>> side_events;  // op -> (fork, done)
   std::map<int, Slot> slots;          // value id -> storage
   size_t arena_bytes = 0;
   std::vector<int> input_ids, output_ids;
@@ -112,6 +118,8 @@ struct Graph {
   void* arena = nullptr;
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
+  hipStream_t side_stream = nullptr;
+  bool use_side_stream = true;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
   bool use_hip_graph = true;

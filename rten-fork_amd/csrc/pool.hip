@@ -14,16 +14,17 @@
 
 namespace rtenhip {
 
-template <bool IS_MAX>
-__global__ void pool_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t total,
+template <bool IS_MAX, typename IDX>
+__global__ void pool_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t total_,
                             int H, int W, int OH, int OW, int kh, int kw, int sh, int sw, int pt,
                             int pl, int count_include_pad) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+  const IDX total = (IDX)total_;
+  const IDX stride = (IDX)gridDim.x * blockDim.x;
+  for (IDX i = (IDX)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
     const int ox = (int)(i % OW);
     const int oy = (int)((i / OW) % OH);
-    const int64_t plane = i / ((int64_t)OW * OH);
-    const float* xp = x + plane * H * W;
+    const IDX plane = i / ((IDX)OW * OH);
+    const float* xp = x + (int64_t)plane * H * W;
     float acc = IS_MAX ? -__builtin_huge_valf() : 0.f;
     int cnt = 0;
     for (int ky = 0; ky < kh; ky++) {
@@ -47,13 +48,26 @@ rtenhip_status launch_pool(int is_max, const float* x, float* y, int64_t NC, int
                            int count_include_pad, hipStream_t s) {
   const int64_t total = NC * OH * OW;
   if (total == 0) return RTENHIP_OK;
+  int64_t blocks32 = (total + 255) / 256;
+  if (blocks32 > 8192) blocks32 = 8192;
+  if (total + blocks32 * 256 < (int64_t(1) << 31) && NC * H * W < (int64_t(1) << 31)) {
+    // 32-bit index math (the 64-bit divisions dominate the 64-bit variant).
+    if (is_max)
+      hipLaunchKernelGGL((pool_kernel<true, int>), dim3((unsigned)blocks32), dim3(256), 0, s, x, y,
+                         total, H, W, OH, OW, kh, kw, sh, sw, pt, pl, count_include_pad);
+    else
+      hipLaunchKernelGGL((pool_kernel<false, int>), dim3((unsigned)blocks32), dim3(256), 0, s, x, y,
+                         total, H, W, OH, OW, kh, kw, sh, sw, pt, pl, count_include_pad);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   int64_t blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (is_max)
-    hipLaunchKernelGGL(pool_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, s, x, y, total, H,
+    hipLaunchKernelGGL((pool_kernel<true, int64_t>), dim3((unsigned)blocks), dim3(256), 0, s, x, y, total, H,
                        W, OH, OW, kh, kw, sh, sw, pt, pl, count_include_pad);
   else
-    hipLaunchKernelGGL(pool_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, s, x, y, total, H,
+    hipLaunchKernelGGL((pool_kernel<false, int64_t>), dim3((unsigned)blocks), dim3(256), 0, s, x, y, total, H,
                        W, OH, OW, kh, kw, sh, sw, pt, pl, count_include_pad);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
