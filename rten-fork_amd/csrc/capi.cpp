@@ -50,6 +50,7 @@ Ctx::~Ctx() {
   for (auto& kv : ktabs) (void)hipFree(kv.second);
   for (auto& kv : dtabs) (void)hipFree(kv.second);
   for (auto& kv : packed_cache) (void)hipFree(kv.second);
+  if (counters) (void)hipFree(counters);
   for (int i = 0; i < NSLOTS; i++)
     if (slots[i]) (void)hipFree(slots[i]);
 }
@@ -67,6 +68,19 @@ float* Ctx::scratch_floats(size_t n, size_t slot) {
     slot_cap[slot] = cap;
   }
   return static_cast<float*>(slots[slot]);
+}
+
+int* Ctx::split_counters(size_t n) {
+  if (n > counters_cap || !counters) {
+    if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+    if (counters) (void)hipFree(counters);
+    counters = nullptr;
+    size_t cap = n + 64;
+    if (hipMalloc(&counters, cap * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemset(counters, 0, cap * sizeof(int)) != hipSuccess) return nullptr;
+    counters_cap = cap;
+  }
+  return counters;
 }
 
 const int* Ctx::dtab(int C, int H, int W, int kh, int kw, int dh, int dw) {
@@ -122,7 +136,6 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     d.OW = (int)a.ow;
     d.P = (int)P;
     d.ktab4 = tab;
-    d.out = a.y + g * opg * P;
     d.out_img = a.y_img;
     d.out_c = P;  // channel stride of an unpadded output plane
     d.out_row = a.ow;
@@ -133,6 +146,7 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
       d.out_row = a.y_row;
       d.out_off = a.y_off;
     }
+    d.out = a.y + g * opg * d.out_c;
     d.residual = a.residual ? a.residual + g * opg * P : nullptr;
     d.res_img = a.O * P;
     d.res_c = P;
@@ -147,6 +161,16 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     d.act = a.act;
     d.act_lo = a.lo;
     d.act_hi = a.hi;
+    if (a.split) {
+      const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
+      if (sp.split_tiles > 0 && a.ws && a.counters && sp.ws_floats <= a.ws_cap &&
+          sp.counters <= a.cnt_cap) {
+        d.split_tiles = sp.split_tiles;
+        d.nkb = sp.nkb;
+        d.ws = a.ws;
+        d.counters = a.counters;
+      }
+    }
     rtenhip_status st = launch_gemm_dma(d, cfg, c->stream);
     if (st) return st;
   }
@@ -205,6 +229,8 @@ rtenhip_status output_size_and_padding(int64_t in_h, int64_t in_w, int64_t k_h, 
   out_hw[1] = (pw - dil_x * (k_w - 1) - 1) / stride_w + 1;
   return RTENHIP_OK;
 }
+
+static bool g_split_enabled = true;
 
 rtenhip_status plan_conv(const rtenhip_tensor* x, const rtenhip_tensor* w, int pad_mode,
                                 const int64_t* pads, const int64_t* strides,
@@ -374,6 +400,17 @@ rtenhip_status conv_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* 
     a.y = y->data;
     a.y_img = p.O * P;
     a.cfg = cfg;
+    if (g_split_enabled) {
+      const DmaSplit sp = dma_split_plan((int)opg, (int)(p.N * P), (int)K, cfg);
+      if (sp.split_tiles > 0) {
+        a.ws = c->scratch_floats((size_t)sp.ws_floats, 3);
+        a.counters = c->split_counters((size_t)sp.counters);
+        if (!a.ws || !a.counters) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+        a.split = true;
+        a.ws_cap = sp.ws_floats;
+        a.cnt_cap = sp.counters;
+      }
+    }
     return conv_dma(c, a);
   }
 
@@ -570,6 +607,7 @@ const char* rtenhip_build_info(void) { return "rten-hip gfx950 (CDNA4) f32 MFMA 
 // Tuning / test knob: route convs through the LDS-DMA GEMM (default) or the
 // register-staged general kernel.  Both produce bit-identical results.
 void rtenhip_debug_set_dma(rtenhip_ctx* ctx, int enabled) { C_(ctx)->use_dma = enabled != 0; }
+void rtenhip_debug_set_split(int enabled) { rtenhip::g_split_enabled = enabled != 0; }
 void rtenhip_debug_trust_weight_cache(rtenhip_ctx* ctx, int enabled) {
   C_(ctx)->trust_weight_cache = enabled != 0;
 }

@@ -37,6 +37,11 @@ struct Ctx {
   // 1 softmax / padded inputs, 2 packed weights, 3 spare).  Synchronizes the
   // stream when it has to grow, so callers must not be capturing.
   float* scratch_floats(size_t n, size_t slot);
+  // Grow-only zeroed int buffer for DMA split arrival counters (the kernel
+  // leaves them zero).  Synchronizes when it grows, like scratch_floats.
+  int* split_counters(size_t n);
+  int* counters = nullptr;
+  size_t counters_cap = 0;
   // Device table of VirtualIm2Col row offsets for one conv geometry.
   const int2* ktab(int C, int H, int W, int kh, int kw, int dh, int dw);
   // Device table of per-k input offsets c*H*W + ky*dh*W + kx*dw (DMA GEMM).
@@ -56,6 +61,13 @@ struct ConvDmaArgs {
   float* y;
   int64_t y_img, y_row, y_off;  // output addressing (padded outputs allowed)
   int cfg;                      // DMA kernel configuration, -1 = default
+  // KC split of the remainder tiles (dma_split_plan): enabled when split is
+  // set and the caller's workspace / zeroed counters are large enough.
+  bool split;
+  float* ws;
+  int64_t ws_cap;
+  int* counters;
+  int64_t cnt_cap;
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
 bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, int64_t groups,

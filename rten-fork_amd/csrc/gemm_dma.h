@@ -45,10 +45,24 @@ struct DmaDesc {
   float alpha, beta;
   int act;
   float act_lo, act_hi;
+  // KC split of the last split_tiles tiles (0 = none): nkb K blocks each,
+  // chains in ws (split_tiles * nkb * BM*BN floats), arrival counters
+  // (split_tiles ints, zero between launches; the kernel re-zeroes them).
+  int split_tiles, nkb;
+  float* ws;
+  int* counters;
+  int n_full;               // set by launch_gemm_dma
   int vec4;                 // outputs/residual row-contiguous with P % 4 == 0, unpadded:
                             // 16-byte epilogue accesses (no cin)
   int dbg;                  // tuning experiments only: 1 = no K-loop DMA, 2 = no MFMA
 };
+
+// KC split plan for one configuration (split_tiles == 0: not worth it).
+struct DmaSplit {
+  int split_tiles, nkb;
+  int64_t ws_floats, counters;
+};
+DmaSplit dma_split_plan(int M, int N, int K, int cfg);
 
 // Kernel configurations (all bit-identical; see gemm_dma.hip).
 int dma_num_cfgs();

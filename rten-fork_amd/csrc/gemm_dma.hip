@@ -65,16 +65,33 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   const int wm = (wave / WAVES_N) * WM;
   const int wn = (wave % WAVES_N) * WN;
 
-  // XCD-aware bijective remap (see gemm_mfma.hip).
-  const int nwg = tiles_m * tiles_n;
+  // Blocks [0, n_full) each own a whole tile (XCD-aware bijective remap, see
+  // gemm_mfma.hip).  With a KC split (d.split_tiles > 0) the remaining tiles
+  // -- the ones that would leave CUs idle in a last partial round -- are cut
+  // at the reference's KC = 256 boundaries: block n_full + t*nkb + kb computes
+  // only K block kb of split tile t and the last of the nkb blocks to finish
+  // folds them in order (see below).
   const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int n_full = d.n_full;
+  int wg, kb_split = -1, split_idx = -1;
+  if (bid < n_full) {
+    const int nwg = n_full;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  } else {
+    const int u = bid - n_full;
+    split_idx = u / d.nkb;
+    kb_split = u - split_idx * d.nkb;
+    wg = n_full + split_idx;
+  }
   const int tmi = wg % tiles_m;
   const int tm = tmi * BM;
   const int tn = (wg / tiles_m) * BN;
   const int M = d.M, N = d.N, K = d.K;
   const int tiles_k = (K + BK - 1) / BK;
+  constexpr int TPB = DKC / BK;  // K tiles per KC block
+  const int kt_lo = kb_split >= 0 ? kb_split * TPB : 0;
+  const int kt_hi = kb_split >= 0 ? min(tiles_k, kt_lo + TPB) : tiles_k;
 
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, 0x7fffffff, 0x00020000);
@@ -219,11 +236,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   auto body = [&](auto set_tag, int kt) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
     mfma_steps(set_tag, I0{}, IMid{});
-    if (kt + 1 < tiles_k) {
+    if (kt + 1 < kt_hi) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_dma(min(STAGES - 2, tiles_k - kt - 2));
+      wait_dma(min(STAGES - 2, kt_hi - kt - 2));
       __builtin_amdgcn_s_barrier();
-      if (kt + STAGES < tiles_k && !(d.dbg & 1)) issue(stage, kt + STAGES);
+      if (kt + STAGES < kt_hi && !(d.dbg & 1)) issue(stage, kt + STAGES);
       stage = stage + 1 == STAGES ? 0 : stage + 1;
       read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
     }
@@ -237,20 +254,145 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
   };
 
-  // Prologue: fill every stage, wait for tile 0, read it.
+  // Vectorised epilogue geometry (see the epilogue) and, for small wave
+  // tiles, the residual prefetched now so its latency hides under the K loop
+  // (it does not depend on the GEMM).
+  constexpr bool VEC_FITS = NW * 1024 <= STAGES * STAGE;
+  constexpr bool RES_PRE = VEC_FITS && MI * NI == 1 && BK == 16;
+  const int rr = lane >> 3;        // row within an 8-row group
+  const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
+  float4 rpre[RES_PRE ? MI : 1][RES_PRE ? NI : 1][4];
+  if constexpr (RES_PRE) {
+    if (d.vec4 && d.residual) {
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++) {
+          const int n = tn + wn + ni * 32 + c4;
+          const bool ncol_ok = n <= N - 1;
+          const int nn = ncol_ok ? n : 0;
+          const int img = nn / d.P;
+          const int64_t rbase = (int64_t)img * d.res_img + (nn - img * d.P);
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int m = tm + wm + mi * 32 + i * 8 + rr;
+            rpre[mi][ni][i] = (ncol_ok && m < M)
+                                  ? *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+    }
+  }
+
+  // Prologue: fill every stage, wait for the first tile, read it.
 #pragma unroll
   for (int s = 0; s < STAGES; s++)
-    if (s < tiles_k) issue(s, s);
-  wait_dma(min(STAGES, tiles_k) - 1);
+    if (kt_lo + s < kt_hi) issue(s, kt_lo + s);
+  wait_dma(min(STAGES, kt_hi - kt_lo) - 1);
   __builtin_amdgcn_s_barrier();
   read_tile(I0{}, 0);
 
   f32x16 sum[MULTI_KB ? MI : 1][MULTI_KB ? NI : 1];
   if constexpr (!MULTI_KB) {
     run(0, tiles_k);
+  } else if (kb_split >= 0) {
+    // One KC block of a split tile: its chain goes to the workspace; the
+    // last of the tile's nkb blocks to arrive folds all chains in K order
+    // exactly as the whole-tile path does, then runs the epilogue.
+    run(kt_lo, kt_hi);
+    // Hand-off without L2 write-back fences (MI355X guide, Guideline 16 /
+    // "Valid forms" row 1): chains are stored write-through (sc1, as 8-byte
+    // agent-scope atomic stores), every storing wave drains (vmcnt(0)) before
+    // the workgroup barrier, one lane adds to the tile's counter (agent scope)
+    // and the workgroup whose add returns nkb-1 reads the chains with sc1
+    // loads only.
+    constexpr int CH = MI * NI * 16 * NT;  // floats per chain (whole block)
+    // 8-byte granules, stored and loaded as agent-scope relaxed atomics
+    // (global_store/load_dwordx2 sc1).  Layout per chain: [(mi*NI+ni)*8 + jp][tid].
+    // (__float_as_uint, not __builtin_bit_cast: clang 22 folds a bit_cast of
+    // an ext_vector element to element 0.)
+    unsigned long long* wsq =
+        reinterpret_cast<unsigned long long*>(d.ws + (int64_t)split_idx * d.nkb * CH);
+    auto qidx = [&](int kb, int mi, int ni, int jp) {
+      return ((int64_t)kb * (CH / 2)) + (((mi * NI + ni) * 8 + jp) * NT + tid);
+    };
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++)
+#pragma unroll
+        for (int jp = 0; jp < 8; jp++) {
+          const unsigned long long q =
+              (unsigned long long)__float_as_uint(acc[mi][ni][2 * jp]) |
+              ((unsigned long long)__float_as_uint(acc[mi][ni][2 * jp + 1]) << 32);
+          __hip_atomic_store(wsq + qidx(kb_split, mi, ni, jp), q, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+    __shared__ int last_arrival;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(d.counters + split_idx, 1, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      last_arrival = prev == d.nkb - 1;
+    }
+    __syncthreads();
+    if (!last_arrival) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
+    auto ldq = [&](int kb, int mi, int ni, int jp) {
+      return __hip_atomic_load(wsq + qidx(kb, mi, ni, jp), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto lo = [](unsigned long long q) { return __uint_as_float((unsigned)(q & 0xffffffffu)); };
+    auto hi = [](unsigned long long q) { return __uint_as_float((unsigned)(q >> 32)); };
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++) {
+        f32x16 c;
+#pragma unroll
+        for (int jp = 0; jp < 8; jp++) {
+          const unsigned long long q = ldq(0, mi, ni, jp);
+          c[2 * jp] = lo(q);
+          c[2 * jp + 1] = hi(q);
+        }
+        first_block(sum[mi][ni], c, mi, ni);
+      }
+    // Remaining chains in K order; loads of a group of blocks are issued
+    // together so the fold is not latency-bound.
+    constexpr int G = MI * NI == 1 ? 2 : 1;
+    for (int kb0 = 1; kb0 < d.nkb; kb0 += G) {
+      f32x16 cg[G][MI][NI];
+#pragma unroll
+      for (int gi = 0; gi < G; gi++) {
+        if (kb0 + gi >= d.nkb) break;
+#pragma unroll
+        for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+          for (int ni = 0; ni < NI; ni++)
+#pragma unroll
+            for (int jp = 0; jp < 8; jp++) {
+              const unsigned long long q = ldq(kb0 + gi, mi, ni, jp);
+              cg[gi][mi][ni][2 * jp] = lo(q);
+              cg[gi][mi][ni][2 * jp + 1] = hi(q);
+            }
+      }
+#pragma unroll
+      for (int gi = 0; gi < G; gi++) {
+        if (kb0 + gi >= d.nkb) break;
+#pragma unroll
+        for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+          for (int ni = 0; ni < NI; ni++)
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+              sum[mi][ni][j] = __fmaf_rn(cg[gi][mi][ni][j], d.alpha, sum[mi][ni][j]);
+      }
+    }
+    if (tid == 0)
+      __hip_atomic_store(d.counters + split_idx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
     // K > DKC: block 0 is peeled so the bias/beta fold sits outside the loop.
-    constexpr int TPB = DKC / BK;
     static_assert(TPB % 2 == 0, "register-set parity across K blocks");
     run(0, TPB);
 #pragma unroll
@@ -282,7 +424,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
     return x;
   };
-  constexpr bool VEC_FITS = NW * 1024 <= STAGES * STAGE;
   if (VEC_FITS && d.vec4) {
     // Row-contiguous outputs (P % 4 == 0, unpadded): each 32x32 accumulator
     // block is transposed through this wave's LDS slot so every lane stores
@@ -290,8 +431,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     // instead of 16 dword accesses.  Same per-element arithmetic as below.
     __syncthreads();  // every wave is done reading the K stages
     float* slot = lds + wave * 1024;
-    const int rr = lane >> 3;        // row within an 8-row group
-    const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
 #pragma unroll
     for (int mi = 0; mi < MI; mi++)
 #pragma unroll
@@ -319,7 +458,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
           const bool ok = ncol_ok && m < M;
           float4 x = *(const float4*)(slot + row * 32 + c4);
           if (d.residual && ok) {
-            const float4 r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
+            float4 r;
+            if constexpr (RES_PRE)
+              r = rpre[mi][ni][i];
+            else
+              r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
             x.x = __fadd_rn(x.x, r.x);
             x.y = __fadd_rn(x.y, r.y);
             x.z = __fadd_rn(x.z, r.z);
@@ -371,7 +514,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
 template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES>
 static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
-  dim3 grid(tiles_m * tiles_n), block(NT);
+  dim3 grid(d.n_full + d.split_tiles * d.nkb), block(NT);
   if (d.K > DKC)
     hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true>), grid,
                        block, 0, s, d, tiles_m, tiles_n);
@@ -394,12 +537,12 @@ static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   X(5, 64, 64, 64, 16, 1, 1, 2, 3)      \
   X(6, 512, 256, 128, 16, 4, 2, 2, 3)   \
   X(7, 256, 64, 64, 16, 2, 2, 4, 3)     \
-  X(8, 128, 64, 64, 16, 2, 1, 3, 3)     \
-  X(9, 256, 128, 64, 16, 4, 1, 3, 3)    \
-  X(10, 256, 64, 128, 16, 2, 2, 3, 3)   \
+  X(8, 128, 64, 64, 16, 2, 1, 2, 3)     \
+  X(9, 256, 128, 64, 16, 4, 1, 2, 3)    \
+  X(10, 256, 64, 128, 16, 2, 2, 2, 3)   \
   X(11, 512, 128, 128, 16, 4, 2, 2, 4)  \
   X(12, 256, 128, 128, 16, 2, 2, 2, 4)  \
-  X(13, 256, 64, 64, 32, 2, 2, 4, 2)    \
+  X(13, 256, 64, 64, 32, 2, 2, 3, 2)    \
   X(14, 256, 64, 64, 16, 2, 2, 4, 4)    \
   X(15, 512, 128, 64, 16, 4, 2, 4, 3)   \
   X(16, 512, 64, 128, 16, 2, 4, 4, 3)   \
@@ -439,6 +582,24 @@ int dma_default_cfg(int M, int N, int K) {
   return 7;
 }
 
+DmaSplit dma_split_plan(int M, int N, int K, int cfg) {
+  DmaSplit sp{0, 0, 0, 0};
+  const DmaCfgInfo& c = kDmaCfgs[cfg];
+  const int tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+  const int nkb = (K + DKC - 1) / DKC;
+  if (nkb < 2) return sp;
+  // Whole tiles fill complete rounds of one tile per CU; the remainder would
+  // run as a partial round, so it is split into KC blocks.
+  constexpr int CUS = 256;
+  const int rem = tiles % CUS;
+  if (rem == 0) return sp;
+  sp.split_tiles = rem;
+  sp.nkb = nkb;
+  sp.ws_floats = (int64_t)rem * nkb * c.bm * c.bn;
+  sp.counters = rem;
+  return sp;
+}
+
 rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty DMA GEMM");
   if (cfg < 0 || cfg >= kNumDmaCfgs) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
@@ -446,6 +607,16 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
     return fail(RTENHIP_INVALID_VALUE, "A packed for another tile shape");
   DmaDesc dd = d;
   dd.dbg = g_dma_dbg;
+  const DmaCfgInfo& ci = kDmaCfgs[cfg];
+  const int tiles = ((d.M + ci.bm - 1) / ci.bm) * ((d.N + ci.bn - 1) / ci.bn);
+  if (d.split_tiles > 0) {
+    if (d.K <= DKC || !d.ws || !d.counters || d.split_tiles > tiles ||
+        d.nkb != (d.K + DKC - 1) / DKC)
+      return fail(RTENHIP_INVALID_VALUE, "bad DMA split");
+    dd.n_full = tiles - d.split_tiles;
+  } else {
+    dd.n_full = tiles;
+  }
   switch (cfg) {
 #define RTENHIP_DMA_CASE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) \
   case id:                                                    \

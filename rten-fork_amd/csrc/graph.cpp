@@ -71,8 +71,11 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 }
 
 Plan::~Plan() {
-  for (auto& kv : convs)
+  for (auto& kv : convs) {
     if (kv.second.packed) (void)hipFree(kv.second.packed);
+    if (kv.second.ws) (void)hipFree(kv.second.ws);
+    if (kv.second.counters) (void)hipFree(kv.second.counters);
+  }
   for (auto& kv : padded)
     if (kv.second.base) (void)hipFree(kv.second.base);
   for (auto& kv : side_events) {
@@ -767,9 +770,40 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     a.y_img = g.O * P;
   }
   const float* w = ptr_of(p, n.inputs[1]);
+  const int64_t opg = g.O / g.groups, K = (g.C / g.groups) * g.kh * g.kw;
+  // KC-split buffers for (cfg, split), plan-owned (no ctx scratch, so side-
+  // stream convs never share them).
+  auto set_split = [&](ConvExec& e, int cfg, bool split) -> rtenhip_status {
+    e.split = false;
+    if (!split) return RTENHIP_OK;
+    const DmaSplit sp = dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg);
+    if (sp.split_tiles == 0) return RTENHIP_OK;
+    if (sp.ws_floats > e.ws_floats) {
+      if (e.ws) RTENHIP_HIP_CHECK(hipFree(e.ws));
+      e.ws = nullptr;
+      RTENHIP_HIP_CHECK(hipMalloc(&e.ws, (size_t)sp.ws_floats * 4));
+      e.ws_floats = sp.ws_floats;
+    }
+    if (sp.counters > e.n_counters) {
+      if (e.counters) RTENHIP_HIP_CHECK(hipFree(e.counters));
+      e.counters = nullptr;
+      RTENHIP_HIP_CHECK(hipMalloc(&e.counters, (size_t)sp.counters * 4));
+      RTENHIP_HIP_CHECK(hipMemset(e.counters, 0, (size_t)sp.counters * 4));
+      e.n_counters = sp.counters;
+    }
+    e.split = true;
+    return RTENHIP_OK;
+  };
+  auto bind = [&](const ConvExec& e) {
+    a.split = e.split;
+    a.ws = e.ws;
+    a.ws_cap = e.ws_floats;
+    a.counters = e.counters;
+    a.cnt_cap = e.n_counters;
+  };
   if (ce.cfg < 0) {
-    const int64_t opg = g.O / g.groups, K = (g.C / g.groups) * g.kh * g.kw;
     int chosen = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
+    bool chosen_split = false;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
     if (autotune && cs == hipStreamCaptureStatusNone) {
@@ -779,6 +813,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
       float best_ms = 1e30f;
       std::vector<float*> bufs;
+      ConvExec trial;  // split buffers reused across candidates
       for (int cfg : kCandidates) {
         if (cfg >= dma_num_cfgs()) continue;
         float* pk = nullptr;
@@ -786,34 +821,47 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         bufs.push_back(pk);
         rtenhip_status st = pack_conv_weights(ctx, w, g, cfg, pk);
         if (st) return st;
-        a.packed_w = pk;
-        a.cfg = cfg;
-        st = conv_dma(ctx, a);  // warm-up
-        if (st) return st;
-        RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
-        for (int r = 0; r < 2 && !st; r++) st = conv_dma(ctx, a);
-        if (st) return st;
-        RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
-        RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
-        float ms = 0;
-        RTENHIP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
-        if (ms < best_ms) {
-          best_ms = ms;
-          chosen = cfg;
+        for (int split = 0; split < 2; split++) {
+          if (split && dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg).split_tiles == 0)
+            continue;
+          st = set_split(trial, cfg, split != 0);
+          if (st) return st;
+          bind(trial);
+          a.packed_w = pk;
+          a.cfg = cfg;
+          st = conv_dma(ctx, a);  // warm-up
+          if (st) return st;
+          RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
+          for (int r = 0; r < 2 && !st; r++) st = conv_dma(ctx, a);
+          if (st) return st;
+          RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
+          RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
+          float ms = 0;
+          RTENHIP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+          if (ms < best_ms) {
+            best_ms = ms;
+            chosen = cfg;
+            chosen_split = split != 0;
+          }
         }
       }
       (void)hipEventDestroy(e0);
       (void)hipEventDestroy(e1);
       RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
       for (float* b : bufs) (void)hipFree(b);
+      if (trial.ws) (void)hipFree(trial.ws);
+      if (trial.counters) (void)hipFree(trial.counters);
     }
     RTENHIP_HIP_CHECK(hipMalloc(&ce.packed, (size_t)packed_conv_weight_floats(g, chosen) * 4));
     rtenhip_status st = pack_conv_weights(ctx, w, g, chosen, ce.packed);
+    if (st) return st;
+    st = set_split(ce, chosen, chosen_split);
     if (st) return st;
     ce.cfg = chosen;
   }
   a.packed_w = ce.packed;
   a.cfg = ce.cfg;
+  bind(ce);
   return conv_dma(ctx, a);
 }
 

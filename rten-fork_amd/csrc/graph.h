@@ -76,6 +76,10 @@ struct ConvExec {
   ConvPlan g;
   int cfg = -1;             // kernel configuration (chosen on the first run)
   float* packed = nullptr;  // weights packed for cfg, owned by the plan
+  bool split = false;       // KC split of the remainder tiles (dma_split_plan)
+  float* ws = nullptr;      // its workspace and arrival counters, plan-owned
+  int* counters = nullptr;
+  int64_t ws_floats = 0, n_counters = 0;
 };
 
 // A value stored with a zero border so the DMA convs reading it need no

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--cfgs", default="g0,d0,d1,d2,d3,d6",
                     help="g<n>: register-staged kernel config n; d<n>: LDS-DMA kernel config n")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--split", type=int, default=1, help="KC split of remainder tiles (standalone conv path)")
     ap.add_argument("--dmamode", type=int, default=0,
                     help="timing experiment: 1 = no K-loop DMA, 2 = no MFMA (wrong results)")
     ap.add_argument("--model", default="resnet50")
@@ -39,6 +40,8 @@ def main():
     lib.rtenhip_debug_trust_weight_cache(ctx, 1)
     lib.rtenhip_debug_set_dma_mode.argtypes = [ctypes.c_int]
     lib.rtenhip_debug_set_dma_mode(args.dmamode)
+    lib.rtenhip_debug_set_split.argtypes = [ctypes.c_int]
+    lib.rtenhip_debug_set_split(args.split)
     spec = getattr(models, args.model)()
     consts = {n.name: n.data for n in spec.nodes if n.kind == "const"}
     # distinct conv shapes with their input spatial size
