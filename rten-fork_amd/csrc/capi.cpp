@@ -135,6 +135,8 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     d.xstride = a.sw;
     d.OW = (int)a.ow;
     d.P = (int)P;
+    d.fdOW = make_fastdiv((uint32_t)a.ow);
+    d.fdP = make_fastdiv((uint32_t)P);
     d.ktab4 = tab;
     d.out_img = a.y_img;
     d.out_c = P;  // channel stride of an unpadded output plane
@@ -161,6 +163,15 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     d.act = a.act;
     d.act_lo = a.lo;
     d.act_hi = a.hi;
+    // 16-byte B copies: pointwise stride-1 convs (B[k][n] = x[img][k][p],
+    // linear in k) whose 4-pixel groups stay inside one image.
+    const bool pointwise = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 &&
+                           a.Hp == a.oh && a.Wp == a.ow;
+    if (pointwise && dma_cfg_bvec(cfg) && P % 4 == 0 && K % tile.bk == 0 &&
+        (a.C * a.Hp * a.Wp) % 4 == 0 && ((uintptr_t)d.x % 16) == 0) {
+      d.bvec = 1;
+      d.kstride = (int)(a.Hp * a.Wp);
+    }
     if (a.split) {
       const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
       if (sp.split_tiles > 0 && a.ws && a.counters && sp.ws_floats <= a.ws_cap &&

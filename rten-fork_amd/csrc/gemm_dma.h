@@ -26,6 +26,18 @@ struct DmaTile {
 //     padded to a multiple of DMA_KTAB_PAD entries),
 //   out index  = img*out_img + m*out_c + oy*out_row + ox + out_off,
 //   residual   = img*res_img + m*res_c + (oy*OW + ox).
+// Division by an invariant divisor for 0 <= n < 2^31 (see fdiv in gemm_dma.hip).
+struct FastDiv {
+  uint64_t mul;
+  uint32_t shift;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((uint64_t(1) << l) < d) l++;
+  const uint32_t shift = 31 + l;
+  return FastDiv{((uint64_t(1) << shift) + d - 1) / d, shift};
+}
+
 struct DmaDesc {
   int M, N, K;
   DmaTile tile;             // tile shape A was packed for
@@ -35,6 +47,7 @@ struct DmaDesc {
   int64_t x_img;
   int64_t ystride, xstride;
   int OW, P;
+  FastDiv fdOW, fdP;        // divisors OW and P
   const int* ktab4;
   float* out;
   int64_t out_img, out_c, out_row, out_off;
@@ -52,6 +65,9 @@ struct DmaDesc {
   float* ws;
   int* counters;
   int n_full;               // set by launch_gemm_dma
+  int bvec;                 // B copied 16 bytes per lane (dma_cfg_bvec(cfg) and pointwise:
+                            // koff(k) = k * kstride, P % 4 == 0, K % BK == 0)
+  int kstride;              // elements between consecutive k rows of B (bvec)
   int vec4;                 // outputs/residual row-contiguous with P % 4 == 0, unpadded:
                             // 16-byte epilogue accesses (no cin)
   int dbg;                  // tuning experiments only: 1 = no K-loop DMA, 2 = no MFMA
@@ -66,6 +82,7 @@ DmaSplit dma_split_plan(int M, int N, int K, int cfg);
 
 // Kernel configurations (all bit-identical; see gemm_dma.hip).
 int dma_num_cfgs();
+bool dma_cfg_bvec(int cfg);
 int dma_default_cfg(int M, int N, int K);
 DmaTile dma_cfg_tile(int cfg);
 int64_t packed_a_floats(int M, int K, const DmaTile& t);

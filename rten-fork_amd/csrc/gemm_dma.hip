@@ -33,10 +33,29 @@ typedef __attribute__((address_space(4))) const int const_int_t;
 
 constexpr int DKC = 256;
 
+// n / d for 0 <= n < 2^31 by a host-precomputed multiplier (FastDiv):
+// q = (n * mul) >> shift with mul = ceil(2^shift / d), shift = 31 + ceil(log2 d)
+// (exact in that range).
+__device__ __forceinline__ int fdiv(int n, FastDiv f) {
+  return (int)(((uint64_t)(uint32_t)n * f.mul) >> f.shift);
+}
+
+// LDS-DMA helpers (buffer_load_dword{,x4} ... lds).  Kept out of the kernel
+// template: clang's host pass rejects the 16-byte form inside some template
+// instantiations (substitution failure, silently dropping the kernel stub).
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff,
+                                          uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+}
+__device__ __forceinline__ void lds_dma4(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff,
+                                         uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 4, voff, soff, 0, 0);
+}
+
 // One block computes a BM x BN tile with WAVES_M x WAVES_N waves, each owning
 // a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA accumulators.
 template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES,
-          bool MULTI_KB>
+          bool MULTI_KB, bool BVEC>
 __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles_m, int tiles_n) {
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int NW = NT / 64;
@@ -47,7 +66,10 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   constexpr int A_LB = BM * BK * 4 >= NT * 16 ? 16 : 4;  // bytes per lane
   constexpr int A_CHUNK = 64 * A_LB;                     // bytes per wave-instruction
   constexpr int A_INSTR = BM * BK * 4 / A_CHUNK;
-  constexpr int B_INSTR = BK * (BN / 64);    // dword wave-instructions per B tile
+  // B tile copy: dword per lane (one k row of 64 columns per instruction), or
+  // with BVEC dwordx4 (4 k rows x 64 columns per instruction; pointwise convs
+  // whose 4-pixel groups are contiguous and whose k stride is linear).
+  constexpr int B_INSTR = BVEC ? BK * BN / 256 : BK * (BN / 64);
   constexpr int A_PER_W = A_INSTR / NW;
   constexpr int B_PER_W = B_INSTR / NW;
   constexpr int STAGE = (BM + BN) * BK;      // floats per stage
@@ -56,6 +78,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "even DMA split");
   static_assert(BN % 64 == 0 && DKC % BK == 0 && BK <= DMA_KTAB_PAD, "tile shape");
   static_assert(MI >= 1 && NI >= 1, "wave tile");
+  static_assert(!BVEC || (NI == 1 && BN == 64 && BK % 4 == 0),
+                "BVEC needs the identity B column layout and 64-column rows");
 
   __shared__ float lds[STAGES * STAGE];
 
@@ -110,13 +134,31 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     const int n = tn + (pos - q) + (q % NI) * 32 + q / NI;
     uint32_t off = DMA_OOB;
     if (n < N) {
-      const int img = n / d.P;
+      const int img = fdiv(n, d.fdP);
       const int p = n - img * d.P;
-      const int oy = p / d.OW;
+      const int oy = fdiv(p, d.fdOW);
       const int ox = p - oy * d.OW;
       off = (uint32_t)(((int64_t)img * d.x_img + (int64_t)oy * d.ystride + (int64_t)ox * d.xstride) * 4);
     }
     vb[g] = off;
+  }
+  // BVEC: instruction i of this wave covers k rows 4*(wave*B_PER_W+i) .. +3 of
+  // the tile; lane -> row (lane >> 4), columns 4*(lane & 15) .. +3.
+  uint32_t vb4[BVEC ? B_PER_W : 1];
+  if constexpr (BVEC) {
+#pragma unroll
+    for (int i = 0; i < B_PER_W; i++) {
+      const int gi = wave * B_PER_W + i;
+      const int kk = gi * 4 + (lane >> 4);
+      const int n = tn + (lane & 15) * 4;
+      uint32_t off = DMA_OOB;
+      if (n < N) {
+        const int img = fdiv(n, d.fdP);
+        const int p = n - img * d.P;
+        off = (uint32_t)(((int64_t)img * d.x_img + p) * 4 + (int64_t)kk * d.kstride * 4);
+      }
+      vb4[i] = off;
+    }
   }
   const uint32_t va = (uint32_t)(wave * A_PER_W * A_CHUNK + lane * A_LB);
   const uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
@@ -130,17 +172,25 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     for (int i = 0; i < A_PER_W; i++) {
       lds_void_t* dst = (lds_void_t*)(As + (wave * A_PER_W + i) * (A_CHUNK / 4));
       if constexpr (A_LB == 16)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 16, va + i * A_CHUNK, a_soff, 0, 0);
+        lds_dma16(ra, dst, va + i * A_CHUNK, a_soff);
       else
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, dst, 4, va + i * A_CHUNK, a_soff, 0, 0);
+        lds_dma4(ra, dst, va + i * A_CHUNK, a_soff);
     }
-    const_int_t* kt4 = ktab4 + kt * BK;
+    if constexpr (BVEC) {
+      const uint32_t b_soff = (uint32_t)kt * (uint32_t)(BK * d.kstride * 4);
 #pragma unroll
-    for (int i = 0; i < B_PER_W; i++) {
-      const int gi = wave * B_PER_W + i;  // wave-uniform
-      const int kl = gi / NG, g = gi % NG;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void_t*)(Bs + kl * BN + g * 64), 4, vb[g],
-                                               (uint32_t)kt4[kl], 0, 0);
+      for (int i = 0; i < B_PER_W; i++) {
+        const int gi = wave * B_PER_W + i;  // rows 4*gi .. 4*gi+3: 1 KB of LDS
+        lds_dma16(rb, (lds_void_t*)(Bs + gi * 256), vb4[i], b_soff);
+      }
+    } else {
+      const_int_t* kt4 = ktab4 + kt * BK;
+#pragma unroll
+      for (int i = 0; i < B_PER_W; i++) {
+        const int gi = wave * B_PER_W + i;  // wave-uniform
+        const int kl = gi / NG, g = gi % NG;
+        lds_dma4(rb, (lds_void_t*)(Bs + kl * BN + g * 64), vb[g], (uint32_t)kt4[kl]);
+      }
     }
   };
 
@@ -156,6 +206,35 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   const int n_lim = N - 1 - tn;
   auto lrow = [&](int mi, int j) __attribute__((always_inline)) { return wm + mi * 32 + (j & 3) + 8 * (j >> 2) + 4 * half; };
 
+  // Bias of accumulator row j: when the wave's 32-row group is inside M and
+  // 16-byte aligned, the 16 rows a lane needs (4 runs of 4) come from 4
+  // float4 loads instead of 16 scalar ones.
+  constexpr bool BIAS_VEC = MI == 1;  // keeps the 16 extra registers off 64-row waves
+  float4 bias4[MI][4];
+  bool bias_vec[MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; mi++) {
+    const int r0 = tm + wm + mi * 32;
+    bias_vec[mi] = BIAS_VEC && d.bias && r0 + 31 < M && ((uintptr_t)(d.bias + r0) % 16) == 0;
+  }
+  auto load_bias = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+      if (bias_vec[mi]) {
+#pragma unroll
+        for (int q4 = 0; q4 < 4; q4++)
+          bias4[mi][q4] = *(const float4*)(d.bias + tm + wm + mi * 32 + 8 * q4 + 4 * half);
+      }
+  };
+  auto bias_row = [&](int mi, int j, int ml) __attribute__((always_inline)) {
+    if (bias_vec[mi]) {
+      const float4 b = bias4[mi][j >> 2];
+      const int e = j & 3;
+      return e == 0 ? b.x : e == 1 ? b.y : e == 2 ? b.z : b.w;
+    }
+    return d.bias[tm + ml];
+  };
+
   // End of K block 0: v = alpha*acc (+ beta*C) + bias (gemm.rs:1004-1050).
   auto first_block = [&](f32x16& v, const f32x16& a, int mi, int ni) __attribute__((always_inline)) {
 #pragma unroll
@@ -167,9 +246,9 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         const float c = d.cin[(int64_t)(tm + ml) * d.out_c + tn + nl];
         x = __fmaf_rn(a[j], d.alpha, __fmul_rn(c, d.beta));
       } else {
-        x = __fmul_rn(a[j], d.alpha);
+        x = d.alpha == 1.f ? a[j] : __fmul_rn(a[j], d.alpha);  // x * 1 == x exactly
       }
-      if (d.bias) x = __fadd_rn(x, d.bias[tm + ml]);
+      if (d.bias) x = __fadd_rn(x, bias_row(mi, j, ml));
       v[j] = x;
     }
   };
@@ -216,7 +295,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   };
   auto mfma_steps = [&](auto set_tag, auto s0_tag, auto s1_tag) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
-    if (d.dbg & 2) return;
 #pragma unroll
     for (int s = decltype(s0_tag)::value; s < decltype(s1_tag)::value; s++)
 #pragma unroll
@@ -240,15 +318,45 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       wait_dma(min(STAGES - 2, kt_hi - kt - 2));
       __builtin_amdgcn_s_barrier();
-      if (kt + STAGES < kt_hi && !(d.dbg & 1)) issue(stage, kt + STAGES);
+      if (kt + STAGES < kt_hi) issue(stage, kt + STAGES);
       stage = stage + 1 == STAGES ? 0 : stage + 1;
       read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
     }
     mfma_steps(set_tag, IMid{}, IEnd{});
   };
-  // Tiles [kt0, kt1) with kt0 even (register set = tile parity).
+  // Steady state (STAGES = 2 or 4, whose ring period divides both the
+  // register-set period 2 and the KC block): a group of STAGES tiles with
+  // compile-time stage and register-set indices, fixed DMA wait counts and
+  // no bounds tests -- LDS addresses become immediates and the per-tile
+  // scalar/vector bookkeeping disappears.  Valid while every tile of the
+  // group still has a refill to issue (kt + STAGES - 1 + STAGES < kt_hi).
+  constexpr bool FAST = STAGES == 2 || STAGES == 4;
+  auto body_fast = [&](auto set_tag, auto stg_tag, int kt) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_tag)::value;
+    constexpr int STG = decltype(stg_tag)::value;
+    mfma_steps(set_tag, I0{}, IMid{});
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(STG, kt + STAGES);
+    read_tile(std::integral_constant<int, SET ^ 1>{}, (STG + 1) % STAGES);
+    mfma_steps(set_tag, IMid{}, IEnd{});
+  };
+  // Tiles [kt0, kt1) with kt0 even (register set = tile parity) and
+  // (kt0 - kt_lo) % STAGES == 0 (stage of tile kt0 is 0).
   auto run = [&](int kt0, int kt1) __attribute__((always_inline)) {
-    for (int kt = kt0; kt < kt1; kt += 2) {
+    int kt = kt0;
+    if constexpr (FAST) {
+      for (; kt + STAGES <= kt1 && kt + 2 * STAGES - 1 < kt_hi; kt += STAGES) {
+        body_fast(I0{}, std::integral_constant<int, 0>{}, kt);
+        body_fast(I1{}, std::integral_constant<int, 1>{}, kt + 1);
+        if constexpr (STAGES == 4) {
+          body_fast(I0{}, std::integral_constant<int, 2>{}, kt + 2);
+          body_fast(I1{}, std::integral_constant<int, 3>{}, kt + 3);
+        }
+      }
+    }
+    for (; kt < kt1; kt += 2) {
       body(I0{}, kt);
       if (kt + 1 < kt1) body(I1{}, kt + 1);
     }
@@ -271,7 +379,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
           const int n = tn + wn + ni * 32 + c4;
           const bool ncol_ok = n <= N - 1;
           const int nn = ncol_ok ? n : 0;
-          const int img = nn / d.P;
+          const int img = fdiv(nn, d.fdP);
           const int64_t rbase = (int64_t)img * d.res_img + (nn - img * d.P);
 #pragma unroll
           for (int i = 0; i < 4; i++) {
@@ -283,6 +391,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         }
     }
   }
+
+  load_bias();
 
   // Prologue: fill every stage, wait for the first tile, read it.
 #pragma unroll
@@ -447,7 +557,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         const int n = tn + wn + ni * 32 + c4;
         const bool ncol_ok = n <= N - 1;  // N % 4 == 0: the whole segment is in range
         const int nn = ncol_ok ? n : 0;
-        const int img = nn / d.P;
+        const int img = fdiv(nn, d.fdP);
         const int p = nn - img * d.P;
         const int64_t obase = (int64_t)img * d.out_img + p;
         const int64_t rbase = (int64_t)img * d.res_img + p;
@@ -484,9 +594,9 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     const int nl = wn + ni * 32 + l32;
     const bool ncol_ok = nl <= n_lim;
     const int n = tn + min(nl, n_lim);
-    const int img = n / d.P;
+    const int img = fdiv(n, d.fdP);
     const int p = n - img * d.P;
-    const int oy = p / d.OW;
+    const int oy = fdiv(p, d.fdOW);
     const int ox = p - oy * d.OW;
     const int64_t obase = (int64_t)img * d.out_img + (int64_t)oy * d.out_row + ox + d.out_off;
     const int64_t rbase = (int64_t)img * d.res_img + p;
@@ -511,16 +621,33 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   }
 }
 
+// Whether a configuration has a BVEC (16-byte B copy) variant.
+template <int NT, int BM, int BN, int BK, int WM_, int WN_>
+constexpr bool dma_bvec_ok() {
+  return BN == 64 && BN / WN_ == 32 && (BK * BN / 256) % (NT / 64) == 0 && BK % 4 == 0;
+}
+
 template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES>
 static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
   dim3 grid(d.n_full + d.split_tiles * d.nkb), block(NT);
+  if constexpr (dma_bvec_ok<NT, BM, BN, BK, WM_, WN_>()) {
+    if (d.bvec) {
+      if (d.K > DKC)
+        hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true, true>),
+                           grid, block, 0, s, d, tiles_m, tiles_n);
+      else
+        hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false, true>),
+                           grid, block, 0, s, d, tiles_m, tiles_n);
+      return;
+    }
+  }
   if (d.K > DKC)
-    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true>), grid,
-                       block, 0, s, d, tiles_m, tiles_n);
+    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true, false>),
+                       grid, block, 0, s, d, tiles_m, tiles_n);
   else
-    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false>), grid,
-                       block, 0, s, d, tiles_m, tiles_n);
+    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false, false>),
+                       grid, block, 0, s, d, tiles_m, tiles_n);
 }
 
 // DMA tile configurations:
@@ -562,6 +689,18 @@ static int g_dma_cfg = -1;
 static int g_dma_dbg = 0;
 
 int dma_num_cfgs() { return kNumDmaCfgs; }
+
+bool dma_cfg_bvec(int cfg) {
+  switch (cfg) {
+#define RTENHIP_DMA_BV(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) \
+  case id:                                                  \
+    return dma_bvec_ok<NT, BM, BN, BK, WMW, WNW>();
+    RTENHIP_DMA_CONFIGS(RTENHIP_DMA_BV)
+#undef RTENHIP_DMA_BV
+    default:
+      return false;
+  }
+}
 
 DmaTile dma_cfg_tile(int cfg) {
   const DmaCfgInfo& c = kDmaCfgs[cfg];

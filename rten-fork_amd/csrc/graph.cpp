@@ -961,14 +961,17 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   rtenhip_status st = RTENHIP_OK;
   // Launch one op on its stream: side ops fork from the main stream and
   // record completion; a join op first waits for the side ops it reads.
-  auto stream_of = [&](int op) { return plan->side.count(op) ? side_stream : exec_stream; };
+  // Timing runs keep every op on the main stream so per-op times do not
+  // include concurrent work.
+  auto on_side = [&](int op) { return !timing && plan->side.count(op) > 0; };
+  auto stream_of = [&](int op) { return on_side(op) ? side_stream : exec_stream; };
   auto before_op = [&](int op) -> rtenhip_status {
-    if (plan->side.count(op)) {
+    if (on_side(op)) {
       auto& ev = plan->side_events[op];
       RTENHIP_HIP_CHECK(hipEventRecord(ev.first, exec_stream));
       RTENHIP_HIP_CHECK(hipStreamWaitEvent(side_stream, ev.first, 0));
       ctx->stream = side_stream;
-    } else {
+    } else if (!timing) {
       auto j = plan->joins.find(op);
       if (j != plan->joins.end())
         for (int d : j->second)
@@ -977,13 +980,14 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     return RTENHIP_OK;
   };
   auto after_op = [&](int op) -> rtenhip_status {
-    if (plan->side.count(op)) {
+    if (on_side(op)) {
       RTENHIP_HIP_CHECK(hipEventRecord(plan->side_events[op].second, side_stream));
       ctx->stream = exec_stream;
     }
     return RTENHIP_OK;
   };
   auto join_all = [&]() -> rtenhip_status {
+    if (timing) return RTENHIP_OK;
     auto j = plan->joins.find(-1);
     if (j != plan->joins.end())
       for (int d : j->second)
