@@ -38,7 +38,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=64, help="images per GPU")
-    p.add_argument("--model", default="resnet50", choices=["resnet50", "mobilenet_v2"])
+    p.add_argument("--model", default="resnet50", choices=["resnet50", "mobilenet_v2", "bert"])
+    p.add_argument("--seq", type=int, default=128, help="BERT sequence length")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--timing-report", action="store_true")
@@ -119,18 +120,27 @@ def main():
     from rten_hip import models
 
     ctx = rten_hip.Context(torch.cuda.current_device())
-    spec = models.resnet50() if args.model == "resnet50" else models.mobilenet_v2()
-    g = spec.to_graph(ctx)
     B = args.batch
-    flops_per_img = models.conv_flops(spec, 1)
     rng = np.random.default_rng(1234 + rank)
-    x = torch.from_numpy(rng.random((B, 3, 224, 224), dtype=np.float32)).cuda()
-    (out,) = g.run({g.input_ids[0]: x}, g.output_ids)  # plans + tunes conv kernels
+    extra = {}
+    if args.model == "bert":
+        spec = models.bert_encoder(seq=args.seq)
+        flops_per_img = models.bert_flops(seq=args.seq)
+        x = torch.from_numpy(rng.random((B, args.seq, 768), dtype=np.float32) - 0.5).cuda()
+        mask = torch.zeros((B, 1, 1, args.seq), dtype=torch.float32).cuda()
+    else:
+        spec = models.resnet50() if args.model == "resnet50" else models.mobilenet_v2()
+        flops_per_img = models.conv_flops(spec, 1)
+        x = torch.from_numpy(rng.random((B, 3, 224, 224), dtype=np.float32)).cuda()
+    g = spec.to_graph(ctx)
+    if args.model == "bert":
+        extra = {g.input_ids[1]: mask}
+    (out,) = g.run({g.input_ids[0]: x, **extra}, g.output_ids)  # plans + tunes conv kernels
 
     from rten_hip.parallel import BatchShardRunner
 
     def forward(xb):
-        g.run({g.input_ids[0]: xb}, g.output_ids, out=[out])
+        g.run({g.input_ids[0]: xb, **extra}, g.output_ids, out=[out])
         return out
 
     # Rank r holds images [r*B, (r+1)*B) of the world*B job; the only
@@ -168,12 +178,12 @@ def main():
     conv_ms = 0.0
     report = ""
     for _ in range(max(1, min(args.steps, 10))):
-        g.run({g.input_ids[0]: x}, g.output_ids, out=[out])
+        g.run({g.input_ids[0]: x, **extra}, g.output_ids, out=[out])
         torch.cuda.synchronize()
         report = g.timing_report()
         for line in report.splitlines()[1:]:
             name = line.split()[0]
-            if name.startswith("Conv") or name == "Gemm":
+            if name.startswith("Conv") or name in ("Gemm", "MatMul"):
                 conv_ms += float(line.split()[1])
     n_prof = max(1, min(args.steps, 10))
     g.set_timing(False)
@@ -181,12 +191,25 @@ def main():
     gemm_flops = flops_per_img * B
     achieved = gemm_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
 
+    if args.model == "bert":
+        workload = (f"{spec.name} encoder f32 batch={B} per GPU, seq {args.seq}, hidden 768, "
+                    f"12 heads, FFN 3072 (BASELINE.json configs[3])")
+        kernel_desc = "MatMul GEMM launches (gemm_mfma_kernel / gemm_dma_kernel)"
+        data = "synthetic (U[-0.5,0.5) hidden states resident in HBM; seeded U(+-0.05) weights)"
+    else:
+        cfg_idx = {"resnet50": 1 if B == 64 and world == 1 else 4, "mobilenet_v2": 2}[args.model]
+        workload = (f"{spec.name} f32 batch={B} per GPU, 224x224 NCHW, BN folded "
+                    f"(BASELINE.json configs[{cfg_idx}])")
+        kernel_desc = ("gemm_dma_kernel (all 53 Conv launches) + FC Gemm" if args.model == "resnet50"
+                       else "Conv (DMA GEMM + depthwise) + FC Gemm")
+        data = "synthetic (U[0,1) images resident in HBM; seeded He-uniform weights)"
     if rank == 0:
         line = {
-            "metric": "images/sec ResNet-50 f32 batch=64 per GPU" if args.model == "resnet50"
-                      else "images/sec MobileNetV2 f32",
+            "metric": {"resnet50": "images/sec ResNet-50 f32 batch=64 per GPU",
+                       "mobilenet_v2": "images/sec MobileNetV2 f32",
+                       "bert": "sequences/sec BERT-base encoder f32"}[args.model],
             "value": round(value, 2),
-            "unit": "images/s",
+            "unit": "sequences/s" if args.model == "bert" else "images/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -195,16 +218,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (U[0,1) images resident in HBM; seeded He-uniform weights)",
-            "config": {"workload": f"{spec.name} f32 batch={B} per GPU, 224x224 NCHW, BN folded "
-                                   f"(BASELINE.json configs[{1 if B == 64 and world == 1 else 4}])",
-                       "model": spec.name, "global_batch": world * B, "seq_len": None,
+            "data": data,
+            "config": {"workload": workload,
+                       "model": spec.name, "global_batch": world * B,
+                       "seq_len": args.seq if args.model == "bert" else None,
                        "parallelism": f"batch-shard x{world} (replicated weights, RCCL all-gather of logits)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
                          "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
                          "traffic": traffic_bytes(args.model, B),
-                         "kernel": "gemm_dma_kernel (all 53 Conv launches) + FC Gemm",
+                         "kernel": kernel_desc,
                          "flops_per_step": gemm_flops,
                          "kernel_ms_per_step": round(conv_ms, 4),
                          "model_frac": round(value / world * flops_per_img / 1e12 /

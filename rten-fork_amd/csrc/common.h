@@ -10,6 +10,19 @@
 
 namespace rtenhip {
 
+// Division by an invariant divisor for 0 <= n < 2^31: q = (n * mul) >> shift
+// with shift = 31 + ceil(log2 d), mul = ceil(2^shift / d) (exact in that range).
+struct FastDiv {
+  uint64_t mul;
+  uint32_t shift;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((uint64_t(1) << l) < d) l++;
+  const uint32_t shift = 31 + l;
+  return FastDiv{((uint64_t(1) << shift) + d - 1) / d, shift};
+}
+
 // Thread-local last error (rtenhip_last_error_message).
 void set_error(int code, const std::string& msg);
 rtenhip_status fail(rtenhip_status code, const char* msg);

@@ -26,18 +26,6 @@ struct DmaTile {
 //     padded to a multiple of DMA_KTAB_PAD entries),
 //   out index  = img*out_img + m*out_c + oy*out_row + ox + out_off,
 //   residual   = img*res_img + m*res_c + (oy*OW + ox).
-// Division by an invariant divisor for 0 <= n < 2^31 (see fdiv in gemm_dma.hip).
-struct FastDiv {
-  uint64_t mul;
-  uint32_t shift;
-};
-inline FastDiv make_fastdiv(uint32_t d) {
-  uint32_t l = 0;
-  while ((uint64_t(1) << l) < d) l++;
-  const uint32_t shift = 31 + l;
-  return FastDiv{((uint64_t(1) << shift) + d - 1) / d, shift};
-}
-
 struct DmaDesc {
   int M, N, K;
   DmaTile tile;             // tile shape A was packed for

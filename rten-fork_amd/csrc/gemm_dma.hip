@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "gemm_dma.h"
+#include "fastdiv_dev.h"
 
 namespace rtenhip {
 
@@ -32,13 +33,6 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(4))) const int const_int_t;
 
 constexpr int DKC = 256;
-
-// n / d for 0 <= n < 2^31 by a host-precomputed multiplier (FastDiv):
-// q = (n * mul) >> shift with mul = ceil(2^shift / d), shift = 31 + ceil(log2 d)
-// (exact in that range).
-__device__ __forceinline__ int fdiv(int n, FastDiv f) {
-  return (int)(((uint64_t)(uint32_t)n * f.mul) >> f.shift);
-}
 
 // LDS-DMA helpers (buffer_load_dword{,x4} ... lds).  Kept out of the kernel
 // template: clang's host pass rejects the 16-byte form inside some template

@@ -359,7 +359,7 @@ __global__ void gemm_k0_kernel(float* out, int64_t out_m, int M, int N, float be
   }
 }
 
-// Small-M dense GEMM (the FC layer: M = batch <= 64, N = 1000, K = 2048).
+// Small-M dense GEMM (the FC layer: M = batch <= 256, N = 1000, K = 2048).
 // MFMA tiles would leave most CUs idle at this size, so the K blocks are
 // split across workgroups instead -- exactly at the reference's KC = 256
 // boundaries, which keeps the arithmetic identical: kernel 1 computes each
@@ -376,7 +376,8 @@ __global__ __launch_bounds__(256) void gemm_kblock_kernel(GemmDesc d, float* __r
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kb = blockIdx.y;
   const int n0 = blockIdx.x * (4 * COLS) + w * COLS;
-  const int m = min(lane, d.M - 1);
+  const int mrow = blockIdx.z * 64 + lane;  // 64 rows per z slice
+  const int m = min(mrow, d.M - 1);
   const int k0 = kb * 256, k1 = min(d.K, k0 + 256);
   const float* ap = d.a + (int64_t)m * d.a_m;
   const_float_t* bp = (const_float_t*)d.b;
@@ -408,10 +409,10 @@ __global__ __launch_bounds__(256) void gemm_kblock_kernel(GemmDesc d, float* __r
     for (int j = 0; j < COLS; j++)
       c[j] = __fmaf_rn(av, bp[(int64_t)k * d.b_k + (int64_t)nn[j] * d.b_n], c[j]);
   }
-  if (lane >= d.M) return;
+  if (mrow >= d.M) return;
 #pragma unroll
   for (int j = 0; j < COLS; j++)
-    if (n0 + j < d.N) ws[((int64_t)kb * d.M + lane) * d.N + n0 + j] = c[j];
+    if (n0 + j < d.N) ws[((int64_t)kb * d.M + mrow) * d.N + n0 + j] = c[j];
 }
 
 __global__ __launch_bounds__(256) void gemm_kfold_kernel(GemmDesc d, const float* __restrict__ ws,
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(256) void gemm_kfold_kernel(GemmDesc d, const float
 }
 
 bool gemm_smallm_eligible(const GemmDesc& d) {
-  return d.K > 0 && d.bmode == 0 && d.nbatch <= 1 && !d.residual && d.M <= 64 && d.N >= 64 &&
+  return d.K > 0 && d.bmode == 0 && d.nbatch <= 1 && !d.residual && d.M <= 256 && d.N >= 64 &&
          (int64_t)d.M * d.N <= (int64_t(1) << 20) && g_forced_cfg < 0;
 }
 
@@ -448,7 +449,7 @@ int64_t gemm_smallm_ws_floats(const GemmDesc& d) {
 
 rtenhip_status launch_gemm_smallm(const GemmDesc& d, float* ws, hipStream_t s) {
   const int nkb = (d.K + 255) / 256;
-  dim3 grid((d.N + 15) / 16, nkb);
+  dim3 grid((d.N + 15) / 16, nkb, (d.M + 63) / 64);
   if (d.a_k == 1 && d.b_k == 1)
     hipLaunchKernelGGL(gemm_kblock_kernel<true>, grid, dim3(256), 0, s, d, ws);
   else

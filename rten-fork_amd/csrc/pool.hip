@@ -11,6 +11,7 @@
 //    exactly.  The Clip/Relu/Add that follow in MobileNetV2 can be fused.
 #include "common.h"
 #include "vecmath.h"
+#include "fastdiv_dev.h"
 
 namespace rtenhip {
 
@@ -132,6 +133,114 @@ __global__ void depthwise_kernel(const float* __restrict__ x, const float* __res
   }
 }
 
+// Same arithmetic as depthwise_kernel (per output: bias, then + v*w in ky, kx
+// order, separately rounded mul and add as conv_2d_depthwise_block does), for
+// outputs that fit 32-bit indexing and kernels at most 8 wide: index math by
+// invariant-divisor multiplies and the per-kx valid output-x range
+// (min_max_out_x_coords, depthwise.rs:24-38, incl. its undivided lower
+// bound) precomputed on the host.
+struct DwBounds {
+  int omin[8], omax[8];
+};
+
+__global__ __launch_bounds__(256) void depthwise32_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ y, int total, int C, int H, int W, int OH, int OW, int kh, int kw, int sh,
+    int sw, int dh, int dw, int pt, int pl, FastDiv fOW, FastDiv fOH, FastDiv fC, DwBounds b,
+    const float* __restrict__ residual, int act, float lo, float hi) {
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int t = fdiv(i, fOW);
+    const int ox = i - t * OW;
+    const int plane = fdiv(t, fOH);
+    const int oy = t - plane * OH;
+    const int c = plane - fdiv(plane, fC) * C;
+    const float* xp = x + (int64_t)plane * H * W;
+    const float* kp = w + c * kh * kw;
+    float acc = bias ? bias[c] : 0.f;
+    for (int ky = 0; ky < kh; ky++) {
+      const int iy = oy * sh + ky * dh;
+      if (iy < pt || iy >= H + pt) continue;
+      const float* row = xp + (iy - pt) * W + ox * sw - pl;
+#pragma unroll 8
+      for (int kx = 0; kx < kw; kx++) {
+        if (ox < b.omin[kx] || ox >= b.omax[kx]) continue;
+        acc = __fadd_rn(acc, __fmul_rn(row[kx * dw], kp[ky * kw + kx]));
+      }
+    }
+    if (residual) acc = __fadd_rn(acc, residual[i]);
+    if (act == RTENHIP_ACT_RELU) acc = rust_max(acc, 0.f);
+    else if (act == RTENHIP_ACT_CLIP) acc = rust_clamp(acc, lo, hi);
+    y[i] = acc;
+  }
+}
+
+// LDS-tiled depthwise conv.  A block owns PB consecutive planes (n*C + c) and
+// TH output rows of each; thread t is column ox = t % OW of plane t / OW and
+// walks the TH rows, so index math happens once per thread.  The input rows
+// those outputs need are staged in LDS first (each plane's rows are one
+// contiguous span: coalesced, no per-element division); weights and bias live
+// in registers.  Tap order, skipping rules and rounding are those of
+// depthwise32_kernel (conv_2d_depthwise_block, depthwise.rs).
+template <int KH, int KW>  // 0 = runtime kernel size (weights read from memory)
+__global__ __launch_bounds__(256) void depthwise_lds_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ y, int planes, int C, int H, int W, int OH, int OW, int kh_, int kw_,
+    int sh, int sw, int dh, int dw, int pt, int pl, int TH, int PB, int rows_in, DwBounds b,
+    const float* __restrict__ residual, int act, float lo, float hi) {
+  extern __shared__ float tile[];
+  const int plane0 = blockIdx.y * PB;
+  const int oy0 = blockIdx.x * TH;
+  const int iy_lo = oy0 * sh - pt;  // input row held in tile row 0
+  const int np = min(PB, planes - plane0);
+  const int r0 = max(iy_lo, 0), r1 = min(iy_lo + rows_in, H);
+  if (r1 > r0) {
+    const int span = (r1 - r0) * W;
+    for (int pp = 0; pp < np; pp++) {
+      const float* src = x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W;
+      float* dst = tile + (pp * rows_in + (r0 - iy_lo)) * W;
+      for (int q = threadIdx.x; q < span; q += blockDim.x) dst[q] = src[q];
+    }
+  }
+  __syncthreads();
+  const int pp = threadIdx.x / OW;
+  const int ox = threadIdx.x - pp * OW;
+  if (pp >= np) return;
+  const int plane = plane0 + pp;
+  const int c = plane % C;
+  const int kh = KH ? KH : kh_, kw = KW ? KW : kw_;
+  constexpr int NT = KH * KW > 0 ? KH * KW : 1;
+  float wr[NT];  // compile-time kernel: weights in registers
+  if constexpr (KH * KW > 0) {
+#pragma unroll
+    for (int t = 0; t < NT; t++) wr[t] = w[c * NT + t];
+  }
+  const float* kp = w + c * kh * kw;
+  const float b0 = bias ? bias[c] : 0.f;
+  const int oh_blk = min(TH, OH - oy0);
+  for (int oyl = 0; oyl < oh_blk; oyl++) {
+    const int oy = oy0 + oyl;
+    float acc = b0;
+#pragma unroll
+    for (int ky = 0; ky < (KH ? KH : kh); ky++) {
+      const int iy = oy * sh + ky * dh;
+      if (iy < pt || iy >= H + pt) continue;
+      const float* row = tile + (pp * rows_in + (iy - pt - iy_lo)) * W + ox * sw - pl;
+#pragma unroll
+      for (int kx = 0; kx < (KW ? KW : kw); kx++) {
+        if (ox < b.omin[kx] || ox >= b.omax[kx]) continue;
+        const float wv = KH * KW > 0 ? wr[(ky * kw + kx) % NT] : kp[ky * kw + kx];
+        acc = __fadd_rn(acc, __fmul_rn(row[kx * dw], wv));
+      }
+    }
+    const int64_t oi = (int64_t)plane * OH * OW + oy * OW + ox;
+    if (residual) acc = __fadd_rn(acc, residual[oi]);
+    if (act == RTENHIP_ACT_RELU) acc = rust_max(acc, 0.f);
+    else if (act == RTENHIP_ACT_CLIP) acc = rust_clamp(acc, lo, hi);
+    y[oi] = acc;
+  }
+}
+
 rtenhip_status launch_depthwise(const float* x, const float* w, const float* bias, float* y,
                                 int N, int C, int H, int W, int OH, int OW, int kh, int kw,
                                 int sh, int sw, int dh, int dw, int pt, int pl,
@@ -141,6 +250,48 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
   if (total == 0) return RTENHIP_OK;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
+  if (kw <= 8 && total + blocks * 256 < (int64_t(1) << 31) &&
+      (int64_t)N * C * H * W < (int64_t(1) << 31)) {
+    DwBounds b{};
+    for (int kx = 0; kx < kw; kx++) {
+      const int kxd = kx * dw;
+      b.omin[kx] = pl - kxd > 0 ? pl - kxd : 0;
+      const int t = W + pl - kxd > 0 ? W + pl - kxd : 0;
+      int omax = (t + sw - 1) / sw;
+      b.omax[kx] = omax > OW ? OW : omax;
+    }
+    // LDS tiling (depthwise_lds_kernel): PB planes x OW columns of threads,
+    // TH output rows each, at most 16 KB of staged input per block.
+    const int planes = N * C;
+    if (OW <= 256 && kh * kw <= 64) {
+      const int PB = 256 / OW;
+      auto rows_for = [&](int th) { return (th - 1) * sh + (kh - 1) * dh + 1; };
+      int TH = OH;
+      while (TH > 1 && PB * rows_for(TH) * W > 4096) TH = (TH + 1) / 2;
+      const int rows_in = rows_for(TH);
+      const size_t lds = (size_t)PB * rows_in * W * sizeof(float);
+      dim3 grid((unsigned)((OH + TH - 1) / TH), (unsigned)((planes + PB - 1) / PB));
+      if (lds <= 64 * 1024 && grid.y <= 65535) {
+        const int threads = (PB * OW + 63) / 64 * 64;
+        if (kh == 3 && kw == 3)
+          hipLaunchKernelGGL((depthwise_lds_kernel<3, 3>), grid, dim3(threads), lds, s, x, w, bias,
+                             y, planes, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, TH, PB,
+                             rows_in, b, residual, act, lo, hi);
+        else
+          hipLaunchKernelGGL((depthwise_lds_kernel<0, 0>), grid, dim3(threads), lds, s, x, w, bias,
+                             y, planes, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, TH, PB,
+                             rows_in, b, residual, act, lo, hi);
+        RTENHIP_LAUNCH_CHECK();
+        return RTENHIP_OK;
+      }
+    }
+    hipLaunchKernelGGL(depthwise32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, w, bias, y,
+                       (int)total, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl,
+                       make_fastdiv((uint32_t)OW), make_fastdiv((uint32_t)OH),
+                       make_fastdiv((uint32_t)C), b, residual, act, lo, hi);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   hipLaunchKernelGGL(depthwise_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, w, bias, y,
                      total, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, residual, act, lo,
                      hi);

@@ -165,3 +165,79 @@ def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
         else:
             shapes[n.outputs[0]] = xs
     return total
+
+
+BERT_BASE_GFLOP_PER_SEQ128 = 22.347  # SURVEY.md App. A.3 (encoder, seq 128)
+
+
+def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int = 3072,
+                 seq: int = 128, eps: float = 1e-12, seed: int = 4321) -> ModelSpec:
+    """BERT-base encoder stack in the operator mix of an ONNX export as RTen
+    runs it after its own fusions (GELU and LayerNormalization fused,
+    src/optimize.rs): per layer Q/K/V MatMul+Add, Reshape/Transpose to heads,
+    QK^T MatMul, Div by sqrt(d_head), Add of the additive attention mask,
+    Softmax, AV MatMul, Transpose/Reshape back, output MatMul+Add, residual
+    Add + LayerNormalization, FFN MatMul+Add -> Gelu -> MatMul+Add, residual
+    Add + LayerNormalization.
+
+    Inputs: ``hidden_states`` [B, S, hidden] (the embedding output: the token
+    Gather is outside the f32 hot path) and ``attention_mask`` [B, 1, 1, S]
+    (additive; zeros for the all-ones mask rten-cli uses, rten-cli main.rs).
+    Weights U(+-0.05) (BERT's N(0, 0.02) init has the same scale), biases
+    U(+-0.01), LayerNorm gamma ~1, beta ~0."""
+    m = ModelSpec("bert_base" if layers == 12 else f"bert_l{layers}")
+    rng = np.random.default_rng(seed)
+    x = m.value("hidden_states")
+    mask = m.value("attention_mask")
+    m.inputs = ["hidden_states", "attention_mask"]
+    dh = hidden // heads
+
+    def lin(name, h, cin, cout):
+        w = m.const(f"{name}.weight", rng.uniform(-0.05, 0.05, (cin, cout)).astype(np.float32))
+        b = m.const(f"{name}.bias", rng.uniform(-0.01, 0.01, (cout,)).astype(np.float32))
+        y = m.op("MatMul", [h, w], name=f"{name}.matmul")
+        return m.op("Add", [y, b], name=f"{name}.add")
+
+    def ln(name, h):
+        g = m.const(f"{name}.gamma", (1.0 + rng.uniform(-0.1, 0.1, (hidden,))).astype(np.float32))
+        b = m.const(f"{name}.beta", rng.uniform(-0.1, 0.1, (hidden,)).astype(np.float32))
+        return m.op("LayerNormalization", [h, g, b], {"axis": -1, "epsilon": eps}, name=name)
+
+    shape_heads = m.const("shape.heads", np.array([0, 0, heads, dh], np.float32))
+    shape_merge = m.const("shape.merge", np.array([0, 0, hidden], np.float32))
+    scale = m.const("attn.scale", np.array([np.sqrt(dh)], np.float32))
+    h = x
+    for i in range(layers):
+        p = f"layer{i}"
+        q = lin(f"{p}.q", h, hidden, hidden)
+        k = lin(f"{p}.k", h, hidden, hidden)
+        v = lin(f"{p}.v", h, hidden, hidden)
+        q = m.op("Reshape", [q, shape_heads], name=f"{p}.q.reshape")
+        q = m.op("Transpose", [q], {"perm": [0, 2, 1, 3]}, name=f"{p}.q.transpose")
+        k = m.op("Reshape", [k, shape_heads], name=f"{p}.k.reshape")
+        k = m.op("Transpose", [k], {"perm": [0, 2, 3, 1]}, name=f"{p}.k.transpose")
+        v = m.op("Reshape", [v, shape_heads], name=f"{p}.v.reshape")
+        v = m.op("Transpose", [v], {"perm": [0, 2, 1, 3]}, name=f"{p}.v.transpose")
+        s = m.op("MatMul", [q, k], name=f"{p}.qk")
+        s = m.op("Div", [s, scale], name=f"{p}.scale")
+        s = m.op("Add", [s, mask], name=f"{p}.mask")
+        s = m.op("Softmax", [s], {"axis": -1}, name=f"{p}.softmax")
+        c = m.op("MatMul", [s, v], name=f"{p}.av")
+        c = m.op("Transpose", [c], {"perm": [0, 2, 1, 3]}, name=f"{p}.ctx.transpose")
+        c = m.op("Reshape", [c, shape_merge], name=f"{p}.ctx.reshape")
+        a = lin(f"{p}.attn_out", c, hidden, hidden)
+        h1 = ln(f"{p}.ln1", m.op("Add", [a, h], name=f"{p}.res1"))
+        f = lin(f"{p}.ffn1", h1, hidden, ffn)
+        f = m.op("Gelu", [f], name=f"{p}.gelu")
+        f = lin(f"{p}.ffn2", f, ffn, hidden)
+        h = ln(f"{p}.ln2", m.op("Add", [f, h1], name=f"{p}.res2"))
+    m.outputs = [h]
+    return m
+
+
+def bert_flops(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int = 3072,
+               seq: int = 128) -> float:
+    """2*MACs per sequence of the encoder's MatMuls."""
+    proj = 4 * seq * hidden * hidden + 2 * seq * hidden * ffn
+    attn = 2 * seq * seq * hidden
+    return 2.0 * layers * (proj + attn)

@@ -89,3 +89,46 @@ def test_graph_errors(rh):
     with pytest.raises(rh.OpError) as e:
         g.run({}, [y])
     assert e.value.kind == "MissingInputs"
+
+
+def _run_bert(rh, spec, batch, seq, hidden=768, runs=2, seed=99):
+    import torch
+    import graph_runner
+
+    rng = np.random.default_rng(seed)
+    x = (rng.random((batch, seq, hidden), dtype=np.float32) - np.float32(0.5))
+    mask = np.zeros((batch, 1, 1, seq), np.float32)
+    # a padded tail on the last sequence: additive mask -10000 (rten-cli style)
+    mask[-1, :, :, seq - seq // 4:] = -10000.0
+    exp = graph_runner.run(spec, {"hidden_states": x, "attention_mask": mask})[spec.outputs[0]]
+    g = spec.to_graph()
+    xd, md = torch.from_numpy(x).cuda(), torch.from_numpy(mask).cuda()
+    outs, out = [], None
+    for _ in range(runs):
+        out = g.run({g.input_ids[0]: xd, g.input_ids[1]: md}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        outs.append(out[0].cpu().numpy())
+    return exp, outs
+
+
+def test_bert_two_layers_bitexact(rh):
+    """BERT encoder (MatMul / Softmax / LayerNormalization / Gelu / Transpose)
+    at a small size: batch 2, seq 32, 2 layers."""
+    from rten_hip import models
+
+    exp, outs = _run_bert(rh, models.bert_encoder(layers=2, seq=32), batch=2, seq=32)
+    for o in outs:
+        if not _bits_equal(o, exp):
+            d = np.abs(o.astype(np.float64) - exp)
+            pytest.fail(f"BERT output differs: max abs {d.max():.3g}, {(d > 0).sum()} elems")
+
+
+def test_bert_base_seq128_bitexact(rh):
+    """BASELINE config 4's model (BERT-base encoder, 12 layers, seq 128) at
+    batch 2, bit-exact vs the oracle."""
+    from rten_hip import models
+
+    exp, outs = _run_bert(rh, models.bert_encoder(), batch=2, seq=128)
+    assert np.isfinite(exp).all()
+    for o in outs:
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
