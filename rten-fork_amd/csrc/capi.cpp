@@ -77,7 +77,9 @@ int* Ctx::split_counters(size_t n) {
     counters = nullptr;
     size_t cap = n + 64;
     if (hipMalloc(&counters, cap * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(counters, 0, cap * sizeof(int)) != hipSuccess) return nullptr;
+    // Ordered on the stream the split kernels run on: a plain hipMemset is not
+    // ordered with a non-blocking stream.
+    if (hipMemsetAsync(counters, 0, cap * sizeof(int), stream) != hipSuccess) return nullptr;
     counters_cap = cap;
   }
   return counters;

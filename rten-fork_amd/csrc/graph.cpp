@@ -383,6 +383,10 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       RTENHIP_HIP_CHECK(hipMemset(pv.base, 0, bytes));
       p.padded[v] = pv;
     }
+    // hipMemset is not ordered with the executor's non-blocking streams: the
+    // zero border must be in place before the first producer writes the
+    // interior, or the memset can land on top of it (first run only).
+    if (!p.padded.empty()) RTENHIP_HIP_CHECK(hipDeviceSynchronize());
   }
 
   // Independent branches: a DMA conv whose inputs were ready two or more ops
@@ -788,7 +792,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       if (e.counters) RTENHIP_HIP_CHECK(hipFree(e.counters));
       e.counters = nullptr;
       RTENHIP_HIP_CHECK(hipMalloc(&e.counters, (size_t)sp.counters * 4));
-      RTENHIP_HIP_CHECK(hipMemset(e.counters, 0, (size_t)sp.counters * 4));
+      RTENHIP_HIP_CHECK(hipMemsetAsync(e.counters, 0, (size_t)sp.counters * 4, s));
       e.n_counters = sp.counters;
     }
     e.split = true;
