@@ -58,6 +58,7 @@ typedef enum {
   RTENHIP_ACT_NONE = 0,
   RTENHIP_ACT_RELU = 1, /* Relu: f32::max(x, 0) (unary_elementwise.rs:571) */
   RTENHIP_ACT_CLIP = 2, /* Clip: f32::clamp(x, lo, hi) (unary_elementwise.rs:314-323) */
+  RTENHIP_ACT_GELU = 3, /* Gelu: simd_gelu (rten-vecmath/src/erf.rs:85-91) */
 } rtenhip_act;
 
 typedef struct rtenhip_ctx rtenhip_ctx;

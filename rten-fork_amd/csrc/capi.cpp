@@ -524,6 +524,90 @@ rtenhip_status conv_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* 
   return RTENHIP_OK;
 }
 
+bool dense_dma_eligible(int64_t M, int64_t N, int64_t K, int64_t a_cs, int64_t b_rs, int64_t b_cs) {
+  // Large enough for MFMA tiles to pay for the per-call A pack; N % 4 == 0 for
+  // 16-byte B copies and epilogue stores; B addressed with 32-bit offsets.
+  return M >= 128 && N >= 128 && K >= 16 && N % 4 == 0 && a_cs == 1 && b_cs == 1 &&
+         b_rs % 4 == 0 && b_rs >= N && M * N * K >= (int64_t(1) << 24) &&
+         K * b_rs < (int64_t(1) << 29) && M < (int64_t(1) << 30);
+}
+
+rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
+  hipStream_t s = c->stream;
+  const int cfg = a.cfg >= 0 ? a.cfg : dma_default_cfg((int)a.M, (int)a.N, (int)a.K);
+  const DmaTile tile = dma_cfg_tile(cfg);
+  float* pk = a.pk;
+  if (!pk) {
+    pk = c->scratch_floats((size_t)packed_a_floats((int)a.M, (int)a.K, tile), 2);
+    if (!pk) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+  }
+  if (a.pack || !a.pk) {
+    rtenhip_status st = launch_pack_a(a.a, a.a_rs, (int)a.M, (int)a.K, tile, pk, s);
+    if (st) return st;
+  }
+  // B as a one-image pointwise conv input [1, C = K, H = 1, W = b_rs].
+  const int* tab = c->dtab((int)a.K, 1, (int)a.b_rs, 1, 1, 1, 1);
+  if (!tab) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
+  DmaDesc d{};
+  d.M = (int)a.M;
+  d.N = (int)a.N;
+  d.K = (int)a.K;
+  d.tile = tile;
+  d.apk = pk;
+  d.x = a.b;
+  d.x_bytes = (uint32_t)(a.K * a.b_rs * 4);
+  d.x_img = a.K * a.b_rs;
+  d.ystride = 0;
+  d.xstride = 1;
+  d.OW = (int)a.N;
+  d.P = (int)a.N;
+  d.fdOW = make_fastdiv((uint32_t)a.N);
+  d.fdP = make_fastdiv((uint32_t)a.N);
+  d.ktab4 = tab;
+  d.out = a.out;
+  d.out_img = a.M * a.out_rs;
+  d.out_c = a.out_rs;
+  d.out_row = a.N;
+  d.out_off = 0;
+  d.residual = a.residual;
+  d.res_img = a.M * a.res_rs;
+  d.res_c = a.res_rs;
+  d.bias = a.bias;
+  d.colbias = a.colbias;
+  d.alpha = 1.f;
+  d.beta = 0.f;
+  d.act = a.act;
+  d.act_lo = a.lo;
+  d.act_hi = a.hi;
+  // 16-byte epilogue: rows contiguous in memory segments of 4.
+  d.vec4 = (a.out_rs % 4 == 0 && (uintptr_t)a.out % 16 == 0 &&
+            (!a.residual || (a.res_rs % 4 == 0 && (uintptr_t)a.residual % 16 == 0)) &&
+            (!a.colbias || (uintptr_t)a.colbias % 16 == 0))
+               ? 1
+               : 0;
+  if (dma_cfg_bvec(cfg) && a.K % tile.bk == 0 && ((uintptr_t)a.b % 16) == 0) {
+    d.bvec = 1;
+    d.kstride = (int)a.b_rs;
+  }
+  if (a.split) {
+    const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
+    if (sp.split_tiles > 0) {
+      float* ws = a.ws;
+      int* cnt = a.counters;
+      if (!ws || sp.ws_floats > a.ws_cap || !cnt || sp.counters > a.cnt_cap) {
+        ws = c->scratch_floats((size_t)sp.ws_floats, 3);
+        cnt = c->split_counters((size_t)sp.counters);
+        if (!ws || !cnt) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+      }
+      d.split_tiles = sp.split_tiles;
+      d.nkb = sp.nkb;
+      d.ws = ws;
+      d.counters = cnt;
+    }
+  }
+  return launch_gemm_dma(d, cfg, s);
+}
+
 // GemmExecutor::gemm_bias on strided device matrices (gemm.rs:733-930).
 rtenhip_status gemm_impl(Ctx* c, int64_t m, int64_t n, int64_t k, const float* a, int64_t a_rs,
                          int64_t a_cs, const float* b, int64_t b_rs, int64_t b_cs, float* out,
@@ -561,6 +645,24 @@ rtenhip_status gemm_impl(Ctx* c, int64_t m, int64_t n, int64_t k, const float* a
     float* ws = c->scratch_floats((size_t)gemm_smallm_ws_floats(d), 3);
     if (!ws) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
     return launch_gemm_smallm(d, ws, s);
+  }
+  if (c->use_dma && k > 0 && alpha == 1.f && beta == 0.f && out_rs == n &&
+      dense_dma_eligible(m, n, k, a_cs, b_rs, b_cs) && gemm_forced_cfg() < 0) {
+    DenseDmaArgs da{};
+    da.M = m;
+    da.N = n;
+    da.K = k;
+    da.a = a;
+    da.a_rs = a_rs;
+    da.b = b;
+    da.b_rs = b_rs;
+    da.out = out;
+    da.out_rs = out_rs;
+    da.bias = bias;
+    da.act = act;
+    da.cfg = -1;
+    da.split = g_split_enabled;
+    return gemm_dense_dma(c, da);
   }
   return launch_gemm(d, s);
 }

@@ -103,6 +103,9 @@ struct GemmDesc {
 };
 // Small-M GEMM split at KC blocks (workspace = gemm_smallm_ws_floats).
 bool gemm_smallm_eligible(const GemmDesc& d);
+// Tile configuration forced for the general MFMA GEMM (tuning/tests), -1 if none;
+// while one is forced, dense GEMMs stay on that kernel.
+int gemm_forced_cfg();
 int64_t gemm_smallm_ws_floats(const GemmDesc& d);
 rtenhip_status launch_gemm_smallm(const GemmDesc& d, float* ws, hipStream_t s);
 rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s);

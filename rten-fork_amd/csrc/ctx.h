@@ -100,6 +100,39 @@ rtenhip_status gemm_impl(Ctx* c, int64_t m, int64_t n, int64_t k, const float* a
                          int64_t a_cs, const float* b, int64_t b_rs, int64_t b_cs, float* out,
                          int64_t out_rs, float alpha, float beta, const float* bias, int act);
 
+// Dense GEMM on the LDS-DMA kernel (MatMul / Gemm with a row-major A and B):
+//   out[m, n] = act(fold(A @ B) (+ bias[m]) (+ colbias[n]) (+ residual[m, n]))
+// A: [M, K] row stride a_rs, unit column stride; packed per call into pk
+// (packed_a_floats(M, K, dma_cfg_tile(cfg)) floats).  B: [K, N] row stride
+// b_rs, unit column stride, read in place through the K table koff(k) = k*b_rs.
+// out / residual: row strides out_rs / res_rs.  Same KC = 256 block order as
+// gemm_impl, so the result is bit-identical to the general kernel.
+struct DenseDmaArgs {
+  int64_t M, N, K;
+  const float* a;
+  int64_t a_rs;
+  const float* b;
+  int64_t b_rs;
+  float* out;
+  int64_t out_rs;
+  const float* bias;
+  const float* colbias;
+  const float* residual;
+  int64_t res_rs;
+  int act;
+  float lo, hi;
+  int cfg;         // -1 = dma_default_cfg
+  float* pk;       // packed-A buffer (nullptr: ctx scratch slot 2)
+  bool pack;       // pack A into pk first (false: pk already holds it)
+  bool split;      // KC split of the remainder tiles
+  float* ws;       // split workspace / zeroed counters (nullptr: ctx scratch)
+  int64_t ws_cap;
+  int* counters;
+  int64_t cnt_cap;
+};
+bool dense_dma_eligible(int64_t M, int64_t N, int64_t K, int64_t a_cs, int64_t b_rs, int64_t b_cs);
+rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a);
+
 // broadcast_shapes (src/ops/binary_elementwise.rs:23-45).
 bool broadcast_shapes(const int64_t* a, int an, const int64_t* b, int bn, int64_t* out, int* on);
 

@@ -42,6 +42,8 @@ struct DmaDesc {
   const float* residual;
   int64_t res_img, res_c;
   const float* bias;
+  const float* colbias;     // per-column bias colbias[p] (p = oy*OW + ox), added after the
+                            // K fold and before the residual (MatMul -> Add(bias[N]))
   const float* cin;         // beta != 0 (dense outputs only; out_c = row stride)
   float alpha, beta;
   int act;

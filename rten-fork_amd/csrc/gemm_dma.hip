@@ -22,6 +22,7 @@
 #include "common.h"
 #include "gemm_dma.h"
 #include "fastdiv_dev.h"
+#include "vecmath.h"
 
 namespace rtenhip {
 
@@ -525,6 +526,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
       x = fmaxf(x, 0.f);
     } else if (d.act == RTENHIP_ACT_CLIP) {
       x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+    } else if (d.act == RTENHIP_ACT_GELU) {
+      x = vm_gelu(x);
     }
     return x;
   };
@@ -561,6 +564,13 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
           const int m = tm + wm + mi * 32 + row;
           const bool ok = ncol_ok && m < M;
           float4 x = *(const float4*)(slot + row * 32 + c4);
+          if (d.colbias && ok) {
+            const float4 cb = *(const float4*)(d.colbias + p);
+            x.x = __fadd_rn(x.x, cb.x);
+            x.y = __fadd_rn(x.y, cb.y);
+            x.z = __fadd_rn(x.z, cb.z);
+            x.w = __fadd_rn(x.w, cb.w);
+          }
           if (d.residual && ok) {
             float4 r;
             if constexpr (RES_PRE)
@@ -607,6 +617,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         const int ml = lrow(mi, j);
         const bool ok = full_tile || (ncol_ok && ml <= m_lim);
         float x = v[j];
+        if (d.colbias) x = __fadd_rn(x, d.colbias[p]);
         if (d.residual) x = __fadd_rn(x, d.residual[ok ? rbase + (int64_t)(tm + ml) * d.res_c : 0]);
         x = apply_act(x);
         if (ok) d.out[obase + (int64_t)(tm + ml) * d.out_c] = x;
@@ -773,22 +784,30 @@ namespace rtenhip {
 
 // Pack A[M, K] (row stride lda, unit column stride) into
 // [tiles_m][tiles_k][BK][BM] tiles, zero padded, rows of each 32*il slab
-// interleaved: position l*il + mi holds row mi*32 + l.
-__global__ void pack_a_kernel(const float* __restrict__ a, int64_t lda, int M, int K, int BM,
-                              int BK, int il, int tiles_k, float* __restrict__ out, int64_t total) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int pos = (int)(i % BM);
-    const int64_t t = i / BM;
-    const int kk = (int)(t % BK);
-    const int64_t tile = t / BK;
-    const int kt = (int)(tile % tiles_k);
-    const int mt = (int)(tile / tiles_k);
-    const int slab = 32 * il;
+// interleaved: position l*il + mi holds row mi*32 + l.  One workgroup per
+// tile: rows are read as contiguous BK-float segments, transposed through
+// LDS, and the tile is written as one contiguous run.
+__global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a, int64_t lda,
+                                                     int M, int K, int BM, int BK, int il,
+                                                     int tiles_k, float* __restrict__ out) {
+  extern __shared__ float sh[];  // [BK][BM + 1]
+  const int tile = blockIdx.x;
+  const int mt = tile / tiles_k, kt = tile - mt * tiles_k;
+  const int n = BM * BK;
+  const int ld = BM + 1;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int r = i / BK, kk = i - r * BK;
+    const int m = mt * BM + r, k = kt * BK + kk;
+    sh[kk * ld + r] = (m < M && k < K) ? a[(int64_t)m * lda + k] : 0.f;
+  }
+  __syncthreads();
+  float* o = out + (int64_t)tile * n;
+  const int slab = 32 * il;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int kk = i / BM, pos = i - kk * BM;
     const int q = pos % slab;
     const int mm = (pos - q) + (q % il) * 32 + q / il;
-    const int m = mt * BM + mm, k = kt * BK + kk;
-    out[i] = (m < M && k < K) ? a[(int64_t)m * lda + k] : 0.f;
+    o[i] = sh[kk * ld + mm];
   }
 }
 
@@ -800,11 +819,13 @@ int64_t packed_a_floats(int M, int K, const DmaTile& t) {
 rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const DmaTile& t,
                              float* out, hipStream_t s) {
   const int tiles_k = (K + t.bk - 1) / t.bk;
-  const int64_t total = packed_a_floats(M, K, t);
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, lda, M, K, t.bm,
-                     t.bk, t.il, tiles_k, out, total);
+  const int tiles_m = (M + t.bm - 1) / t.bm;
+  const int64_t tiles = (int64_t)tiles_m * tiles_k;
+  if (tiles == 0) return RTENHIP_OK;
+  if (tiles > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "A too large to pack");
+  const size_t lds = (size_t)t.bk * (t.bm + 1) * sizeof(float);
+  hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)tiles), dim3(256), lds, s, a, lda, M, K, t.bm,
+                     t.bk, t.il, tiles_k, out);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

@@ -325,6 +325,7 @@ static int forced_cfg() {
   }
   return g_forced_cfg;
 }
+int gemm_forced_cfg() { return forced_cfg(); }
 
 }  // namespace rtenhip
 

@@ -78,10 +78,45 @@ Plan::~Plan() {
   }
   for (auto& kv : padded)
     if (kv.second.base) (void)hipFree(kv.second.base);
+  for (auto& kv : matmuls) {
+    if (kv.second.ws) (void)hipFree(kv.second.ws);
+    if (kv.second.counters) (void)hipFree(kv.second.counters);
+  }
+  if (mm_pack) (void)hipFree(mm_pack);
   for (auto& kv : side_events) {
     if (kv.second.first) (void)hipEventDestroy(kv.second.first);
     if (kv.second.second) (void)hipEventDestroy(kv.second.second);
   }
+}
+
+// FusedTranspose: the permuted view of an operator input (PermuteSpec::apply,
+// src/ops/fused.rs:16-38; an empty perm reverses the axes).
+static bool valid_perm(const std::vector<int64_t>& perm, size_t ndim) {
+  if (perm.empty()) return true;
+  if (perm.size() != ndim) return false;
+  std::vector<bool> seen(ndim, false);
+  for (int64_t p : perm) {
+    if (p < 0 || p >= (int64_t)ndim || seen[p]) return false;
+    seen[p] = true;
+  }
+  return true;
+}
+static int64_t perm_at(const std::vector<int64_t>& perm, size_t ndim, size_t i) {
+  return perm.empty() ? (int64_t)(ndim - 1 - i) : perm[i];
+}
+static Shape permute_shape(const Shape& s, const std::vector<int64_t>& perm) {
+  Shape r(s.size());
+  for (size_t i = 0; i < s.size(); i++) r[i] = s[perm_at(perm, s.size(), i)];
+  return r;
+}
+static rtenhip_tensor permute_desc(const rtenhip_tensor& t, const std::vector<int64_t>& perm) {
+  rtenhip_tensor r = t;
+  for (int i = 0; i < t.ndim; i++) {
+    const int64_t src = perm_at(perm, (size_t)t.ndim, (size_t)i);
+    r.shape[i] = t.shape[src];
+    r.strides[i] = t.strides[src];
+  }
+  return r;
 }
 
 // Conv attributes as conv_impl takes them.
@@ -309,8 +344,27 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   for (int op : p.ops) {
     std::vector<const Shape*> ins;
     for (int i : nodes[op].inputs) ins.push_back(shape_of(i));
+    std::vector<Shape> permuted(ins.size());
+    for (auto& kv : nodes[op].input_perm) {
+      const int idx = kv.first;
+      if (idx >= (int)ins.size() || !ins[idx]) continue;
+      if (!valid_perm(kv.second, ins[idx]->size()))
+        return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
+      permuted[idx] = permute_shape(*ins[idx], kv.second);
+      ins[idx] = &permuted[idx];
+    }
     std::vector<Shape> outs;
     rtenhip_status st = infer_shapes(op, ins, outs);
+    if (!st && nodes[op].op_type == "MatMul" && nodes[op].fused_residual >= 0) {
+      // MatMul -> [Add(bias)] -> Add(residual): the Add broadcasts.
+      const Shape* rs = shape_of(nodes[op].fused_residual);
+      int64_t bs[RTENHIP_MAX_DIMS];
+      int bn;
+      if (!rs || !broadcast_shapes(outs[0].data(), (int)outs[0].size(), rs->data(), (int)rs->size(), bs, &bn))
+        st = fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast inputs");
+      else
+        outs[0].assign(bs, bs + bn);
+    }
     if (st) {
       std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
       set_error(st, msg);
@@ -343,6 +397,36 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
                   ce.g) != RTENHIP_OK)
       continue;
     if (!ce.g.one_d && conv_takes_dma(ce.g)) p.convs[op] = ce;
+  }
+  // MatMuls that run on the dense DMA GEMM: A contiguous (batch folds into
+  // M), B 2-D (or with unit batch dims) with unit column stride.
+  for (int op : p.ops) {
+    const Node& n = nodes[op];
+    if (n.op_type != "MatMul" || n.inputs.size() < 2 || n.input_perm.count(0)) continue;
+    const Shape* as = shape_of(n.inputs[0]);
+    const Shape* bs0 = shape_of(n.inputs[1]);
+    if (!as || !bs0 || as->size() < 2 || bs0->size() < 2) continue;
+    rtenhip_tensor bt = desc(nullptr, *bs0);
+    auto bp = n.input_perm.find(1);
+    if (bp != n.input_perm.end()) bt = permute_desc(bt, bp->second);
+    int64_t nb = 1;
+    for (int i = 0; i < bt.ndim - 2; i++) nb *= bt.shape[i];
+    const int64_t K = (*as)[as->size() - 1];
+    const int64_t M = prod(*as) / std::max<int64_t>(K, 1);
+    const int64_t N = bt.shape[bt.ndim - 1];
+    if (nb != 1 || bt.shape[bt.ndim - 2] != K) continue;
+    if (n.fused_residual >= 0) {
+      const Shape* rs = shape_of(n.fused_residual);
+      if (!rs || *rs != shapes[n.outputs[0]] || prod(*rs) != M * N) continue;
+    }
+    const int64_t b_rs = bt.strides[bt.ndim - 2], b_cs = bt.strides[bt.ndim - 1];
+    if (!dense_dma_eligible(M, N, K, 1, b_rs, b_cs)) continue;
+    MatMulExec me;
+    me.M = M;
+    me.N = N;
+    me.K = K;
+    me.b_rs = b_rs;
+    p.matmuls[op] = me;
   }
   // Values produced by a DMA conv and read only (as input 0) by padded DMA
   // convs that agree on the padding get a persistent zero-bordered buffer.
@@ -566,7 +650,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       b.refs = -1;
       release(b.off, b.size);
     }
-    if (n.fused_residual >= 0) {
+    if (n.fused_residual >= 0 && n.op_type == "Conv") {
       const Shape* rs = shape_of(n.fused_residual);
       if (!rs || *rs != os)
         return fail(RTENHIP_UNSUPPORTED_VALUE, "Fused residual must match the Conv output shape");
@@ -681,8 +765,11 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
                                (int)n.attrs.num("transB", 0), &y);
   }
   if (t == "MatMul") {
-    rtenhip_tensor b = T(n.inputs[1]);
-    return rtenhip_matmul_f32(c, &x, &b, &y);
+    rtenhip_tensor a = x, b = T(n.inputs[1]);
+    auto p0 = n.input_perm.find(0), p1 = n.input_perm.find(1);
+    if (p0 != n.input_perm.end()) a = permute_desc(a, p0->second);
+    if (p1 != n.input_perm.end()) b = permute_desc(b, p1->second);
+    return exec_matmul(p, op_id, a, b, y);
   }
   if (t == "BatchNormalization") {
     return rtenhip_batch_norm_f32(c, &x, P(1), P(2), P(3), P(4), (float)n.attrs.num("epsilon", 1e-5), &y);
@@ -710,6 +797,185 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   std::string msg = "Unsupported operator type: " + t;
   set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
   return RTENHIP_UNSUPPORTED_VALUE;
+}
+
+// MatMul (matmul_impl, src/ops/matmul.rs:123-239) with the load-time fused
+// epilogue: + colbias[N] (MatMul -> Add(bias)), + residual (-> Add), act.
+// Large folded MatMuls run on the dense DMA GEMM with the epilogue in its
+// store; the rest run matmul_impl and apply the epilogue as the same f32
+// element-wise ops the unfused graph would run.
+rtenhip_status Graph::exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b,
+                                  rtenhip_tensor y) {
+  const Node& n = nodes[op_id];
+  auto mit = p.matmuls.find(op_id);
+  if (mit != p.matmuls.end() && ctx->use_dma && gemm_forced_cfg() < 0)
+    return exec_matmul_dma(p, op_id, a, b, y, mit->second);
+  rtenhip_ctx* c = cptr;
+  const bool fused = n.fused_colbias >= 0 || n.fused_residual >= 0 || n.fused_act;
+  if (!fused) return rtenhip_matmul_f32(c, &a, &b, &y);
+  // Plain MatMul result: into y, or into scratch when the residual Add
+  // broadcasts it to a larger shape.
+  int64_t mm_shape[RTENHIP_MAX_DIMS];
+  int pn = 0;
+  {
+    const int an = a.ndim, bn = b.ndim;
+    if (!broadcast_shapes(a.shape, an - 2, b.shape, bn - 2, mm_shape, &pn))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast shapes");
+    mm_shape[pn] = a.shape[an - 2];
+    mm_shape[pn + 1] = b.shape[bn - 1];
+  }
+  rtenhip_tensor mm = y;
+  bool same = mm.ndim == pn + 2;
+  for (int i = 0; same && i < pn + 2; i++) same = mm.shape[i] == mm_shape[i];
+  if (!same) {
+    int64_t cnt = 1;
+    for (int i = 0; i < pn + 2; i++) cnt *= mm_shape[i];
+    float* tmp = ctx->scratch_floats((size_t)std::max<int64_t>(cnt, 1), 1);
+    if (!tmp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    mm = desc(tmp, Shape(mm_shape, mm_shape + pn + 2));
+  }
+  rtenhip_status st = rtenhip_matmul_f32(c, &a, &b, &mm);
+  if (st) return st;
+  if (n.fused_colbias >= 0) {
+    const Node& cb = nodes[n.fused_colbias];
+    rtenhip_tensor cbt = desc(cb.dev, cb.shape);
+    st = rtenhip_binary_f32(c, RTENHIP_BINARY_ADD, &mm, &cbt, &mm);
+    if (st) return st;
+  }
+  if (n.fused_residual >= 0) {
+    const Shape* rs = plan_shape(*this, p, n.fused_residual);
+    rtenhip_tensor r = desc(ptr_of(p, n.fused_residual), rs ? *rs : Shape());
+    st = rtenhip_binary_f32(c, RTENHIP_BINARY_ADD, &mm, &r, &y);
+    if (st) return st;
+  }
+  if (n.fused_act == RTENHIP_ACT_RELU) return rtenhip_unary_f32(c, RTENHIP_UNARY_RELU, &y, 0.f, 0.f, &y);
+  if (n.fused_act == RTENHIP_ACT_CLIP)
+    return rtenhip_unary_f32(c, RTENHIP_UNARY_CLIP, &y, n.act_lo, n.act_hi, &y);
+  if (n.fused_act == RTENHIP_ACT_GELU) return rtenhip_unary_f32(c, RTENHIP_UNARY_GELU, &y, 0.f, 0.f, &y);
+  return RTENHIP_OK;
+}
+
+// Dense DMA MatMul.  A is packed per run into the plan's shared buffer; on the
+// plan's first (eager) run the tile configuration and KC split are chosen by
+// timing the candidates on the real operands (all bit-identical).
+rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& a,
+                                      const rtenhip_tensor& b, const rtenhip_tensor& y,
+                                      MatMulExec& me) {
+  const Node& n = nodes[op_id];
+  hipStream_t s = ctx->stream;
+  if (!is_contiguous(a)) return fail(RTENHIP_UNSUPPORTED_VALUE, "dense MatMul needs a contiguous A");
+  DenseDmaArgs da{};
+  da.M = me.M;
+  da.N = me.N;
+  da.K = me.K;
+  da.a = a.data;
+  da.a_rs = me.K;
+  da.b = b.data;
+  da.b_rs = me.b_rs;
+  da.out = y.data;
+  da.out_rs = me.N;
+  da.colbias = n.fused_colbias >= 0 ? nodes[n.fused_colbias].dev : nullptr;
+  da.residual = ptr_of(p, n.fused_residual);
+  da.res_rs = me.N;
+  da.act = n.fused_act;
+  da.lo = n.act_lo;
+  da.hi = n.act_hi;
+  da.pack = true;
+  auto ensure_pack = [&](int cfg) -> rtenhip_status {
+    const int64_t need = packed_a_floats((int)me.M, (int)me.K, dma_cfg_tile(cfg));
+    if (need > p.mm_pack_floats) {
+      RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
+      if (p.mm_pack) RTENHIP_HIP_CHECK(hipFree(p.mm_pack));
+      p.mm_pack = nullptr;
+      RTENHIP_HIP_CHECK(hipMalloc(&p.mm_pack, (size_t)need * 4));
+      p.mm_pack_floats = need;
+    }
+    return RTENHIP_OK;
+  };
+  auto set_split = [&](MatMulExec& e, int cfg, bool split) -> rtenhip_status {
+    e.split = false;
+    if (!split) return RTENHIP_OK;
+    const DmaSplit sp = dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg);
+    if (sp.split_tiles == 0) return RTENHIP_OK;
+    if (sp.ws_floats > e.ws_floats) {
+      if (e.ws) RTENHIP_HIP_CHECK(hipFree(e.ws));
+      e.ws = nullptr;
+      RTENHIP_HIP_CHECK(hipMalloc(&e.ws, (size_t)sp.ws_floats * 4));
+      e.ws_floats = sp.ws_floats;
+    }
+    if (sp.counters > e.n_counters) {
+      if (e.counters) RTENHIP_HIP_CHECK(hipFree(e.counters));
+      e.counters = nullptr;
+      RTENHIP_HIP_CHECK(hipMalloc(&e.counters, (size_t)sp.counters * 4));
+      RTENHIP_HIP_CHECK(hipMemsetAsync(e.counters, 0, (size_t)sp.counters * 4, s));
+      e.n_counters = sp.counters;
+    }
+    e.split = true;
+    return RTENHIP_OK;
+  };
+  auto bind = [&](const MatMulExec& e, int cfg) {
+    da.cfg = cfg;
+    da.split = e.split;
+    da.ws = e.ws;
+    da.ws_cap = e.ws_floats;
+    da.counters = e.counters;
+    da.cnt_cap = e.n_counters;
+    da.pk = p.mm_pack;
+  };
+  if (me.cfg < 0) {
+    int chosen = dma_default_cfg((int)me.M, (int)me.N, (int)me.K);
+    bool chosen_split = false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(s, &cs);
+    if (autotune && cs == hipStreamCaptureStatusNone && da.residual != da.out) {
+      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18};
+      hipEvent_t e0, e1;
+      RTENHIP_HIP_CHECK(hipEventCreate(&e0));
+      RTENHIP_HIP_CHECK(hipEventCreate(&e1));
+      float best_ms = 1e30f;
+      MatMulExec trial = me;
+      trial.ws = nullptr;
+      trial.counters = nullptr;
+      trial.ws_floats = trial.n_counters = 0;
+      for (int cfg : kCandidates) {
+        if (cfg >= dma_num_cfgs()) continue;
+        rtenhip_status st = ensure_pack(cfg);
+        if (st) return st;
+        for (int split = 0; split < 2; split++) {
+          if (split && dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg).split_tiles == 0) continue;
+          st = set_split(trial, cfg, split != 0);
+          if (st) return st;
+          bind(trial, cfg);
+          st = gemm_dense_dma(ctx, da);  // warm-up (the output is rewritten below)
+          if (st) return st;
+          RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
+          for (int r = 0; r < 3 && !st; r++) st = gemm_dense_dma(ctx, da);
+          if (st) return st;
+          RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
+          RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
+          float ms = 0;
+          RTENHIP_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+          if (ms < best_ms) {
+            best_ms = ms;
+            chosen = cfg;
+            chosen_split = split != 0;
+          }
+        }
+      }
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+      RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
+      if (trial.ws) (void)hipFree(trial.ws);
+      if (trial.counters) (void)hipFree(trial.counters);
+    }
+    rtenhip_status st = ensure_pack(chosen);
+    if (st) return st;
+    st = set_split(me, chosen, chosen_split);
+    if (st) return st;
+    me.cfg = chosen;
+  }
+  bind(me, me.cfg);
+  return gemm_dense_dma(ctx, da);
 }
 
 // DMA conv with plan-owned packed weights and zero-bordered inputs/outputs.
@@ -1065,7 +1331,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         per_op[i] = ms;
         const Node& n = nodes[plan->ops[i]];
         std::string key = n.op_type;
-        if (n.op_type == "Conv" && (n.fused_residual >= 0 || n.fused_act)) key = "Conv(fused)";
+        if ((n.op_type == "Conv" || n.op_type == "MatMul") &&
+            (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0))
+          key = n.op_type + "(fused)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -1194,6 +1462,84 @@ rtenhip_status Graph::optimize() {
       a.removed = true;
       conv.outputs[0] = a.outputs[0];
       fused++;
+    }
+  }
+  // FusedTranspose (optimize.rs:329-378): a MatMul reads a Transpose's input
+  // as a permuted view instead of the materialised copy.  The Transpose stays
+  // in the graph and is only planned if something else still reads it.
+  std::map<int, int> producer;
+  for (int i = 0; i < (int)nodes.size(); i++)
+    if (nodes[i].kind == NodeKind::Operator && !nodes[i].removed)
+      for (int o : nodes[i].outputs) producer[o] = i;
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& mm = nodes[i];
+    if (mm.kind != NodeKind::Operator || mm.removed || mm.op_type != "MatMul") continue;
+    for (int k = 0; k < 2 && k < (int)mm.inputs.size(); k++) {
+      auto it = producer.find(mm.inputs[k]);
+      if (it == producer.end() || mm.input_perm.count(k)) continue;
+      const Node& tr = nodes[it->second];
+      if (tr.op_type != "Transpose" || tr.inputs.empty() || tr.inputs[0] < 0) continue;
+      mm.input_perm[k] = tr.attrs.ints("perm", {});
+      mm.inputs[k] = tr.inputs[0];
+      fused++;
+    }
+  }
+  // MatMul epilogue: MatMul -> Add(constant bias [N]) -> Add(residual) ->
+  // Relu|Clip|Gelu, each step only when its value has that sole consumer and
+  // in this order (the order of the f32 adds is kept).
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& mm = nodes[i];
+    if (mm.kind != NodeKind::Operator || mm.removed || mm.op_type != "MatMul") continue;
+    if (mm.outputs.size() != 1 || mm.fused_colbias >= 0 || mm.fused_residual >= 0 || mm.fused_act)
+      continue;
+    int64_t ncols = -1;  // N when B is a constant
+    if (mm.inputs.size() > 1 && mm.inputs[1] >= 0 && nodes[mm.inputs[1]].kind == NodeKind::Constant &&
+        !mm.input_perm.count(1) && nodes[mm.inputs[1]].shape.size() >= 2)
+      ncols = nodes[mm.inputs[1]].shape.back();
+    int v = mm.outputs[0];
+    int nxt = sole(v);
+    auto other_of = [&](const Node& a) { return a.inputs[0] == v ? a.inputs[1] : a.inputs[0]; };
+    if (nxt >= 0 && !nodes[nxt].removed && nodes[nxt].op_type == "Add" && nodes[nxt].inputs.size() == 2 &&
+        nodes[nxt].outputs.size() == 1) {
+      const int o = other_of(nodes[nxt]);
+      bool colbias = o >= 0 && o != v && nodes[o].kind == NodeKind::Constant && ncols > 0 &&
+                     !nodes[o].shape.empty() && nodes[o].shape.back() == ncols &&
+                     prod(nodes[o].shape) == ncols;
+      if (colbias) {
+        mm.fused_colbias = o;
+        nodes[nxt].removed = true;
+        v = mm.outputs[0] = nodes[nxt].outputs[0];
+        fused++;
+        nxt = sole(v);
+      }
+    }
+    if (nxt >= 0 && !nodes[nxt].removed && nodes[nxt].op_type == "Add" && nodes[nxt].inputs.size() == 2 &&
+        nodes[nxt].outputs.size() == 1) {
+      const int o = other_of(nodes[nxt]);
+      if (o >= 0 && o != v) {
+        mm.fused_residual = o;
+        nodes[nxt].removed = true;
+        v = mm.outputs[0] = nodes[nxt].outputs[0];
+        fused++;
+        nxt = sole(v);
+      }
+    }
+    if (nxt >= 0 && !nodes[nxt].removed) {
+      int act;
+      float lo, hi;
+      if (nodes[nxt].op_type == "Gelu") {
+        mm.fused_act = RTENHIP_ACT_GELU;
+        nodes[nxt].removed = true;
+        mm.outputs[0] = nodes[nxt].outputs[0];
+        fused++;
+      } else if (act_of(nxt, act, lo, hi)) {
+        mm.fused_act = act;
+        mm.act_lo = lo;
+        mm.act_hi = hi;
+        nodes[nxt].removed = true;
+        mm.outputs[0] = nodes[nxt].outputs[0];
+        fused++;
+      }
     }
   }
   for (auto& pl : plans)

@@ -61,6 +61,12 @@ struct Node {
   int fused_residual = -1;   // value id added after the bias
   int fused_act = 0;         // RTENHIP_ACT_*
   float act_lo = 0.f, act_hi = 0.f;
+  // MatMul epilogue: constant [N] added per column after the K fold
+  // (MatMul -> Add(bias)), before the residual and the activation.
+  int fused_colbias = -1;
+  // FusedTranspose (src/ops/fused.rs:45-80): input index -> permutation of
+  // that input's view (empty = reversed axes, Transpose without perm).
+  std::map<int, std::vector<int64_t>> input_perm;
   bool removed = false;      // op folded into another
   bool alias_input0 = false; // output is a view of input 0 (Flatten/Reshape)
 };
@@ -82,6 +88,17 @@ struct ConvExec {
   int64_t ws_floats = 0, n_counters = 0;
 };
 
+// A MatMul the plan runs on the dense LDS-DMA GEMM: [batch.., M, K] @ [K, N]
+// with the batch folded into M (matmul.rs:162-169), A contiguous.
+struct MatMulExec {
+  int64_t M, N, K, b_rs;
+  int cfg = -1;          // kernel configuration (chosen on the first run)
+  bool split = false;
+  float* ws = nullptr;   // split workspace and arrival counters, plan-owned
+  int* counters = nullptr;
+  int64_t ws_floats = 0, n_counters = 0;
+};
+
 // A value stored with a zero border so the DMA convs reading it need no
 // per-run padding copy: physical [N, C, H + pt + pb, W + pl + pr], written by
 // its producer (a DMA conv) into the interior.  Persistent, outside the arena,
@@ -97,6 +114,9 @@ struct Plan {
   std::vector<int> ops;               // topological order
   std::map<int, ConvExec> convs;      // op id -> DMA conv state
   std::map<int, PaddedValue> padded;  // value id -> zero-bordered storage
+  std::map<int, MatMulExec> matmuls;  // op id -> dense DMA MatMul state
+  float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
+  int64_t mm_pack_floats = 0;
   // Ops launched on the side stream (independent branches such as the
   // ResNet downsample conv), and for each op the side ops it must wait for.
   std::set<int> side;
@@ -148,6 +168,9 @@ struct Graph {
                               std::vector<Shape>& outs);
   rtenhip_status exec_op(Plan& p, int op_id);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
+  rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
+  rtenhip_status exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& a,
+                                 const rtenhip_tensor& b, const rtenhip_tensor& y, MatMulExec& me);
   float* ptr_of(Plan& p, int value_id);
 };
 

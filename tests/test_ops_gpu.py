@@ -71,7 +71,9 @@ def assert_bits(actual, expected, what=""):
 
 GEMM_SHAPES = [(1, 1, 1), (2, 3, 4), (7, 17, 33), (64, 64, 64), (65, 130, 257), (128, 128, 256),
                (100, 300, 600), (33, 1025, 300), (257, 129, 1000), (64, 1000, 2048),
-               (16, 16, 0)]
+               (16, 16, 0),
+               # dense LDS-DMA route (A packed per call, B read in place)
+               (256, 256, 256), (300, 516, 700), (520, 768, 1030), (512, 3072, 768)]
 
 
 @pytest.mark.parametrize("m,n,k", GEMM_SHAPES)
@@ -93,6 +95,16 @@ def test_gemm_alpha_beta(rh, oracle):
         out = dev(init)
         rh.gemm(dev(a), dev(b), alpha, beta, out=out)
         assert_bits(host(out), exp, f"alpha={alpha} beta={beta}")
+
+
+def test_gemm_strided_b_rows(rh, oracle):
+    """B with a row stride larger than N (a column slice) on the dense DMA route."""
+    m, n, k = 260, 512, 300
+    a = rnd(oracle, 12, m, k)
+    bfull = rnd(oracle, 13, k, n + 64)
+    exp = oracle.gemm(a, np.ascontiguousarray(bfull[:, 32:32 + n]))
+    got = host(rh.gemm(dev(a), dev(bfull)[:, 32:32 + n]))
+    assert_bits(got, exp, "strided B rows")
 
 
 def test_gemm_transposed_views(rh, oracle):
@@ -282,7 +294,10 @@ def test_gemm_op_fc_bitexact(rh, oracle, batch):
 
 
 @pytest.mark.parametrize("sa,sb", [((2, 3, 5, 64), (3, 64, 7)), ((4, 33, 70), (70, 9)),
-                                   ((2, 12, 128, 64), (2, 12, 64, 128)), ((6, 1, 40), (6, 40, 30))])
+                                   ((2, 12, 128, 64), (2, 12, 64, 128)), ((6, 1, 40), (6, 40, 30)),
+                                   # BERT projections: batch folded into M, dense DMA route
+                                   ((4, 128, 768), (768, 768)), ((2, 128, 3072), (3072, 768)),
+                                   ((3, 100, 260), (260, 1028))])
 def test_matmul_bitexact(rh, oracle, sa, sb):
     a = rnd(oracle, 111, *sa)
     b = rnd(oracle, 112, *sb)
