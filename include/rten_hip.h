@@ -70,6 +70,9 @@ void rtenhip_destroy(rtenhip_ctx* ctx);
 rtenhip_status rtenhip_set_stream(rtenhip_ctx* ctx, void* stream);
 void* rtenhip_get_stream(rtenhip_ctx* ctx);
 const char* rtenhip_last_error_message(void);
+/* Status code of the last error on this thread (for entry points that return
+ * a handle rather than a status, e.g. rtenhip_model_load). */
+int32_t rtenhip_last_error_code(void);
 /* Blocks until the context's stream is idle. */
 rtenhip_status rtenhip_synchronize(rtenhip_ctx* ctx);
 /* Device memory helpers (hipMalloc / hipFree / hipMemcpy H2D, D2H, D2D). */
@@ -223,6 +226,15 @@ const char* rtenhip_graph_timing_report(rtenhip_graph* g);
 /* .rten V2 model loader (src/model.rs:265-522): parses the file bytes (host),
  * uploads constants, builds the graph.  Returns NULL on error. */
 rtenhip_graph* rtenhip_model_load(rtenhip_ctx* ctx, const uint8_t* bytes, size_t len);
+/* Model::load with ModelOptions::with_optimize (src/model.rs:156-162, 190-199):
+ * optimize = 0 keeps the graph as stored (no load-time fusion). */
+rtenhip_graph* rtenhip_model_load_with_options(rtenhip_ctx* ctx, const uint8_t* bytes, size_t len,
+                                               int optimize);
+/* Parse a .rten file on the host only (no device) and return a text listing of
+ * its nodes (index, kind, name, op type, decoded attributes, constant shape and
+ * checksum), or NULL with the load error in rtenhip_last_error_message().
+ * Errors use the reference's ModelLoadError texts (model.rs:677-689). */
+const char* rtenhip_model_describe(const uint8_t* bytes, size_t len);
 int32_t rtenhip_model_input_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
 int32_t rtenhip_model_output_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
 int32_t rtenhip_graph_node_id(rtenhip_graph* g, const char* name);

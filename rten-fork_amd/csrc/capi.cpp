@@ -19,9 +19,10 @@
 namespace rtenhip {
 
 static thread_local std::string g_err;
+static thread_local int g_err_code = 0;
 
 void set_error(int code, const std::string& msg) {
-  (void)code;
+  g_err_code = code;
   g_err = msg;
 }
 rtenhip_status fail(rtenhip_status code, const char* msg) {
@@ -692,6 +693,7 @@ rtenhip_status rtenhip_set_stream(rtenhip_ctx* ctx, void* stream) {
 void* rtenhip_get_stream(rtenhip_ctx* ctx) { return C_(ctx)->stream; }
 
 const char* rtenhip_last_error_message(void) { return g_err.c_str(); }
+int32_t rtenhip_last_error_code(void) { return g_err_code; }
 
 rtenhip_status rtenhip_synchronize(rtenhip_ctx* ctx) {
   RTENHIP_HIP_CHECK(hipStreamSynchronize(C_(ctx)->stream));

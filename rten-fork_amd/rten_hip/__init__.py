@@ -72,9 +72,16 @@ def lib():
                 L.rtenhip_graph_destroy.argtypes = [C.c_void_p]
                 L.rtenhip_graph_timing_report.restype = C.c_char_p
                 L.rtenhip_graph_timing_report.argtypes = [C.c_void_p]
-            if hasattr(L, "rtenhip_model_load"):
-                L.rtenhip_model_load.restype = C.c_void_p
-                L.rtenhip_model_load.argtypes = [C.c_void_p, C.c_char_p, C.c_size_t]
+            L.rtenhip_last_error_code.restype = C.c_int32
+            L.rtenhip_model_load.restype = C.c_void_p
+            L.rtenhip_model_load.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t]
+            L.rtenhip_model_load_with_options.restype = C.c_void_p
+            L.rtenhip_model_load_with_options.argtypes = [C.c_void_p, C.POINTER(C.c_uint8),
+                                                          C.c_size_t, C.c_int]
+            L.rtenhip_model_describe.restype = C.c_char_p
+            L.rtenhip_model_describe.argtypes = [C.POINTER(C.c_uint8), C.c_size_t]
+            L.rtenhip_model_input_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
+            L.rtenhip_model_output_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
             _lib = L
     return _lib
 
@@ -90,7 +97,8 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_create", "rtenhip_graph_destroy", "rtenhip_graph_add_value",
     "rtenhip_graph_add_constant", "rtenhip_graph_add_op", "rtenhip_graph_optimize",
     "rtenhip_graph_run", "rtenhip_graph_value_shape", "rtenhip_graph_set_timing",
-    "rtenhip_graph_timing_report", "rtenhip_model_load", "rtenhip_model_input_ids",
+    "rtenhip_graph_timing_report", "rtenhip_model_load", "rtenhip_model_load_with_options",
+    "rtenhip_model_describe", "rtenhip_last_error_code", "rtenhip_model_input_ids",
     "rtenhip_model_output_ids", "rtenhip_graph_node_id", "rtenhip_graph_set_io",
     "rtenhip_graph_plan",
 ]

@@ -1,0 +1,303 @@
+""".rten V2 model files: writer (the layout rten-convert produces,
+rten-convert/rten_convert/converter.py:1395-1545 and tensor_data.py) and the
+device loader binding (``load_model`` -> rtenhip_model_load, src/model.rs:265-522).
+
+The file is a 32-byte header (src/header.rs:57-146: b"RTEN", version 2, model
+offset/length, tensor-data offset), a FlatBuffers ``Model`` (src/schema.fbs,
+schema_version 1) and a 64-byte-aligned tensor-data segment holding large
+constants (``ConstantNode.data_offset``); small constants are stored inline.
+There is no flatbuffers package in this image, so ``_Builder`` is a minimal
+FlatBuffers encoder: tables with vtables, scalar/offset vectors, strings and
+unions, children laid out after their parents (uoffsets point forward).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+# sg::OperatorType (schema.fbs:12-121), enum order.
+OP_TYPES = [
+    "Add", "ArgMin", "ArgMax", "AveragePool", "BatchNormalization", "Cast", "Clip", "Concat",
+    "ConstantOfShape", "Conv", "ConvTranspose", "Cos", "CumSum", "Div", "Equal", "Erf", "Expand",
+    "Flatten", "Gather", "Gemm", "GlobalAveragePool", "Greater", "GRU", "Identity", "LeakyRelu",
+    "Less", "LessOrEqual", "Log", "LogSoftmax", "LSTM", "MatMul", "MaxPool", "Mod", "Mul", "Pad",
+    "Pow", "Range", "ReduceMean", "ReduceL2", "Relu", "Reshape", "Resize", "Shape", "Sigmoid",
+    "Sin", "Slice", "Split", "Sqrt", "Squeeze", "Softmax", "Sub", "Tanh", "Transpose", "Unsqueeze",
+    "Where", "ReduceProd", "ReduceSum", "ReduceMin", "ReduceMax", "NonZero", "ScatterElements",
+    "Tile", "Not", "Abs", "Max", "Mean", "Min", "Sum", "OneHot", "Round", "Floor", "Ceil",
+    "Reciprocal", "TopK", "Neg", "Exp", "GreaterOrEqual", "Size", "Tan", "Acos", "Asin", "Atan",
+    "InstanceNormalization", "HardSigmoid", "HardSwish", "And", "Or", "Xor", "Trilu", "ScatterND",
+    "NonMaxSuppression", "Sign", "GatherElements", "LayerNormalization", "ReduceSumSquare",
+    "RandomUniform", "Elu", "RandomUniformLike", "RandomNormal", "RandomNormalLike", "Softplus",
+    "GatherND", "Gelu", "Einsum", "If"]
+
+# sg::OperatorAttrs union ids (schema.fbs OperatorAttrs, NONE = 0).
+ATTRS_AVERAGE_POOL, ATTRS_BATCH_NORM, ATTRS_CONV, ATTRS_FLATTEN = 2, 3, 7, 9
+ATTRS_GEMM, ATTRS_MAX_POOL, ATTRS_RESHAPE, ATTRS_SOFTMAX = 11, 15, 17, 20
+ATTRS_TRANSPOSE, ATTRS_LAYER_NORM, ATTRS_GELU = 21, 30, 37
+NODE_OPERATOR, NODE_CONSTANT, NODE_VALUE = 1, 2, 3
+CONST_FLOAT_DATA, CONST_INT_DATA = 1, 2
+DTYPE_INT32, DTYPE_FLOAT32 = 0, 1
+AUTOPAD_SAME, AUTOPAD_NOTSET = 0, 1
+
+HEADER_LEN = 32
+TENSOR_ALIGN = 64
+INLINE_MAX_ELEMS = 16
+
+_SCALAR = {"u8": "<B", "bool": "<B", "u16": "<H", "i32": "<i", "u32": "<I", "f32": "<f",
+           "u64": "<Q"}
+
+
+class Table:
+    """A FlatBuffers table: fields = [(slot, kind, value)]; kind is a scalar
+    kind from _SCALAR or "ref" (value: Table / Vector / String)."""
+
+    def __init__(self, fields):
+        self.fields = [f for f in fields if f[2] is not None]
+
+
+class Vector:
+    def __init__(self, kind: str, items):
+        self.kind = kind            # "u32" | "i32" | "f32" | "ref"
+        self.items = items
+
+
+class String:
+    def __init__(self, s: str):
+        self.data = s.encode()
+
+
+class _Builder:
+    """Forward FlatBuffers encoder: the root offset at 0, then each object
+    appended after the one that references it."""
+
+    def __init__(self):
+        self.buf = bytearray(4)
+        self.queue: List[Tuple[int, object]] = []
+
+    def _align(self, a: int, extra: int = 0):
+        while (len(self.buf) + extra) % a:
+            self.buf.append(0)
+
+    def _put(self, fmt: str, v):
+        self.buf += struct.pack(fmt, v)
+
+    def _place(self, obj) -> int:
+        if isinstance(obj, String):
+            self._align(4)
+            pos = len(self.buf)
+            self._put("<I", len(obj.data))
+            self.buf += obj.data + b"\0"
+            return pos
+        if isinstance(obj, Vector):
+            esize = 8 if obj.kind == "u64" else 4
+            self._align(max(4, esize), 4)
+            pos = len(self.buf)
+            self._put("<I", len(obj.items))
+            if obj.kind == "ref":
+                for it in obj.items:
+                    self.queue.append((len(self.buf), it))
+                    self._put("<I", 0)
+            elif obj.kind == "f32":
+                self.buf += np.asarray(obj.items, "<f4").tobytes()
+            else:
+                self.buf += struct.pack("<%d%s" % (len(obj.items), _SCALAR[obj.kind][1]),
+                                        *obj.items)
+            return pos
+        assert isinstance(obj, Table)
+        size = {k: struct.calcsize(f) for k, f in _SCALAR.items()}
+        size["ref"] = 4
+        fields = sorted(obj.fields, key=lambda f: -size[f[1]])
+        # inline layout: soffset at 0, fields by descending size, each aligned
+        offs, cur = {}, 4
+        for slot, kind, _ in fields:
+            sz = size[kind]
+            cur = (cur + sz - 1) // sz * sz
+            offs[slot] = cur
+            cur += sz
+        tsize = (cur + 3) // 4 * 4
+        nslots = max([f[0] for f in fields], default=-1) + 1
+        # vtable right before the table
+        self._align(2)
+        vt = len(self.buf)
+        self._put("<H", 4 + 2 * nslots)
+        self._put("<H", tsize)
+        for s in range(nslots):
+            self._put("<H", offs.get(s, 0))
+        self._align(8)
+        pos = len(self.buf)
+        self.buf += bytes(tsize)
+        struct.pack_into("<i", self.buf, pos, pos - vt)
+        for slot, kind, v in fields:
+            if kind == "ref":
+                self.queue.append((pos + offs[slot], v))
+            else:
+                struct.pack_into(_SCALAR[kind], self.buf, pos + offs[slot], v)
+        return pos
+
+    def finish(self, root: Table) -> bytes:
+        self.queue.append((0, root))
+        while self.queue:
+            at, obj = self.queue.pop(0)
+            pos = self._place(obj)
+            struct.pack_into("<I", self.buf, at, pos - at)
+        self._align(8)
+        return bytes(self.buf)
+
+
+def _u32v(v):
+    return Vector("u32", [int(x) for x in v])
+
+
+def _op_attrs(op_type: str, a: dict):
+    """(union type, attrs table) as rten-convert writes them."""
+    def padding(fields_at):
+        auto, pads = fields_at
+        if str(a.get("auto_pad", "notset")).lower() in ("same", "same_upper"):
+            return [(auto, "u8", AUTOPAD_SAME)]
+        return [(auto, "u8", AUTOPAD_NOTSET), (pads, "ref", _u32v(a.get("pads", [0, 0, 0, 0])))]
+
+    if op_type == "Conv":
+        return ATTRS_CONV, Table(padding((0, 1)) + [
+            (2, "u32", int(a.get("groups", 1))),
+            (3, "ref", _u32v(a.get("strides", [1, 1]))),
+            (4, "ref", _u32v(a.get("dilations", [1, 1])))])
+    if op_type in ("MaxPool", "AveragePool"):
+        f = [(0, "ref", _u32v(a["kernel_size"]))] + padding((1, 2)) + [
+            (3, "ref", _u32v(a.get("strides", [1, 1])))]
+        if op_type == "AveragePool":
+            f.append((4, "bool", int(bool(a.get("count_include_pad", 0)))))
+            return ATTRS_AVERAGE_POOL, Table(f)
+        return ATTRS_MAX_POOL, Table(f)
+    if op_type == "BatchNormalization":
+        return ATTRS_BATCH_NORM, Table([(0, "f32", float(a.get("epsilon", 1e-5)))])
+    if op_type == "Gemm":
+        return ATTRS_GEMM, Table([(0, "f32", float(a.get("alpha", 1.0))),
+                                  (1, "f32", float(a.get("beta", 1.0))),
+                                  (2, "bool", int(bool(a.get("transA", 0)))),
+                                  (3, "bool", int(bool(a.get("transB", 0))))])
+    if op_type == "Flatten":
+        return ATTRS_FLATTEN, Table([(0, "i32", int(a.get("axis", 1)))])
+    if op_type == "Softmax":
+        return ATTRS_SOFTMAX, Table([(0, "i32", int(a.get("axis", -1)))])
+    if op_type == "LayerNormalization":
+        return ATTRS_LAYER_NORM, Table([(0, "i32", int(a.get("axis", -1))),
+                                        (1, "f32", float(a.get("epsilon", 1e-5)))])
+    if op_type == "Transpose":
+        perm = a.get("perm")
+        return ATTRS_TRANSPOSE, Table([(0, "ref", _u32v(perm) if perm is not None else None)])
+    if op_type == "Reshape":
+        return ATTRS_RESHAPE, Table([(0, "bool", int(bool(a.get("allowzero", 0))))])
+    if op_type == "Gelu":
+        return ATTRS_GELU, Table([])
+    return 0, None
+
+
+def to_rten_bytes(spec, inline_max: int = INLINE_MAX_ELEMS) -> bytes:
+    """Serialize a ModelSpec as a .rten V2 file.  Constants read as a shape
+    (Reshape input 1) are stored as int32, like an ONNX export."""
+    index: Dict[str, int] = {n.name: i for i, n in enumerate(spec.nodes)}
+    int_consts = set()
+    for n in spec.nodes:
+        if n.kind == "op" and n.op_type == "Reshape" and len(n.inputs) > 1 and n.inputs[1]:
+            int_consts.add(n.inputs[1])
+    tensors: List[np.ndarray] = []
+    tensor_off = 0
+    nodes = []
+    for n in spec.nodes:
+        if n.kind == "value":
+            data = Table([(0, "ref", None)])
+            kind = NODE_VALUE
+        elif n.kind == "const":
+            arr = np.asarray(n.data)
+            is_int = n.name in int_consts
+            arr = arr.astype("<i4" if is_int else "<f4")
+            shape = _u32v(arr.shape)
+            if arr.size <= inline_max:
+                payload = Table([(0, "ref", Vector("i32" if is_int else "f32", arr.reshape(-1).tolist()))])
+                data = Table([(0, "ref", shape), (1, "u8", CONST_INT_DATA if is_int else CONST_FLOAT_DATA),
+                              (2, "ref", payload)])
+            else:
+                pad = (-tensor_off) % TENSOR_ALIGN
+                tensor_off += pad
+                tensors.append((tensor_off, arr))
+                data = Table([(0, "ref", shape), (3, "u16", DTYPE_INT32 if is_int else DTYPE_FLOAT32),
+                              (4, "u64", tensor_off)])
+                tensor_off += arr.size * 4
+            kind = NODE_CONSTANT
+        else:
+            at, attrs = _op_attrs(n.op_type, n.attrs)
+            fields = [(0, "u8", OP_TYPES.index(n.op_type)),
+                      (3, "ref", Vector("i32", [-1 if i is None else index[i] for i in n.inputs])),
+                      (4, "ref", Vector("i32", [index[o] for o in n.outputs]))]
+            if attrs is not None:
+                fields += [(1, "u8", at), (2, "ref", attrs)]
+            data = Table(fields)
+            kind = NODE_OPERATOR
+        nodes.append(Table([(0, "ref", String(n.name)), (1, "u8", kind), (2, "ref", data)]))
+    graph = Table([(0, "ref", Vector("ref", nodes)),
+                   (1, "ref", _u32v([index[i] for i in spec.inputs])),
+                   (2, "ref", _u32v([index[o] for o in spec.outputs]))])
+    model = Table([(0, "i32", 1), (1, "ref", graph)])
+    fb = _Builder().finish(model)
+    tensor_data_offset = (HEADER_LEN + len(fb) + TENSOR_ALIGN - 1) // TENSOR_ALIGN * TENSOR_ALIGN
+    out = bytearray(b"RTEN" + struct.pack("<IQQQ", 2, HEADER_LEN, len(fb), tensor_data_offset))
+    out += fb
+    out += bytes(tensor_data_offset - len(out))
+    for off, arr in tensors:
+        out += bytes(tensor_data_offset + off - len(out))
+        out += arr.tobytes()
+    return bytes(out)
+
+
+def write_rten(spec, path: str, **kw) -> None:
+    with open(path, "wb") as f:
+        f.write(to_rten_bytes(spec, **kw))
+
+
+def _bytes(src) -> bytes:
+    if isinstance(src, (bytes, bytearray)):
+        return bytes(src)
+    with open(os.fspath(src), "rb") as f:
+        return f.read()
+
+
+def describe_model(src) -> str:
+    """Host-only parse of a .rten file (rtenhip_model_describe)."""
+    from . import OpError, lib
+
+    data = _bytes(src)
+    buf = C.create_string_buffer(data, len(data))
+    r = lib().rtenhip_model_describe(C.cast(buf, C.POINTER(C.c_uint8)), C.c_size_t(len(data)))
+    if not r:
+        raise OpError(lib().rtenhip_last_error_code(), lib().rtenhip_last_error_message().decode())
+    return r.decode()
+
+
+def load_model(src, ctx=None, optimize: bool = True):
+    """Model::load (src/model.rs:190-199): parse a .rten file, upload its
+    constants and return a device Graph with input_ids / output_ids set."""
+    from . import OpError, default_context, lib
+    from .graph import Graph
+
+    data = _bytes(src)
+    buf = C.create_string_buffer(data, len(data))
+    g = Graph.__new__(Graph)
+    g.ctx = ctx or default_context()
+    g.names = {}
+    ptr = lib().rtenhip_model_load_with_options(C.c_void_p(g.ctx.ptr), C.cast(buf, C.POINTER(C.c_uint8)),
+                                                C.c_size_t(len(data)), C.c_int(int(optimize)))
+    if not ptr:
+        g.ptr = None
+        raise OpError(lib().rtenhip_last_error_code(), lib().rtenhip_last_error_message().decode())
+    g.ptr = ptr
+    ids = (C.c_int32 * 64)()
+    n = lib().rtenhip_model_input_ids(C.c_void_p(ptr), ids, 64)
+    g.input_ids = [ids[i] for i in range(min(n, 64))]
+    n = lib().rtenhip_model_output_ids(C.c_void_p(ptr), ids, 64)
+    g.output_ids = [ids[i] for i in range(min(n, 64))]
+    return g

@@ -1,0 +1,239 @@
+""".rten V2 files: the writer (rten-convert's layout) and the C++ loader
+(Model::load, src/model.rs:265-522; Header::from_buf, src/header.rs:84-131).
+
+CPU tests parse files on the host only (rtenhip_model_describe: no device);
+GPU tests load a file into a device graph and check its outputs bit-exactly
+against the oracle running the ModelSpec the file was written from.
+
+Parity note: the reference ships no .rten files and cannot be built here (no
+Rust toolchain), so no reference-written file is available: the format is
+pinned by src/schema.fbs and src/header.rs (field slots, union ids and
+defaults transcribed from them), and the error texts by model.rs:677-689,
+header.rs:150-158 and op_registry.rs:211-220.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from rten_hip import OpError, models, rten_file
+from rten_hip.graph import ModelSpec
+
+
+def _model_bytes(spec, **kw):
+    return rten_file.to_rten_bytes(spec, **kw)
+
+
+def _tiny_spec():
+    m = ModelSpec("tiny")
+    x = m.value("x")
+    m.inputs = ["x"]
+    w = m.const("w", np.arange(2 * 3 * 3 * 3, dtype=np.float32).reshape(2, 3, 3, 3) / 10)
+    b = m.const("b", np.array([0.5, -0.5], np.float32))
+    y = m.op("Conv", [x, w, b], {"pads": [1, 1, 1, 1], "strides": [1, 1], "groups": 1}, name="conv")
+    y = m.op("Relu", [y], name="relu")
+    shape = m.const("shape", np.array([0, -1], np.float32))
+    y = m.op("Reshape", [y, shape], name="reshape")
+    m.outputs = [y]
+    return m
+
+
+def _parse(desc):
+    lines = desc.strip().splitlines()
+    nodes = {}
+    for ln in lines[2:]:
+        idx, kind, rest = ln.split(" ", 2)
+        nodes[int(idx)] = (kind, rest)
+    return lines[0], lines[1], nodes
+
+
+def test_header_layout():
+    b = _model_bytes(_tiny_spec())
+    magic, version, moff, mlen, toff = struct.unpack_from("<4sIQQQ", b, 0)
+    assert magic == b"RTEN" and version == 2
+    assert moff == 32 and moff + mlen <= len(b)
+    assert toff % 64 == 0 and toff >= moff + mlen
+
+
+def test_describe_round_trip_tiny():
+    desc = rten_file.describe_model(_model_bytes(_tiny_spec()))
+    ins, outs, nodes = _parse(desc)
+    assert ins == "inputs 0"
+    kinds = [nodes[i][0] for i in sorted(nodes)]
+    assert kinds == ["value", "const", "const", "value", "op", "value", "op", "const", "value", "op"]
+    conv = nodes[4][1]
+    assert conv.startswith("conv Conv in=0,1,2 out=3")
+    assert "pads=1,1,1,1" in conv and "strides=1,1" in conv and "groups=1" in conv
+    assert "dilations=1,1" in conv
+    assert "allowzero=0" in nodes[9][1]
+    # int32 shape constant (Reshape input) and an inline float constant
+    assert nodes[7][1].startswith("shape 2 sum=-1")
+    assert nodes[2][1].startswith("b 2 sum=0")
+
+
+@pytest.mark.parametrize("name", ["resnet50", "mobilenet_v2", "bert_encoder"])
+def test_describe_round_trip_models(name):
+    spec = getattr(models, name)() if name != "bert_encoder" else models.bert_encoder(layers=2, seq=32)
+    desc = rten_file.describe_model(_model_bytes(spec))
+    _, _, nodes = _parse(desc)
+    assert len(nodes) == len(spec.nodes)
+    for i, n in enumerate(spec.nodes):
+        kind, rest = nodes[i]
+        if n.kind == "op":
+            assert kind == "op"
+            assert rest.split(" ")[1] == n.op_type, (i, rest)
+        elif n.kind == "const":
+            assert kind == "const"
+            s = float(rest.rsplit("sum=", 1)[1])
+            exp = float(np.asarray(n.data, np.float64).sum())
+            assert abs(s - exp) <= 1e-6 * max(1.0, np.abs(np.asarray(n.data, np.float64)).sum())
+            shape = rest.split(" ")[1]
+            assert shape == "x".join(str(d) for d in np.asarray(n.data).shape)
+        else:
+            assert kind == "value"
+
+
+def test_inline_and_external_constants_agree():
+    spec = _tiny_spec()
+    a = rten_file.describe_model(_model_bytes(spec, inline_max=0))
+    b = rten_file.describe_model(_model_bytes(spec, inline_max=10 ** 9))
+    assert a == b
+
+
+def test_v2_header_errors():
+    good = bytearray(_model_bytes(_tiny_spec()))
+    bad = bytearray(good)
+    struct.pack_into("<I", bad, 4, 3)
+    with pytest.raises(OpError, match="invalid header: unsupported file version"):
+        rten_file.describe_model(bytes(bad))
+    with pytest.raises(OpError, match="invalid header: header is too short"):
+        rten_file.describe_model(bytes(good[:20]))
+    bad = bytearray(good)
+    struct.pack_into("<Q", bad, 8, len(good) + 1)
+    with pytest.raises(OpError, match="invalid header: segment offset is invalid"):
+        rten_file.describe_model(bytes(bad))
+    bad = bytearray(good)
+    struct.pack_into("<Q", bad, 16, len(good))
+    with pytest.raises(OpError, match="invalid header: segment length is invalid"):
+        rten_file.describe_model(bytes(bad))
+
+
+def test_v1_file_without_header():
+    """No "RTEN" magic: the whole buffer is the FlatBuffers model (V1)."""
+    b = _model_bytes(_tiny_spec(), inline_max=10 ** 9)
+    moff, mlen = struct.unpack_from("<QQ", b, 8)
+    v1 = b[moff:moff + mlen]
+    assert rten_file.describe_model(v1) == rten_file.describe_model(b)
+    # ... but an external constant needs the tensor data section
+    b = _model_bytes(_tiny_spec(), inline_max=0)
+    moff, mlen = struct.unpack_from("<QQ", b, 8)
+    v1 = b[moff:moff + mlen]
+    with pytest.raises(OpError, match="graph error: tensor data section missing"):
+        rten_file.describe_model(v1)
+
+
+def test_truncated_model_is_a_parse_error():
+    b = _model_bytes(_tiny_spec())
+    with pytest.raises(OpError, match="parse error"):
+        rten_file.describe_model(b[32:72])
+
+
+def test_unsupported_operator_error():
+    m = ModelSpec("cast")
+    x = m.value("x")
+    m.inputs = ["x"]
+    m.outputs = [m.op("Cast", [x], name="cast")]
+    with pytest.raises(OpError, match="operator error: operator Cast is not supported or not enabled"):
+        rten_file.describe_model(_model_bytes(m))
+
+
+def test_wrong_attrs_union_error(monkeypatch):
+    m = ModelSpec("conv")
+    x = m.value("x")
+    m.inputs = ["x"]
+    w = m.const("w", np.zeros((1, 1, 1, 1), np.float32))
+    m.outputs = [m.op("Conv", [x, w], name="conv")]
+    assert "Conv" in rten_file.describe_model(_model_bytes(m))
+    # A Conv whose attrs union holds GemmAttrs (op.attrs_as_conv_attrs() is None).
+    monkeypatch.setattr(rten_file, "_op_attrs", lambda t, a: (rten_file.ATTRS_GEMM, rten_file.Table([])))
+    with pytest.raises(OpError, match="operator error: invalid attributes for operator"):
+        rten_file.describe_model(_model_bytes(m))
+
+
+def test_schema_version_checked():
+    b = bytearray(_model_bytes(_tiny_spec()))
+    moff = 32
+    root = struct.unpack_from("<I", b, moff)[0] + moff
+    vt = root - struct.unpack_from("<i", b, root)[0]
+    field = struct.unpack_from("<H", b, vt + 4)[0]
+    struct.pack_into("<i", b, root + field, 2)
+    with pytest.raises(OpError, match="unsupported schema version"):
+        rten_file.describe_model(bytes(b))
+
+
+# --------------------------------------------------------------------------
+# Load into a device graph and run (GPU)
+# --------------------------------------------------------------------------
+
+def _bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rten_hip
+
+    rten_hip.default_context()
+    return torch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("optimize", [True, False])
+def test_load_resnet50_file_bitexact(gpu, tmp_path, optimize):
+    import graph_runner
+
+    spec = models.resnet50()
+    path = tmp_path / "resnet50.rten"
+    rten_file.write_rten(spec, str(path))
+    g = rten_file.load_model(str(path), optimize=optimize)
+    x = np.random.default_rng(5).random((2, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {"input": x})[spec.outputs[0]]
+    xd = gpu.from_numpy(x).cuda()
+    out = None
+    for _ in range(2):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        gpu.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
+@pytest.mark.gpu
+def test_load_bert_file_bitexact(gpu):
+    import graph_runner
+
+    spec = models.bert_encoder(layers=2, seq=64)
+    g = rten_file.load_model(rten_file.to_rten_bytes(spec))
+    rng = np.random.default_rng(6)
+    x = rng.random((4, 64, 768), dtype=np.float32) - np.float32(0.5)
+    mask = np.zeros((4, 1, 1, 64), np.float32)
+    mask[-1, :, :, 48:] = -10000.0
+    exp = graph_runner.run(spec, {"hidden_states": x, "attention_mask": mask})[spec.outputs[0]]
+    out = g.run({g.input_ids[0]: gpu.from_numpy(x).cuda(), g.input_ids[1]: gpu.from_numpy(mask).cuda()},
+                g.output_ids)
+    gpu.cuda.synchronize()
+    assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
+@pytest.mark.gpu
+def test_load_errors_on_device(gpu):
+    m = ModelSpec("cast")
+    x = m.value("x")
+    m.inputs = ["x"]
+    m.outputs = [m.op("Cast", [x], name="cast")]
+    with pytest.raises(OpError, match="operator error: operator Cast"):
+        rten_file.load_model(rten_file.to_rten_bytes(m))
