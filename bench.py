@@ -183,7 +183,7 @@ def main():
         report = g.timing_report()
         for line in report.splitlines()[1:]:
             name = line.split()[0]
-            if name.startswith("Conv") or name.startswith("MatMul") or name == "Gemm":
+            if name.startswith(("Conv", "MatMul", "FusedAttention")) or name == "Gemm":
                 conv_ms += float(line.split()[1])
     n_prof = max(1, min(args.steps, 10))
     g.set_timing(False)

@@ -144,6 +144,27 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s);
 rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s);
+
+// Fused attention (attention.hip): per (b, h), out = softmax(scale(Q K^T) +
+// mask) V with element strides for every operand (unit stride along the head
+// dimension of Q, V and out); scale_op 0 none, 1 divide, 2 multiply.
+struct AttnDesc {
+  int B, H, S, D;
+  const float* q;
+  int64_t q_b, q_h, q_s;
+  const float* k;  // K^T view [B, H, D, S]
+  int64_t k_b, k_h, k_d, k_s;
+  const float* v;
+  int64_t v_b, v_h, v_s;
+  const float* mask;  // broadcast view [B, H, S, S] or null
+  int64_t m_b, m_h, m_i, m_j;
+  float scale;
+  int scale_op;
+  float* out;
+  int64_t o_b, o_h, o_s;
+};
+bool attention_fast_ok(const AttnDesc& d);
+rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s);
 rtenhip_status launch_pad_nchw(const float* x, float* y, int64_t planes, int H, int W, int pt,
                                int pl, int pb, int pr, hipStream_t s);
 

@@ -21,9 +21,9 @@ struct Ctx {
   std::mutex mu;
   std::map<std::tuple<int, int, int, int, int, int, int>, int2*> ktabs;
   std::map<std::tuple<int, int, int, int, int, int, int>, int*> dtabs;
-  static constexpr int NSLOTS = 4;
-  void* slots[NSLOTS] = {nullptr, nullptr, nullptr, nullptr};
-  size_t slot_cap[NSLOTS] = {0, 0, 0, 0};
+  static constexpr int NSLOTS = 6;
+  void* slots[NSLOTS] = {};
+  size_t slot_cap[NSLOTS] = {};
   bool use_dma = true;
   // Packed-weight cache keyed by (weights pointer, M, K, bm, bk, il).  Only valid
   // when the caller guarantees weights are immutable (graph constants); the
@@ -34,7 +34,8 @@ struct Ctx {
   explicit Ctx(int dev);
   ~Ctx();
   // Grow-only device scratch (independent slots: 0 contiguous copies,
-  // 1 softmax / padded inputs, 2 packed weights, 3 spare).  Synchronizes the
+  // 1 softmax / padded inputs, 2 packed weights, 3 split workspaces, 4 and 5
+  // the unfused attention sequence's scores and output).  Synchronizes the
   // stream when it has to grow, so callers must not be capturing.
   float* scratch_floats(size_t n, size_t slot);
   // Grow-only zeroed int buffer for DMA split arrival counters (the kernel

@@ -60,11 +60,6 @@ bool parse_attrs(const char* s, Attrs& out) {
   return true;
 }
 
-static int64_t prod(const Shape& s, size_t from = 0, size_t to = SIZE_MAX) {
-  int64_t n = 1;
-  for (size_t i = from; i < std::min(to, s.size()); i++) n *= s[i];
-  return n;
-}
 
 static rtenhip_tensor desc(float* p, const Shape& s) {
   return make_tensor(p, s.data(), (int)s.size());
@@ -168,6 +163,45 @@ static bool const_values(const Graph& g, int id, std::vector<float>& out) {
   return true;
 }
 
+// Output shape of matmul_impl (matmul.rs:123-160): broadcast prefix + [M, N].
+static rtenhip_status matmul_shape(const Shape& a, const Shape& b, Shape& out) {
+  if (a.size() < 2 || b.size() < 2) return fail(RTENHIP_INVALID_VALUE, "Inputs must have >= 2 dimensions");
+  if (a[a.size() - 1] != b[b.size() - 2])
+    return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES,
+                "Columns of first matrix does not match rows of second matrix");
+  int64_t pre[RTENHIP_MAX_DIMS];
+  int pn;
+  if (!broadcast_shapes(a.data(), (int)a.size() - 2, b.data(), (int)b.size() - 2, pre, &pn))
+    return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast shapes");
+  out.assign(pre, pre + pn);
+  out.push_back(a[a.size() - 2]);
+  out.push_back(b[b.size() - 1]);
+  return RTENHIP_OK;
+}
+
+// Shapes through a FusedAttention node: q @ kT (+ mask, broadcast) @ v, then
+// the trailing Transpose.  `scores` receives the softmax input shape.
+static rtenhip_status attention_shapes(const Shape& q, const Shape& kt, const Shape& v,
+                                       const Shape* mask, const std::vector<int64_t>& out_perm,
+                                       Shape& scores, Shape& out) {
+  rtenhip_status st = matmul_shape(q, kt, scores);
+  if (st) return st;
+  if (mask) {
+    int64_t bs[RTENHIP_MAX_DIMS];
+    int bn;
+    if (!broadcast_shapes(scores.data(), (int)scores.size(), mask->data(), (int)mask->size(), bs, &bn))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast inputs");
+    scores.assign(bs, bs + bn);
+  }
+  st = matmul_shape(scores, v, out);
+  if (st) return st;
+  if (!out_perm.empty()) {
+    if (!valid_perm(out_perm, out.size())) return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
+    out = permute_shape(out, out_perm);
+  }
+  return RTENHIP_OK;
+}
+
 rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& ins,
                                    std::vector<Shape>& outs) {
   const Node& op = nodes[op_id];
@@ -229,6 +263,11 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
     outs[0].assign(pre, pre + pn);
     outs[0].push_back(x[x.size() - 2]);
     outs[0].push_back(b[b.size() - 1]);
+  } else if (t == "FusedAttention") {
+    if ((st = need(1)) || (st = need(2))) return st;
+    Shape scores;
+    st = attention_shapes(x, *in(1), *in(2), in(3), op.attrs.ints("out_perm", {}), scores, outs[0]);
+    if (st) return st;
   } else if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div") {
     if ((st = need(1))) return st;
     const Shape& b = *in(1);
@@ -771,6 +810,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     if (p1 != n.input_perm.end()) b = permute_desc(b, p1->second);
     return exec_matmul(p, op_id, a, b, y);
   }
+  if (t == "FusedAttention") return exec_attention(p, op_id, y);
   if (t == "BatchNormalization") {
     return rtenhip_batch_norm_f32(c, &x, P(1), P(2), P(3), P(4), (float)n.attrs.num("epsilon", 1e-5), &y);
   }
@@ -797,6 +837,121 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   std::string msg = "Unsupported operator type: " + t;
   set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
   return RTENHIP_UNSUPPORTED_VALUE;
+}
+
+// FusedAttention (see Graph::optimize): attention.hip when the shapes fit
+// (rank 4, head dim 64, S <= 128 even, unit stride along the head dim), else
+// the original operator sequence on scratch buffers.
+rtenhip_status Graph::exec_attention(Plan& p, int op_id, rtenhip_tensor y) {
+  const Node& n = nodes[op_id];
+  auto view = [&](size_t idx) -> rtenhip_tensor {
+    const int v = n.inputs[idx];
+    const Shape* s = plan_shape(*this, p, v);
+    rtenhip_tensor t = desc(ptr_of(p, v), s ? *s : Shape());
+    auto it = n.input_perm.find((int)idx);
+    if (it != n.input_perm.end()) t = permute_desc(t, it->second);
+    return t;
+  };
+  const rtenhip_tensor q = view(0), kt = view(1), v = view(2);
+  const bool has_mask = n.inputs.size() > 3 && n.inputs[3] >= 0;
+  const rtenhip_tensor mask = has_mask ? view(3) : rtenhip_tensor{};
+  const int scale_op = (int)n.attrs.num("scale_op", 0);
+  const Node* scale_node = scale_op ? &nodes[n.inputs[4]] : nullptr;
+  const std::vector<int64_t> out_perm = n.attrs.ints("out_perm", {});
+  // The output before the trailing Transpose, as a view of y.
+  rtenhip_tensor o = y;
+  if (!out_perm.empty())
+    for (int i = 0; i < y.ndim; i++) {
+      o.shape[out_perm[i]] = y.shape[i];
+      o.strides[out_perm[i]] = y.strides[i];
+    }
+
+  bool fast = q.ndim == 4 && kt.ndim == 4 && v.ndim == 4 && o.ndim == 4;
+  AttnDesc d{};
+  if (fast) {
+    d.B = (int)q.shape[0];
+    d.H = (int)q.shape[1];
+    d.S = (int)q.shape[2];
+    d.D = (int)q.shape[3];
+    const int64_t want_k[4] = {d.B, d.H, d.D, d.S}, want_v[4] = {d.B, d.H, d.S, d.D};
+    for (int i = 0; i < 4; i++)
+      fast = fast && kt.shape[i] == want_k[i] && v.shape[i] == want_v[i] && o.shape[i] == want_v[i];
+    fast = fast && q.strides[3] == 1 && v.strides[3] == 1 && o.strides[3] == 1;
+    int64_t ms[4] = {0, 0, 0, 0};
+    if (fast && has_mask) {
+      const int64_t target[4] = {d.B, d.H, d.S, d.S};
+      fast = mask.ndim <= 4;
+      for (int i = 0; fast && i < 4; i++) {
+        const int mi = i - (4 - mask.ndim);
+        if (mi < 0 || mask.shape[mi] == 1) continue;
+        if (mask.shape[mi] != target[i]) fast = false;
+        ms[i] = mask.strides[mi];
+      }
+    }
+    if (fast) {
+      d.q = q.data;
+      d.q_b = q.strides[0];
+      d.q_h = q.strides[1];
+      d.q_s = q.strides[2];
+      d.k = kt.data;
+      d.k_b = kt.strides[0];
+      d.k_h = kt.strides[1];
+      d.k_d = kt.strides[2];
+      d.k_s = kt.strides[3];
+      d.v = v.data;
+      d.v_b = v.strides[0];
+      d.v_h = v.strides[1];
+      d.v_s = v.strides[2];
+      d.mask = has_mask ? mask.data : nullptr;
+      d.m_b = ms[0];
+      d.m_h = ms[1];
+      d.m_i = ms[2];
+      d.m_j = ms[3];
+      d.scale_op = scale_op;
+      d.scale = scale_node ? scale_node->host_small[0] : 1.f;
+      d.out = o.data;
+      d.o_b = o.strides[0];
+      d.o_h = o.strides[1];
+      d.o_s = o.strides[2];
+      fast = attention_fast_ok(d);
+    }
+  }
+  if (fast) return launch_attention(d, ctx->stream);
+
+  // Unfused: s = q @ kT; s = s (/|*) c; s = s + mask; softmax; out = s @ v.
+  rtenhip_ctx* c = cptr;
+  auto shape_of_t = [](const rtenhip_tensor& t) { return Shape(t.shape, t.shape + t.ndim); };
+  Shape s0, ss, os;
+  rtenhip_status st = matmul_shape(shape_of_t(q), shape_of_t(kt), s0);
+  if (!st) {
+    const Shape ms = shape_of_t(mask);
+    st = attention_shapes(shape_of_t(q), shape_of_t(kt), shape_of_t(v), has_mask ? &ms : nullptr, {},
+                          ss, os);
+  }
+  if (st) return st;
+  if (prod(ss) != prod(s0))
+    return fail(RTENHIP_UNSUPPORTED_VALUE, "attention mask must not broadcast the scores");
+  float* sbuf = ctx->scratch_floats((size_t)std::max<int64_t>(1, prod(ss)), 4);
+  if (!sbuf) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+  rtenhip_tensor s = desc(sbuf, s0);
+  if ((st = rtenhip_matmul_f32(c, &q, &kt, &s))) return st;
+  if (scale_op) {
+    rtenhip_tensor ct = desc(scale_node->dev, scale_node->shape);
+    st = rtenhip_binary_f32(c, scale_op == 1 ? RTENHIP_BINARY_DIV : RTENHIP_BINARY_MUL, &s, &ct, &s);
+    if (st) return st;
+  }
+  s = desc(sbuf, ss);
+  if (has_mask) {
+    rtenhip_tensor s_in = desc(sbuf, s0);
+    if ((st = rtenhip_binary_f32(c, RTENHIP_BINARY_ADD, &s_in, &mask, &s))) return st;
+  }
+  if ((st = rtenhip_softmax_f32(c, &s, (int64_t)n.attrs.num("axis", -1), &s))) return st;
+  if (out_perm.empty()) return rtenhip_matmul_f32(c, &s, &v, &y);
+  float* obuf = ctx->scratch_floats((size_t)std::max<int64_t>(1, prod(os)), 5);
+  if (!obuf) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+  rtenhip_tensor ot = desc(obuf, os);
+  if ((st = rtenhip_matmul_f32(c, &s, &v, &ot))) return st;
+  return launch_copy_strided(permute_desc(ot, out_perm), y.data, ctx->stream);
 }
 
 // MatMul (matmul_impl, src/ops/matmul.rs:123-239) with the load-time fused
@@ -1481,6 +1636,77 @@ rtenhip_status Graph::optimize() {
       if (tr.op_type != "Transpose" || tr.inputs.empty() || tr.inputs[0] < 0) continue;
       mm.input_perm[k] = tr.attrs.ints("perm", {});
       mm.inputs[k] = tr.inputs[0];
+      fused++;
+    }
+  }
+  // Attention: MatMul(q, kT) -> [Div|Mul(scalar constant)] -> [Add(mask)] ->
+  // Softmax(axis -1) -> MatMul(., v) [-> Transpose] collapses into one
+  // FusedAttention node (inputs q, kT, v, mask, scale; the permuted views of
+  // FusedTranspose carried over; the trailing Transpose as "out_perm").  The
+  // node runs attention.hip when the shapes fit it and the same operator
+  // sequence otherwise, so results do not depend on the choice.
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& m1 = nodes[i];
+    if (m1.kind != NodeKind::Operator || m1.removed || m1.op_type != "MatMul" || m1.outputs.size() != 1 ||
+        m1.inputs.size() != 2 || m1.fused_colbias >= 0 || m1.fused_residual >= 0 || m1.fused_act)
+      continue;
+    std::vector<int> chain;
+    int v = m1.outputs[0];
+    int nxt = sole(v);
+    auto live = [&](int op) { return op >= 0 && !nodes[op].removed && nodes[op].outputs.size() == 1; };
+    int scale_op = 0, scale_v = -1, mask_v = -1;
+    if (live(nxt) && (nodes[nxt].op_type == "Div" || nodes[nxt].op_type == "Mul") &&
+        nodes[nxt].inputs.size() == 2) {
+      const Node& sn = nodes[nxt];
+      const bool mul = sn.op_type == "Mul";
+      const int c = sn.inputs[0] == v ? sn.inputs[1] : (mul ? sn.inputs[0] : -1);
+      if (c >= 0 && c != v && nodes[c].kind == NodeKind::Constant && prod(nodes[c].shape) == 1 &&
+          !nodes[c].host_small.empty()) {
+        scale_op = mul ? 2 : 1;
+        scale_v = c;
+        chain.push_back(nxt);
+        v = sn.outputs[0];
+        nxt = sole(v);
+      }
+    }
+    if (live(nxt) && nodes[nxt].op_type == "Add" && nodes[nxt].inputs.size() == 2) {
+      const Node& an = nodes[nxt];
+      const int o = an.inputs[0] == v ? an.inputs[1] : an.inputs[0];
+      if (o >= 0 && o != v) {
+        mask_v = o;
+        chain.push_back(nxt);
+        v = an.outputs[0];
+        nxt = sole(v);
+      }
+    }
+    if (!live(nxt) || nodes[nxt].op_type != "Softmax") continue;
+    const int64_t axis = (int64_t)nodes[nxt].attrs.num("axis", -1);
+    if (axis != -1 && axis != 3) continue;
+    chain.push_back(nxt);
+    v = nodes[nxt].outputs[0];
+    nxt = sole(v);
+    if (!live(nxt)) continue;
+    Node& m2 = nodes[nxt];
+    if (m2.op_type != "MatMul" || m2.inputs.size() != 2 || m2.inputs[0] != v || m2.inputs[1] == v ||
+        m2.input_perm.count(0) || m2.fused_colbias >= 0 || m2.fused_residual >= 0 || m2.fused_act)
+      continue;
+    std::map<int, std::vector<int64_t>> perms;
+    for (auto& kv : m1.input_perm) perms[kv.first] = kv.second;
+    if (m2.input_perm.count(1)) perms[2] = m2.input_perm[1];
+    m2.inputs = {m1.inputs[0], m1.inputs[1], m2.inputs[1], mask_v, scale_v};
+    m2.input_perm = perms;
+    m2.op_type = "FusedAttention";
+    m2.attrs.nums["scale_op"] = {(double)scale_op};
+    if (axis == 3) m2.attrs.nums["rank4"] = {1};
+    m1.removed = true;
+    for (int op : chain) nodes[op].removed = true;
+    fused += 2 + (int)chain.size();
+    const int tr = sole(m2.outputs[0]);
+    if (live(tr) && nodes[tr].op_type == "Transpose" && nodes[tr].inputs.size() == 1 &&
+        nodes[tr].attrs.nums.count("perm")) {
+      m2.attrs.nums["out_perm"] = nodes[tr].attrs.nums["perm"];
+      nodes[tr].removed = true;
+      m2.outputs[0] = nodes[tr].outputs[0];
       fused++;
     }
   }

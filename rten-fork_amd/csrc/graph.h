@@ -18,6 +18,13 @@ namespace rtenhip {
 
 using Shape = std::vector<int64_t>;
 
+inline int64_t prod(const Shape& s, size_t from = 0, size_t to = SIZE_MAX) {
+  int64_t n = 1;
+  for (size_t i = from; i < std::min(to, s.size()); i++) n *= s[i];
+  return n;
+}
+
+
 struct Attrs {
   std::map<std::string, std::vector<double>> nums;
   std::map<std::string, std::string> strs;
@@ -169,6 +176,7 @@ struct Graph {
   rtenhip_status exec_op(Plan& p, int op_id);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
+  rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   rtenhip_status exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& a,
                                  const rtenhip_tensor& b, const rtenhip_tensor& y, MatMulExec& me);
   float* ptr_of(Plan& p, int value_id);

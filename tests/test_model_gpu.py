@@ -132,3 +132,61 @@ def test_bert_base_seq128_bitexact(rh):
     assert np.isfinite(exp).all()
     for o in outs:
         assert _bits_equal(o, exp), np.abs(o - exp).max()
+
+
+def _attention_spec(S, D, H=3, scale_op="Div", mask_shape="b11s", out_transpose=True):
+    """q, k, v [B, H, S, D] -> MatMul(q, Transpose(k)) -> Div|Mul -> [Add(mask)]
+    -> Softmax -> MatMul(., v) -> [Transpose]: the pattern Graph::optimize
+    collapses into FusedAttention."""
+    from rten_hip.graph import ModelSpec
+
+    m = ModelSpec(f"attn_s{S}_d{D}")
+    q, k, v = m.value("q"), m.value("k"), m.value("v")
+    m.inputs = ["q", "k", "v"]
+    kt = m.op("Transpose", [k], {"perm": [0, 1, 3, 2]}, name="kt")
+    s = m.op("MatMul", [q, kt], name="qk")
+    c = m.const("scale", np.array([np.sqrt(D)] if scale_op == "Div" else [1.0 / np.sqrt(D)], np.float32))
+    s = m.op(scale_op, [s, c], name="scale")
+    if mask_shape:
+        m.value("mask")
+        m.inputs.append("mask")
+        s = m.op("Add", [s, "mask"], name="mask_add")
+    s = m.op("Softmax", [s], {"axis": -1}, name="softmax")
+    o = m.op("MatMul", [s, v], name="av")
+    if out_transpose:
+        o = m.op("Transpose", [o], {"perm": [0, 2, 1, 3]}, name="out_t")
+    m.outputs = [o]
+    return m
+
+
+@pytest.mark.parametrize("S,D,scale_op,mask_shape,out_t", [
+    (40, 64, "Div", "b11s", True),     # attention.hip
+    (128, 64, "Mul", "b1ss", False),   # attention.hip, full mask, no transpose
+    (64, 16, "Div", "b11s", True),     # head dim 16: unfused sequence
+    (130, 64, "Mul", None, True),      # S > 128: unfused sequence
+    (33, 64, "Div", "b11s", False),    # odd S: unfused sequence
+])
+def test_fused_attention_bitexact(rh, S, D, scale_op, mask_shape, out_t):
+    import torch
+    import graph_runner
+
+    B, H = 2, 3
+    spec = _attention_spec(S, D, H, scale_op, mask_shape, out_t)
+    rng = np.random.default_rng(S * 100 + D)
+    ins = {n: (rng.random((B, H, S, D), dtype=np.float32) - np.float32(0.5)) * 2 for n in ("q", "k", "v")}
+    if mask_shape:
+        shape = (B, 1, 1, S) if mask_shape == "b11s" else (B, 1, S, S)
+        mask = np.zeros(shape, np.float32)
+        mask[-1, ..., S - S // 4:] = -10000.0
+        ins["mask"] = mask
+    exp = graph_runner.run(spec, ins)[spec.outputs[0]]
+    g = spec.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[name]).cuda() for i, name in enumerate(spec.inputs)}
+    out = None
+    for _ in range(2):  # eager, then hipGraph replay
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        got = out[0].cpu().numpy()
+        if not _bits_equal(got, exp):
+            d = np.abs(got.astype(np.float64) - exp)
+            pytest.fail(f"attention differs: max abs {d.max():.3g}, {(d > 0).sum()} elems")
