@@ -785,29 +785,58 @@ namespace rtenhip {
 // Pack A[M, K] (row stride lda, unit column stride) into
 // [tiles_m][tiles_k][BK][BM] tiles, zero padded, rows of each 32*il slab
 // interleaved: position l*il + mi holds row mi*32 + l.  One workgroup per
-// tile: rows are read as contiguous BK-float segments, transposed through
-// LDS, and the tile is written as one contiguous run.
+// (m tile, kcw-wide k chunk; kcw = 64, or 32 for 256-row tiles so the LDS
+// stays under 64 KB): the BM rows are read as kcw*4-byte segments (float4 per
+// lane when aligned), transposed through LDS, and the chunk's kcw/BK tiles --
+// contiguous in the packed layout -- written with float4 stores.
+
 __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a, int64_t lda,
                                                      int M, int K, int BM, int BK, int il,
-                                                     int tiles_k, float* __restrict__ out) {
-  extern __shared__ float sh[];  // [BK][BM + 1]
-  const int tile = blockIdx.x;
-  const int mt = tile / tiles_k, kt = tile - mt * tiles_k;
-  const int n = BM * BK;
+                                                     int tiles_k, int kcw, int vec,
+                                                     float* __restrict__ out) {
+  extern __shared__ float sh[];  // [kcw][BM + 1]
   const int ld = BM + 1;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int r = i / BK, kk = i - r * BK;
-    const int m = mt * BM + r, k = kt * BK + kk;
-    sh[kk * ld + r] = (m < M && k < K) ? a[(int64_t)m * lda + k] : 0.f;
+  const int mt = blockIdx.x, kc = blockIdx.y;
+  const int k0 = kc * kcw;
+  const int64_t m0 = (int64_t)mt * BM;
+  const int q4 = kcw / 4;  // float4s per row segment (8 or 16)
+  for (int idx = threadIdx.x; idx < BM * q4; idx += blockDim.x) {
+    const int r = idx / q4, c = (idx - r * q4) * 4;
+    const int64_t m = m0 + r;
+    const int k = k0 + c;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (m < M) {
+      const float* src = a + m * lda + k;
+      if (vec && k + 3 < K) {
+        v = *(const float4*)src;
+      } else {
+        if (k < K) v.x = src[0];
+        if (k + 1 < K) v.y = src[1];
+        if (k + 2 < K) v.z = src[2];
+        if (k + 3 < K) v.w = src[3];
+      }
+    }
+    sh[(c + 0) * ld + r] = v.x;
+    sh[(c + 1) * ld + r] = v.y;
+    sh[(c + 2) * ld + r] = v.z;
+    sh[(c + 3) * ld + r] = v.w;
   }
   __syncthreads();
-  float* o = out + (int64_t)tile * n;
+  const int kt0 = k0 / BK;
+  const int nkt = min(kcw / BK, tiles_k - kt0);
+  float* o = out + ((int64_t)mt * tiles_k + kt0) * (int64_t)(BK * BM);
   const int slab = 32 * il;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int kk = i / BM, pos = i - kk * BM;
-    const int q = pos % slab;
-    const int mm = (pos - q) + (q % il) * 32 + q / il;
-    o[i] = sh[kk * ld + mm];
+  const int n = nkt * BK * BM;  // floats; BM % 4 == 0
+  for (int i = threadIdx.x * 4; i < n; i += blockDim.x * 4) {
+    const int kk = i / BM, pos = i - kk * BM;  // kk counts across the chunk's tiles
+    float vals[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int q = (pos + e) % slab;
+      const int mm = (pos + e - q) + (q % il) * 32 + q / il;
+      vals[e] = sh[kk * ld + mm];
+    }
+    *(float4*)(o + i) = make_float4(vals[0], vals[1], vals[2], vals[3]);
   }
 }
 
@@ -820,12 +849,17 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
                              float* out, hipStream_t s) {
   const int tiles_k = (K + t.bk - 1) / t.bk;
   const int tiles_m = (M + t.bm - 1) / t.bm;
-  const int64_t tiles = (int64_t)tiles_m * tiles_k;
-  if (tiles == 0) return RTENHIP_OK;
-  if (tiles > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "A too large to pack");
-  const size_t lds = (size_t)t.bk * (t.bm + 1) * sizeof(float);
-  hipLaunchKernelGGL(pack_a_kernel, dim3((unsigned)tiles), dim3(256), lds, s, a, lda, M, K, t.bm,
-                     t.bk, t.il, tiles_k, out);
+  if ((int64_t)tiles_m * tiles_k == 0) return RTENHIP_OK;
+  const int kcw = t.bm >= 256 ? 32 : 64;
+  if (kcw % t.bk != 0 || t.bm % 4 != 0 || tiles_m > 0x7fffffff)
+    return fail(RTENHIP_UNSUPPORTED_VALUE, "unsupported A pack shape");
+  // packed output chunks are 16-byte aligned (BK * BM % 4 == 0); float4 reads
+  // need 16-byte aligned rows
+  const int vec = ((uintptr_t)a % 16 == 0 && lda % 4 == 0) ? 1 : 0;
+  const size_t lds = (size_t)kcw * (t.bm + 1) * sizeof(float);
+  dim3 grid((unsigned)tiles_m, (unsigned)((K + kcw - 1) / kcw));
+  hipLaunchKernelGGL(pack_a_kernel, grid, dim3(256), lds, s, a, lda, M, K, t.bm, t.bk, t.il,
+                     tiles_k, kcw, vec, out);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

@@ -1082,7 +1082,17 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     bool chosen_split = false;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
-    if (autotune && cs == hipStreamCaptureStatusNone && da.residual != da.out) {
+    // A MatMul with the same A value and shape already tuned (the Q/K/V
+    // projections): reuse its choice so the packed A can be shared.
+    const MatMulExec* twin = nullptr;
+    for (auto& kv : p.matmuls)
+      if (kv.first != op_id && kv.second.cfg >= 0 && nodes[kv.first].inputs[0] == n.inputs[0] &&
+          kv.second.M == me.M && kv.second.N == me.N && kv.second.K == me.K)
+        twin = &kv.second;
+    if (twin) {
+      chosen = twin->cfg;
+      chosen_split = twin->split;
+    } else if (autotune && cs == hipStreamCaptureStatusNone && da.residual != da.out) {
       static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
@@ -1128,8 +1138,13 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     st = set_split(me, chosen, chosen_split);
     if (st) return st;
     me.cfg = chosen;
+    p.mm_pack_value = -1;  // tuning overwrote the buffer
   }
   bind(me, me.cfg);
+  const DmaTile tile = dma_cfg_tile(me.cfg);
+  da.pack = !(p.mm_pack_value == n.inputs[0] && p.mm_pack_tile == tile);
+  p.mm_pack_value = n.inputs[0];
+  p.mm_pack_tile = tile;
   return gemm_dense_dma(ctx, da);
 }
 
@@ -1420,6 +1435,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     return RTENHIP_OK;
   };
   const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
+  plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
   if (replay) {
     if (!same_binding) {
       if (plan->exec) {

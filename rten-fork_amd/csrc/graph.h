@@ -13,6 +13,7 @@
 
 #include "common.h"
 #include "ctx.h"
+#include "gemm_dma.h"
 
 namespace rtenhip {
 
@@ -124,6 +125,11 @@ struct Plan {
   std::map<int, MatMulExec> matmuls;  // op id -> dense DMA MatMul state
   float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
   int64_t mm_pack_floats = 0;
+  // What mm_pack holds during a run: the A value it was packed from (value
+  // ids are single-assignment, so MatMuls reading the same A -- Q/K/V
+  // projections -- pack it once) and the tile shape; -1 = nothing.
+  int mm_pack_value = -1;
+  DmaTile mm_pack_tile{0, 0, 0};
   // Ops launched on the side stream (independent branches such as the
   // ResNet downsample conv), and for each op the side ops it must wait for.
   std::set<int> side;
