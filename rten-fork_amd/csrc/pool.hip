@@ -44,11 +44,103 @@ __global__ void pool_kernel(const float* __restrict__ x, float* __restrict__ y, 
   }
 }
 
+// One workgroup per (n, c) plane staged in LDS with 16-byte loads; each
+// output then reads its window from LDS.  Same per-window (ky, kx) order and
+// arithmetic as pool_kernel: taps in the padding are skipped (for max a
+// skipped tap and a -inf tap are the same, for avg the add is predicated so a
+// -0.0 sum is kept).  KH/KW > 0: compile-time window, fully unrolled.
+template <bool IS_MAX, int KH, int KW>
+__global__ __launch_bounds__(256) void pool_plane_kernel(const float* __restrict__ x,
+                                                         float* __restrict__ y, int H, int W,
+                                                         int OH, int OW, FastDiv fd_ow, int kh_,
+                                                         int kw_, int sh, int sw, int pt, int pl,
+                                                         int count_include_pad, int rb) {
+  extern __shared__ float plane[];
+  const int kh = KH > 0 ? KH : kh_, kw = KW > 0 ? KW : kw_;
+  const int64_t pidx = blockIdx.x;
+  // Output rows [oy0, oy1) of this block and the input rows [r_lo, r_hi) they read.
+  const int oy0 = blockIdx.y * rb, oy1 = min(OH, oy0 + rb);
+  const int r_lo = max(0, oy0 * sh - pt), r_hi = min(H, (oy1 - 1) * sh - pt + kh);
+  const float* xp = x + pidx * H * W + (int64_t)r_lo * W;
+  const int n = max(0, r_hi - r_lo) * W;
+  if ((W & 3) == 0) {
+    for (int i = threadIdx.x * 4; i < n; i += 1024)
+      *(float4*)(plane + i) = *(const float4*)(xp + i);
+  } else {
+    for (int i = threadIdx.x; i < n; i += 256) plane[i] = xp[i];
+  }
+  __syncthreads();
+  float* yp = y + pidx * OH * OW;
+  for (int o = oy0 * OW + threadIdx.x; o < oy1 * OW; o += 256) {
+    const int oy = fdiv(o, fd_ow), ox = o - oy * OW;
+    const int iy0 = oy * sh - pt, ix0 = ox * sw - pl;
+    float acc = IS_MAX ? -__builtin_huge_valf() : 0.f;
+    int cnt = 0;
+#pragma unroll
+    for (int ky = 0; ky < (KH > 0 ? KH : 1); ky++) {
+      for (int kyr = (KH > 0 ? ky : 0); kyr < (KH > 0 ? ky + 1 : kh); kyr++) {
+        const int iy = iy0 + kyr;
+        const bool row_ok = iy >= 0 && iy < H;
+#pragma unroll
+        for (int kx = 0; kx < (KW > 0 ? KW : 1); kx++) {
+          for (int kxr = (KW > 0 ? kx : 0); kxr < (KW > 0 ? kx + 1 : kw); kxr++) {
+            const int ix = ix0 + kxr;
+            const bool ok = row_ok && ix >= 0 && ix < W;
+            const float v = plane[ok ? (iy - r_lo) * W + ix : 0];
+            if (IS_MAX) {
+              acc = ok ? rust_max(acc, v) : acc;
+            } else {
+              acc = ok ? __fadd_rn(acc, v) : acc;
+              cnt += ok;
+            }
+          }
+        }
+      }
+    }
+    if (!IS_MAX) acc = __fdiv_rn(acc, count_include_pad ? (float)(kh * kw) : (float)cnt);
+    yp[o] = acc;
+  }
+}
+
+template <bool IS_MAX>
+static void launch_pool_plane(const float* x, float* y, int64_t NC, int H, int W, int OH, int OW,
+                              int kh, int kw, int sh, int sw, int pt, int pl, int cip,
+                              hipStream_t s) {
+  // Row bands of rb output rows whose input rows fit ~16 KB of LDS (more
+  // resident blocks per CU, so staging overlaps other blocks' compute).
+  const int rows_in = std::max(kh, 4096 / W);
+  const int rb = std::max(1, std::min(OH, (rows_in - kh) / sh + 1));
+  const int bands = (OH + rb - 1) / rb;
+  const int max_rows = std::min(H, (rb - 1) * sh + kh);
+  const size_t bytes = (size_t)max_rows * W * sizeof(float);
+  const FastDiv fd = make_fastdiv((uint32_t)OW);
+  const dim3 grid((unsigned)NC, (unsigned)bands);
+  if (kh == 3 && kw == 3)
+    hipLaunchKernelGGL((pool_plane_kernel<IS_MAX, 3, 3>), grid, dim3(256), bytes, s, x, y, H, W,
+                       OH, OW, fd, kh, kw, sh, sw, pt, pl, cip, rb);
+  else if (kh == 2 && kw == 2)
+    hipLaunchKernelGGL((pool_plane_kernel<IS_MAX, 2, 2>), grid, dim3(256), bytes, s, x, y, H, W,
+                       OH, OW, fd, kh, kw, sh, sw, pt, pl, cip, rb);
+  else
+    hipLaunchKernelGGL((pool_plane_kernel<IS_MAX, 0, 0>), grid, dim3(256), bytes, s, x, y, H, W,
+                       OH, OW, fd, kh, kw, sh, sw, pt, pl, cip, rb);
+}
+
 rtenhip_status launch_pool(int is_max, const float* x, float* y, int64_t NC, int H, int W,
                            int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
                            int count_include_pad, hipStream_t s) {
   const int64_t total = NC * OH * OW;
   if (total == 0) return RTENHIP_OK;
+  const size_t plane_bytes = (size_t)H * W * sizeof(float);
+  if (plane_bytes <= 64 * 1024 && OH * OW >= 256 && NC < (int64_t(1) << 31) && sh >= 1 &&
+      kh >= 1 && ((uintptr_t)x % 16) == 0) {
+    if (is_max)
+      launch_pool_plane<true>(x, y, NC, H, W, OH, OW, kh, kw, sh, sw, pt, pl, count_include_pad, s);
+    else
+      launch_pool_plane<false>(x, y, NC, H, W, OH, OW, kh, kw, sh, sw, pt, pl, count_include_pad, s);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   int64_t blocks32 = (total + 255) / 256;
   if (blocks32 > 8192) blocks32 = 8192;
   if (total + blocks32 * 256 < (int64_t(1) << 31) && NC * H * W < (int64_t(1) << 31)) {
@@ -87,8 +179,36 @@ __global__ void gap_kernel(const float* __restrict__ x, float* __restrict__ y, i
   y[i] = __fdiv_rn(s, (float)HW);
 }
 
+// Same sequential chain per plane, with the block's planes (contiguous in
+// memory) first staged through LDS by coalesced loads.
+__global__ __launch_bounds__(256) void gap_lds_kernel(const float* __restrict__ x,
+                                                      float* __restrict__ y, int64_t NC, int HW,
+                                                      int ppb) {
+  extern __shared__ float buf[];
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int np = (int)min((int64_t)ppb, NC - p0);
+  const float* src = x + p0 * HW;
+  const int n = np * HW;
+  for (int i = threadIdx.x; i < n; i += 256) buf[i] = src[i];
+  __syncthreads();
+  if ((int)threadIdx.x < np) {
+    const float* p = buf + threadIdx.x * HW;
+    float acc = 0.f;
+    for (int k = 0; k < HW; k++) acc = __fadd_rn(acc, p[k]);
+    y[p0 + threadIdx.x] = __fdiv_rn(acc, (float)HW);
+  }
+}
+
 rtenhip_status launch_gap(const float* x, float* y, int64_t NC, int64_t HW, hipStream_t s) {
   if (NC == 0) return RTENHIP_OK;
+  const int64_t ppb = std::min<int64_t>(256, HW > 0 ? 12288 / HW : 0);
+  if (HW > 0 && ppb >= 32 && NC / ppb < (int64_t(1) << 31)) {
+    const int64_t blocks = (NC + ppb - 1) / ppb;
+    hipLaunchKernelGGL(gap_lds_kernel, dim3((unsigned)blocks), dim3(256),
+                       (size_t)(ppb * HW * sizeof(float)), s, x, y, NC, (int)HW, (int)ppb);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   hipLaunchKernelGGL(gap_kernel, dim3((unsigned)((NC + 255) / 256)), dim3(256), 0, s, x, y, NC,
                      HW);
   RTENHIP_LAUNCH_CHECK();

@@ -224,6 +224,18 @@ def test_pooling_bitexact(rh, oracle):
     assert_bits(host(rh.global_average_pool(dev(g))), oracle.global_average_pool(g), "gap")
 
 
+@pytest.mark.parametrize("hw", [112, 50])
+def test_pooling_plane_kernel_bitexact(rh, oracle, hw):
+    """Planes that fit LDS take the plane-staged kernel (ResNet stem maxpool);
+    W % 4 != 0 stages with scalar loads."""
+    x = rnd(oracle, 53, 2, 3, hw, hw)
+    assert_bits(host(rh.max_pool(dev(x), (3, 3), (2, 2), (1, 1, 1, 1))),
+                oracle.max_pool(x, (3, 3), (2, 2), (1, 1, 1, 1)), "maxpool")
+    for incl in (False, True):
+        assert_bits(host(rh.average_pool(dev(x), (3, 3), (1, 1), (1, 1, 1, 1), incl)),
+                    oracle.average_pool(x, (3, 3), (1, 1), (1, 1, 1, 1), incl), "avgpool")
+
+
 def test_batch_norm_bitexact(rh, oracle):
     x = rnd(oracle, 61, 2, 5, 6, 7)
     sc, bi, mu = rnd(oracle, 62, 5), rnd(oracle, 63, 5), rnd(oracle, 64, 5)
