@@ -10,6 +10,7 @@
 //    reference's min_max_out_x_coords (depthwise.rs:24-38), reproduced
 //    exactly.  The Clip/Relu/Add that follow in MobileNetV2 can be fused.
 #include "common.h"
+#include <cstdlib>
 #include "vecmath.h"
 #include "fastdiv_dev.h"
 
@@ -316,10 +317,23 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
   const int r0 = max(iy_lo, 0), r1 = min(iy_lo + rows_in, H);
   if (r1 > r0) {
     const int span = (r1 - r0) * W;
-    for (int pp = 0; pp < np; pp++) {
-      const float* src = x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W;
-      float* dst = tile + (pp * rows_in + (r0 - iy_lo)) * W;
-      for (int q = threadIdx.x; q < span; q += blockDim.x) dst[q] = src[q];
+    if ((W & 3) == 0 && ((uintptr_t)x & 15) == 0) {
+      // 16-byte copies, several in flight per thread (loads are batched
+      // ahead of the LDS stores: the two address spaces cannot alias).
+      const int n4 = span >> 2, total4 = np * n4;
+#pragma unroll 4
+      for (int t = threadIdx.x; t < total4; t += blockDim.x) {
+        const int pp = t / n4, q4 = t - pp * n4;
+        const float4 v =
+            *(const float4*)(x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + 4 * q4);
+        *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
+      }
+    } else {
+      for (int pp = 0; pp < np; pp++) {
+        const float* src = x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W;
+        float* dst = tile + (pp * rows_in + (r0 - iy_lo)) * W;
+        for (int q = threadIdx.x; q < span; q += blockDim.x) dst[q] = src[q];
+      }
     }
   }
   __syncthreads();
@@ -387,7 +401,11 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
       const int PB = 256 / OW;
       auto rows_for = [&](int th) { return (th - 1) * sh + (kh - 1) * dh + 1; };
       int TH = OH;
-      while (TH > 1 && PB * rows_for(TH) * W > 4096) TH = (TH + 1) / 2;
+      static const int budget = [] {
+        const char* e = getenv("RTENHIP_DW_LDS_FLOATS");  // tuning experiments
+        return e ? atoi(e) : 4096;
+      }();
+      while (TH > 1 && PB * rows_for(TH) * W > budget) TH = (TH + 1) / 2;
       const int rows_in = rows_for(TH);
       const size_t lds = (size_t)PB * rows_in * W * sizeof(float);
       dim3 grid((unsigned)((OH + TH - 1) / TH), (unsigned)((planes + PB - 1) / PB));
