@@ -352,6 +352,70 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
   const float* kp = w + c * kh * kw;
   const float b0 = bias ? bias[c] : 0.f;
   const int oh_blk = min(TH, OH - oy0);
+  auto epilogue = [&](int oy, float acc) __attribute__((always_inline)) {
+    const int64_t oi = (int64_t)plane * OH * OW + oy * OW + ox;
+    if (residual) acc = __fadd_rn(acc, residual[oi]);
+    if (act == RTENHIP_ACT_RELU) acc = rust_max(acc, 0.f);
+    else if (act == RTENHIP_ACT_CLIP) acc = rust_clamp(acc, lo, hi);
+    y[oi] = acc;
+  };
+  if constexpr (KH == 3 && KW == 3) {
+    if (dh == 1 && dw == 1) {
+      // 3x3 window in registers: consecutive output rows share 3 - sh input
+      // rows, so each row loads only sh new rows of three taps from LDS;
+      // column validity is fixed per thread.  Taps, skips and rounding order
+      // as in the generic loop below.
+      bool colok[3];
+#pragma unroll
+      for (int kx = 0; kx < 3; kx++) colok[kx] = ox >= b.omin[kx] && ox < b.omax[kx];
+      const int cbase = ox * sw - pl;
+      float win[3][3];
+      auto load_row = [&](int slot, int iy) __attribute__((always_inline)) {
+        const bool ok = iy >= 0 && iy < H;
+        const float* row = tile + (pp * rows_in + (ok ? iy - iy_lo : 0)) * W + cbase;
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++) win[slot][kx] = (ok && colok[kx]) ? row[kx] : 0.f;
+      };
+      int top = oy0 * sh - pt;  // input row of window row 0
+      load_row(0, top);
+      load_row(1, top + 1);
+      load_row(2, top + 2);
+      for (int oyl = 0; oyl < oh_blk; oyl++) {
+        const int oy = oy0 + oyl;
+        if (oyl > 0) {
+          top = oy * sh - pt;
+          if (sh == 1) {
+#pragma unroll
+            for (int kx = 0; kx < 3; kx++) {
+              win[0][kx] = win[1][kx];
+              win[1][kx] = win[2][kx];
+            }
+            load_row(2, top + 2);
+          } else if (sh == 2) {
+#pragma unroll
+            for (int kx = 0; kx < 3; kx++) win[0][kx] = win[2][kx];
+            load_row(1, top + 1);
+            load_row(2, top + 2);
+          } else {
+            load_row(0, top);
+            load_row(1, top + 1);
+            load_row(2, top + 2);
+          }
+        }
+        float acc = b0;
+#pragma unroll
+        for (int ky = 0; ky < 3; ky++) {
+          const int iy = top + ky;
+          if (iy < 0 || iy >= H) continue;
+#pragma unroll
+          for (int kx = 0; kx < 3; kx++)
+            if (colok[kx]) acc = __fadd_rn(acc, __fmul_rn(win[ky][kx], wr[ky * 3 + kx]));
+        }
+        epilogue(oy, acc);
+      }
+      return;
+    }
+  }
   for (int oyl = 0; oyl < oh_blk; oyl++) {
     const int oy = oy0 + oyl;
     float acc = b0;
@@ -367,11 +431,7 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
         acc = __fadd_rn(acc, __fmul_rn(row[kx * dw], wv));
       }
     }
-    const int64_t oi = (int64_t)plane * OH * OW + oy * OW + ox;
-    if (residual) acc = __fadd_rn(acc, residual[oi]);
-    if (act == RTENHIP_ACT_RELU) acc = rust_max(acc, 0.f);
-    else if (act == RTENHIP_ACT_CLIP) acc = rust_clamp(acc, lo, hi);
-    y[oi] = acc;
+    epilogue(oy, acc);
   }
 }
 
