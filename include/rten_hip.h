@@ -121,6 +121,20 @@ rtenhip_status rtenhip_conv_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
                                 const int64_t* dilations, int64_t groups, const float* residual,
                                 int act, float act_lo, float act_hi, rtenhip_tensor* y);
 
+/* ConvTranspose (src/ops/conv.rs:443-577).  x NCHW or NCW, w [C, O, kh, kw]
+ * or [C, O, kw], bias [O] or NULL; pads [top, left, bottom, right] (NCW:
+ * [left, right]) or pad_mode 1 = Same; strides [sh, sw] (NCW: [s]).  Errors
+ * and the Same-padding offsets follow conv_transpose_output_size_and_padding
+ * (conv.rs:382-440) exactly. */
+rtenhip_status rtenhip_conv_transpose_output_shape(const rtenhip_tensor* x,
+                                                   const rtenhip_tensor* w, int pad_mode,
+                                                   const int64_t* pads, const int64_t* strides,
+                                                   int64_t* out_shape, int32_t* out_ndim);
+rtenhip_status rtenhip_conv_transpose_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                          const rtenhip_tensor* w, const float* bias,
+                                          int pad_mode, const int64_t* pads,
+                                          const int64_t* strides, rtenhip_tensor* y);
+
 /* ONNX Gemm (src/ops/matmul.rs:27-81): y = alpha*op(a)@op(b) + beta*c, c
  * broadcast to [M,N] (c may be NULL). */
 rtenhip_status rtenhip_gemm_op_f32(rtenhip_ctx* ctx, const rtenhip_tensor* a,

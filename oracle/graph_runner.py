@@ -29,6 +29,12 @@ def run_op(node, ins):
                       strides=a.get("strides", (1, 1)), dilations=a.get("dilations", (1, 1)),
                       groups=a.get("groups", 1),
                       padding="same" if a.get("auto_pad", "notset").lower() in ("same", "same_upper") else "fixed")
+    if t == "ConvTranspose":
+        one_d = x.ndim == 3
+        return O.conv_transpose(x, ins[1], ins[2] if len(ins) > 2 else None,
+                                pads=a.get("pads", (0, 0) if one_d else (0, 0, 0, 0)),
+                                strides=a.get("strides", (1,) if one_d else (1, 1)),
+                                padding="same" if a.get("auto_pad", "notset").lower() in ("same", "same_upper") else "fixed")
     if t in ("Relu", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu"):
         return O.unary(t, x)
     if t in ("Add", "Sub", "Mul", "Div"):

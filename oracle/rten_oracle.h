@@ -81,6 +81,18 @@ int orc_conv(const float* x, const int64_t* x_shape, int x_ndim, const float* w,
              const int64_t* strides, const int64_t* dilations, int64_t groups, float* out,
              int64_t* out_shape);
 
+/* ConvTranspose: conv_transpose (src/ops/conv.rs:443-535) with col2im
+ * (329-375).  x NCHW (or NCW), w [C, O, kh, kw]; pads [top,left,bottom,right]
+ * (or [left,right] for 1-D), pad_mode 1 = Same.  Output size and the
+ * reference's padding order: conv_transpose_output_size_and_padding (382-440). */
+int orc_conv_transpose_output_size(int64_t in_h, int64_t in_w, int64_t k_h, int64_t k_w,
+                                   int pad_mode, const int64_t* pads_in, int64_t stride_h,
+                                   int64_t stride_w, int64_t out_hw[2], int64_t pads_out[4]);
+int orc_conv_transpose(const float* x, const int64_t* x_shape, int x_ndim, const float* w,
+                       const int64_t* w_shape, const float* bias, int pad_mode,
+                       const int64_t* pads, const int64_t* strides, float* out,
+                       int64_t* out_shape);
+
 /* MaxPool / AveragePool (src/ops/pooling.rs:104-375), NCHW. */
 int orc_max_pool(const float* x, const int64_t x_shape[4], const int64_t kernel[2],
                  const int64_t strides[2], int pad_mode, const int64_t pads[4], float* out,

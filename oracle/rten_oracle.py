@@ -158,6 +158,42 @@ def conv(x, w, bias=None, pads=(0, 0, 0, 0), strides=(1, 1), dilations=(1, 1), g
     return out
 
 
+def conv_transpose_output_size(in_hw, k_hw, strides, padding="fixed", pads=(0, 0, 0, 0)):
+    """conv_transpose_output_size_and_padding (src/ops/conv.rs:382-440); the
+    pads come back in the reference's order (Same: top, bottom, left, right)."""
+    out_hw = (C.c_int64 * 2)()
+    pads_out = (C.c_int64 * 4)()
+    _check(lib().orc_conv_transpose_output_size(
+        C.c_int64(in_hw[0]), C.c_int64(in_hw[1]), C.c_int64(k_hw[0]), C.c_int64(k_hw[1]),
+        C.c_int(1 if padding == "same" else 0), _shape(list(pads)), C.c_int64(strides[0]),
+        C.c_int64(strides[1]), out_hw, pads_out))
+    return (out_hw[0], out_hw[1]), tuple(pads_out)
+
+
+def conv_transpose(x, w, bias=None, pads=(0, 0, 0, 0), strides=(1, 1), padding="fixed"):
+    """ConvTranspose (src/ops/conv.rs:443-535).  w is [C, O, kh, kw] (or
+    [C, O, kw] for 1-D, pads [left, right], strides [s])."""
+    x, w = _c(x), _c(w)
+    nd = x.ndim
+    if nd == 4:
+        (oh, ow), _ = conv_transpose_output_size(x.shape[2:], w.shape[2:], strides, padding, pads)
+        out = np.empty((x.shape[0], w.shape[1], oh, ow), np.float32)
+    elif nd == 3:
+        p4 = (0, pads[0], 0, pads[1]) if len(pads) == 2 else tuple(pads)
+        (oh, ow), _ = conv_transpose_output_size((1, x.shape[2]), (1, w.shape[2]),
+                                                 (1, strides[0]), padding, p4)
+        out = np.empty((x.shape[0], w.shape[1], ow), np.float32)
+    else:
+        raise OpError(5, "Input must have 4 dims (NCHW)")
+    out_shape = (C.c_int64 * 4)()
+    b = _c(bias) if bias is not None else None
+    _check(lib().orc_conv_transpose(_f(x), _shape(x.shape), C.c_int(nd), _f(w), _shape(w.shape),
+                                    _f(b) if b is not None else None,
+                                    C.c_int(1 if padding == "same" else 0), _shape(list(pads)),
+                                    _shape(list(strides)), _f(out), out_shape))
+    return out
+
+
 def max_pool(x, kernel, strides=(1, 1), pads=(0, 0, 0, 0), padding="fixed"):
     x = _c(x)
     (oh, ow), _ = output_size_and_padding(x.shape[2:], kernel, strides, padding, pads)

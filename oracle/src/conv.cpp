@@ -1,3 +1,4 @@
+#include <vector>
 // CPU restatement of RTen's Conv and pooling operators (test infrastructure;
 // see rten_oracle.h).
 //
@@ -260,6 +261,102 @@ int orc_conv(const float* x, const int64_t* x_shape, int x_ndim, const float* w,
   if (x_ndim != 4) return fail(ORC_INVALID_VALUE, "Input must have 4 dims (NCHW)");
   return conv2d(x, x_shape, w, w_shape, bias, pad_mode, pads, strides, dilations, groups, out,
                 out_shape);
+}
+
+// conv_transpose_output_size_and_padding (src/ops/conv.rs:382-440).  The
+// padding comes back ordered as the reference orders it: Same ->
+// [top, bottom, left, right], Fixed -> [top, left, bottom, right];
+// conv_transpose then reads elements [0] and [1] as the top and left pads in
+// both cases (conv.rs:505, 535-541), which this restatement keeps.
+int orc_conv_transpose_output_size(int64_t in_h, int64_t in_w, int64_t k_h, int64_t k_w,
+                                   int pad_mode, const int64_t* pads_in, int64_t stride_h,
+                                   int64_t stride_w, int64_t out_hw[2], int64_t pads_out[4]) {
+  if (stride_h == 0 || stride_w == 0) return fail(ORC_INVALID_VALUE, "Strides must be > 0");
+  if (in_h == 0 || in_w == 0) return fail(ORC_INVALID_VALUE, "Input width and height must be > 0");
+  if (pad_mode == 1) {
+    const int64_t out_h = in_h * stride_h, out_w = in_w * stride_w;
+    const int64_t full_h = (in_h - 1) * stride_h + k_h, full_w = (in_w - 1) * stride_w + k_w;
+    if (full_h < out_h || full_w < out_w) return fail(ORC_INVALID_VALUE, "Input is too small");
+    const int64_t pad_h = full_h - out_h, pad_w = full_w - out_w;
+    pads_out[0] = pad_h / 2;
+    pads_out[1] = (pad_h + 1) / 2;
+    pads_out[2] = pad_w / 2;
+    pads_out[3] = (pad_w + 1) / 2;
+    out_hw[0] = out_h;
+    out_hw[1] = out_w;
+    return ORC_OK;
+  }
+  const int64_t pt = pads_in[0], pl = pads_in[1], pb = pads_in[2], pr = pads_in[3];
+  const int64_t full_h = (in_h - 1) * stride_h + k_h, full_w = (in_w - 1) * stride_w + k_w;
+  if (full_h < pt + pb || full_w < pl + pr) return fail(ORC_INVALID_VALUE, "Input is too small");
+  out_hw[0] = full_h - (pt + pb);
+  out_hw[1] = full_w - (pl + pr);
+  for (int i = 0; i < 4; i++) pads_out[i] = pads_in[i];
+  return ORC_OK;
+}
+
+// conv_transpose (src/ops/conv.rs:443-535) + col2im (329-375): per image
+// col[out_c*kh*kw, H*W] = kernel^T @ x_n (one gemm, alpha 1, no bias), then
+// each output channel is filled with its bias (or 0) and the columns are
+// added in (ky, kx, y, x) order.
+int orc_conv_transpose(const float* x, const int64_t* x_shape, int x_ndim, const float* w,
+                       const int64_t* w_shape, const float* bias, int pad_mode,
+                       const int64_t* pads, const int64_t* strides, float* out,
+                       int64_t* out_shape) {
+  int64_t xs[4], ws[4], p4[4] = {0, 0, 0, 0}, st2[2];
+  if (x_ndim == 3) {
+    // 1-D as 2-D with H = 1 (conv.rs:453-480; Padding::expand_1d_to_2d).
+    xs[0] = x_shape[0], xs[1] = x_shape[1], xs[2] = 1, xs[3] = x_shape[2];
+    ws[0] = w_shape[0], ws[1] = w_shape[1], ws[2] = 1, ws[3] = w_shape[2];
+    if (pads) p4[1] = pads[0], p4[3] = pads[1];
+    st2[0] = 1, st2[1] = strides[0];
+  } else if (x_ndim == 4) {
+    for (int i = 0; i < 4; i++) xs[i] = x_shape[i], ws[i] = w_shape[i];
+    if (pads)
+      for (int i = 0; i < 4; i++) p4[i] = pads[i];
+    st2[0] = strides[0], st2[1] = strides[1];
+  } else {
+    return fail(ORC_INVALID_VALUE, "Input must have 4 dims (NCHW)");
+  }
+  const int64_t N = xs[0], C = xs[1], H = xs[2], W = xs[3];
+  const int64_t KC = ws[0], O = ws[1], kh = ws[2], kw = ws[3];
+  if (C != KC)
+    return fail(ORC_INCOMPATIBLE_INPUT_SHAPES, "Input channels does not match kernel input channels");
+  int64_t ohw[2], pp[4];
+  int st = orc_conv_transpose_output_size(H, W, kh, kw, pad_mode, p4, st2[0], st2[1], ohw, pp);
+  if (st) return st;
+  const int64_t OH = ohw[0], OW = ohw[1], pad_top = pp[0], pad_left = pp[1];
+  const int64_t M = O * kh * kw, HW = H * W;
+  std::vector<float> col((size_t)(M * HW));
+  for (int64_t n = 0; n < N; n++) {
+    const float* xn = x + n * C * HW;
+    orc_gemm(col.data(), HW, w, 1, M, xn, HW, 1, M, HW, C, 1.f, 0.f, nullptr);
+    float* on = out + n * O * OH * OW;
+    for (int64_t c = 0; c < O; c++) {
+      float* img = on + c * OH * OW;
+      const float b = bias ? bias[c] : 0.f;
+      for (int64_t i = 0; i < OH * OW; i++) img[i] = b;
+      for (int64_t ky = 0; ky < kh; ky++)
+        for (int64_t kx = 0; kx < kw; kx++) {
+          const float* src = col.data() + ((c * kh + ky) * kw + kx) * HW;
+          for (int64_t y = 0; y < H; y++) {
+            const int64_t oy = y * st2[0] + ky;
+            if (oy < pad_top || oy >= OH + pad_top) continue;
+            for (int64_t xx = 0; xx < W; xx++) {
+              const int64_t ox = xx * st2[1] + kx;
+              if (ox < pad_left || ox >= OW + pad_left) continue;
+              img[(oy - pad_top) * OW + (ox - pad_left)] += src[y * W + xx];
+            }
+          }
+        }
+    }
+  }
+  if (x_ndim == 3) {
+    out_shape[0] = N, out_shape[1] = O, out_shape[2] = OW;
+  } else {
+    out_shape[0] = N, out_shape[1] = O, out_shape[2] = OH, out_shape[3] = OW;
+  }
+  return ORC_OK;
 }
 
 int orc_max_pool(const float* x, const int64_t x_shape[4], const int64_t kernel[2],

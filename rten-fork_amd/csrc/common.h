@@ -144,6 +144,12 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s);
 rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s);
+// col2im of ConvTranspose (conv.rs:329-375): col [N, O*kh*kw, H, W] -> y
+// [N, O, OH, OW], each output = bias (or 0) + its columns in (ky, kx) order.
+rtenhip_status launch_col2im(const float* col, const float* bias, float* y, int64_t N, int64_t O,
+                             int64_t OH, int64_t OW, int64_t H, int64_t W, int64_t kh,
+                             int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl,
+                             hipStream_t s);
 
 // Fused attention (attention.hip): per (b, h), out = softmax(scale(Q K^T) +
 // mask) V with element strides for every operand (unit stride along the head

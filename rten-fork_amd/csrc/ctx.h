@@ -134,6 +134,15 @@ struct DenseDmaArgs {
 bool dense_dma_eligible(int64_t M, int64_t N, int64_t K, int64_t a_cs, int64_t b_rs, int64_t b_cs);
 rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a);
 
+// ConvTranspose (conv_transpose.cpp).
+rtenhip_status conv_transpose_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* w,
+                                   const float* bias, int pad_mode, const int64_t* pads,
+                                   const int64_t* strides, rtenhip_tensor* y);
+rtenhip_status conv_transpose_output_shape(const rtenhip_tensor* x, const rtenhip_tensor* w,
+                                           int pad_mode, const int64_t* pads,
+                                           const int64_t* strides, int64_t* out_shape,
+                                           int32_t* out_ndim);
+
 // broadcast_shapes (src/ops/binary_elementwise.rs:23-45).
 bool broadcast_shapes(const int64_t* a, int an, const int64_t* b, int bn, int64_t* out, int* on);
 

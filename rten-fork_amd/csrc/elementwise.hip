@@ -235,4 +235,50 @@ rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStr
   return RTENHIP_OK;
 }
 
+// col2im (src/ops/conv.rs:329-375), one thread per output element: the
+// reference fills the plane with the bias and adds each (ky, kx) column image
+// in turn, so an output receives bias + its columns in (ky, kx) order.
+__global__ void col2im_kernel(const float* __restrict__ col, const float* __restrict__ bias,
+                              float* __restrict__ y, int64_t total, int O, int OH, int OW, int H,
+                              int W, int kh, int kw, int sh, int sw, int pt, int pl) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ox = (int)(i % OW);
+    const int oy = (int)((i / OW) % OH);
+    const int64_t nc = i / ((int64_t)OW * OH);
+    const int c = (int)(nc % O);
+    const int64_t n = nc / O;
+    float acc = bias ? bias[c] : 0.f;
+    const float* cb = col + ((n * O + c) * kh * kw) * (int64_t)H * W;
+    for (int ky = 0; ky < kh; ky++) {
+      const int yy = oy + pt - ky;
+      if (yy < 0 || yy % sh) continue;
+      const int yi = yy / sh;
+      if (yi >= H) continue;
+      for (int kx = 0; kx < kw; kx++) {
+        const int xx = ox + pl - kx;
+        if (xx < 0 || xx % sw) continue;
+        const int xi = xx / sw;
+        if (xi >= W) continue;
+        acc = __fadd_rn(acc, cb[((int64_t)(ky * kw + kx) * H + yi) * W + xi]);
+      }
+    }
+    y[i] = acc;
+  }
+}
+
+rtenhip_status launch_col2im(const float* col, const float* bias, float* y, int64_t N, int64_t O,
+                             int64_t OH, int64_t OW, int64_t H, int64_t W, int64_t kh,
+                             int64_t kw, int64_t sh, int64_t sw, int64_t pt, int64_t pl,
+                             hipStream_t s) {
+  const int64_t total = N * O * OH * OW;
+  if (total == 0) return RTENHIP_OK;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)blocks), dim3(256), 0, s, col, bias, y, total,
+                     (int)O, (int)OH, (int)OW, (int)H, (int)W, (int)kh, (int)kw, (int)sh, (int)sw,
+                     (int)pt, (int)pl);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 }  // namespace rtenhip

@@ -232,6 +232,22 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
                                    (int64_t)op.attrs.num("groups", 1), os, &ond);
     if (st) return st;
     outs[0].assign(os, os + ond);
+  } else if (t == "ConvTranspose") {
+    if ((st = need(1))) return st;
+    rtenhip_tensor xd = desc(nullptr, x), wd = desc(nullptr, *in(1));
+    const bool one_d = x.size() == 3;
+    std::string ap = op.attrs.str("auto_pad", "notset");
+    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+    auto pads = op.attrs.ints("pads", one_d ? std::vector<int64_t>{0, 0} : std::vector<int64_t>{0, 0, 0, 0});
+    auto strides = op.attrs.ints("strides", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
+    if (pads.size() != (one_d ? 2u : 4u)) return fail(RTENHIP_INVALID_VALUE, "Wrong number of pad values");
+    if (strides.size() != (one_d ? 1u : 2u))
+      return fail(RTENHIP_INVALID_VALUE, one_d ? "expected 1 stride value" : "expected 2 stride values");
+    int64_t os[4];
+    int32_t ond;
+    st = conv_transpose_output_shape(&xd, &wd, mode, pads.data(), strides.data(), os, &ond);
+    if (st) return st;
+    outs[0].assign(os, os + ond);
   } else if (t == "MaxPool" || t == "AveragePool") {
     if (x.size() != 4) return fail(RTENHIP_INVALID_VALUE, "Expected input to have 4 dims");
     auto k = op.attrs.ints("kernel_size", {1, 1});
@@ -758,6 +774,15 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     ConvAttrs ca = conv_attrs(n, x.ndim == 3);
     return conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(),
                      ca.groups, ptr_of(p, n.fused_residual), n.fused_act, n.act_lo, n.act_hi, &y);
+  }
+  if (t == "ConvTranspose") {
+    rtenhip_tensor w = T(n.inputs[1]);
+    const bool one_d = x.ndim == 3;
+    std::string ap = n.attrs.str("auto_pad", "notset");
+    int mode = (ap == "same" || ap == "SAME_UPPER" || ap == "Same") ? 1 : 0;
+    auto pads = n.attrs.ints("pads", one_d ? std::vector<int64_t>{0, 0} : std::vector<int64_t>{0, 0, 0, 0});
+    auto strides = n.attrs.ints("strides", one_d ? std::vector<int64_t>{1} : std::vector<int64_t>{1, 1});
+    return conv_transpose_impl(ctx, &x, &w, P(2), mode, pads.data(), strides.data(), &y);
   }
   if (is_unary(t)) {
     int op = t == "Relu" ? RTENHIP_UNARY_RELU : t == "Clip" ? RTENHIP_UNARY_CLIP

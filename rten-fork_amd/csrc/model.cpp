@@ -38,6 +38,7 @@ enum AttrsType : uint8_t {
   kAveragePoolAttrs = 2,
   kBatchNormalizationAttrs = 3,
   kConvAttrs = 7,
+  kConvTransposeAttrs = 8,
   kFlattenAttrs = 9,
   kGemmAttrs = 11,
   kMaxPoolAttrs = 15,
@@ -186,6 +187,15 @@ void read_op(const std::string& type, uint8_t attrs_type, const Table& a, Attrs&
     out.nums["groups"] = {(double)a.scalar<uint32_t>(2, 0)};
     out.nums["strides"] = a.vec_of(3, u) ? to_d(u) : std::vector<double>{1, 1};
     out.nums["dilations"] = a.vec_of(4, u) ? to_d(u) : std::vector<double>{1, 1};
+  } else if (type == "ConvTranspose") {
+    // ConvTransposeAttrs: strides (default [1, 1]), auto_pad (default NotSet), pads.
+    need(kConvTransposeAttrs);
+    out.nums["strides"] = a.vec_of(0, u) ? to_d(u) : std::vector<double>{1, 1};
+    const uint8_t auto_pad = a.scalar<uint8_t>(1, 1);
+    if (auto_pad == 0)
+      out.strs["auto_pad"] = "same";
+    else
+      out.nums["pads"] = a.vec_of(2, u) ? to_d(u) : std::vector<double>{0, 0, 0, 0};
   } else if (type == "MaxPool" || type == "AveragePool") {
     need(type == "MaxPool" ? kMaxPoolAttrs : kAveragePoolAttrs);
     if (!a.vec_of(0, u) || u.size() < 2) attr_error();  // kernel_size (required)

@@ -62,6 +62,31 @@ rtenhip_status launch_softmax(const float* x, float* y, int64_t rows, int64_t le
   return RTENHIP_OK;
 }
 
+// Per-wave LDS floats of layer_norm_kernel's partial sums (multiple of 4).
+__host__ __device__ constexpr int ln_part_stride(int len) { return (len / 4 + 8 + 3) & ~3; }
+
+// 0 + p[0] + p[1] + ... + p[n-1], strictly in index order (the reference's
+// serial fold); the LDS reads are issued 16 at a time as 16-byte loads so the
+// chain waits on adds, not on LDS latency.  p is 16-byte aligned.
+__device__ __forceinline__ float serial_sum(const float* p, int n) {
+  float acc = 0.f;
+  int i = 0;
+  for (; i + 16 <= n; i += 16) {
+    float4 q[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) q[j] = *(const float4*)(p + i + 4 * j);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      acc = __fadd_rn(acc, q[j].x);
+      acc = __fadd_rn(acc, q[j].y);
+      acc = __fadd_rn(acc, q[j].z);
+      acc = __fadd_rn(acc, q[j].w);
+    }
+  }
+  for (; i < n; i++) acc = __fadd_rn(acc, p[i]);
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict__ x,
                                                          float* __restrict__ y, int64_t rows,
                                                          int len, const float* __restrict__ scale,
@@ -73,8 +98,9 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
   const bool active = row < rows;
   const float* xr = x + (active ? row : 0) * len;
   float* yr = y + (active ? row : 0) * len;
-  // Per-wave scratch: chunk/group partial sums (len/4 + 2 floats max).
-  float* part = lds + wave * (len / 4 + 8);
+  // Per-wave scratch: chunk/group partial sums (len/4 + 2 floats max), each
+  // wave's slice 16-byte aligned for the vector reads of the serial folds.
+  float* part = lds + wave * ln_part_stride(len);
 
   // slice_sum: full 8-chunks in parallel, then a serial fold.
   const int nchunks = len / 8;
@@ -88,8 +114,7 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
   __syncthreads();
   float mean = 0.f;
   if (lane == 0 && active) {
-    float total = 0.f;
-    for (int c = 0; c < nchunks; c++) total = __fadd_rn(total, part[c]);
+    float total = serial_sum(part, nchunks);
     if (nchunks * 8 < len) {
       float t = 0.f;
       for (int i = nchunks * 8; i < len; i++) t = __fadd_rn(t, xr[i]);
@@ -114,8 +139,7 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
   __syncthreads();
   float inv = 0.f;
   if (lane == 0 && active) {
-    float sum = 0.f;
-    for (int g = 0; g < ngroups; g++) sum = __fadd_rn(sum, part[g]);
+    float sum = serial_sum(part, ngroups);
     for (int i = 4 * ngroups; i < len; i++) {
       float d = __fsub_rn(xr[i], mean);
       sum = __fadd_rn(sum, __fmul_rn(d, d));
@@ -137,7 +161,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s) {
   if (rows == 0 || len == 0) return RTENHIP_OK;
-  size_t shmem = (size_t)ROWS_PER_BLOCK * (len / 4 + 8) * sizeof(float);
+  size_t shmem = (size_t)ROWS_PER_BLOCK * ln_part_stride((int)len) * sizeof(float);
   if (shmem > 160 * 1024) return fail(RTENHIP_UNSUPPORTED_VALUE, "LayerNorm row too long");
   int64_t blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
   hipLaunchKernelGGL(layer_norm_kernel, dim3((unsigned)blocks), dim3(256), shmem, s, x, y, rows,

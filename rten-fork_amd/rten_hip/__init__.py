@@ -91,7 +91,8 @@ EXPORTED_SYMBOLS = [
     "rtenhip_last_error_message", "rtenhip_synchronize", "rtenhip_malloc", "rtenhip_free",
     "rtenhip_memcpy_h2d", "rtenhip_memcpy_d2h", "rtenhip_build_info",
     "rtenhip_output_size_and_padding", "rtenhip_gemm_f32", "rtenhip_conv_output_shape",
-    "rtenhip_conv_f32", "rtenhip_gemm_op_f32", "rtenhip_matmul_f32", "rtenhip_max_pool_f32",
+    "rtenhip_conv_f32", "rtenhip_conv_transpose_output_shape", "rtenhip_conv_transpose_f32",
+    "rtenhip_gemm_op_f32", "rtenhip_matmul_f32", "rtenhip_max_pool_f32",
     "rtenhip_average_pool_f32", "rtenhip_global_average_pool_f32", "rtenhip_batch_norm_f32",
     "rtenhip_layer_norm_f32", "rtenhip_softmax_f32", "rtenhip_unary_f32", "rtenhip_binary_f32",
     "rtenhip_graph_create", "rtenhip_graph_destroy", "rtenhip_graph_add_value",
@@ -258,6 +259,28 @@ def conv(x, w, bias=None, padding=None, groups: int = 1, strides=None, dilations
         _i64(strides), _i64(dilations), C.c_int64(groups),
         C.c_void_p(residual.data_ptr() if residual is not None else None), C.c_int(ACT[act]),
         C.c_float(act_range[0]), C.c_float(act_range[1]), C.byref(yd)))
+    return y
+
+
+def conv_transpose(x, w, bias=None, padding=None, strides=None, ctx=None):
+    """ConvTranspose (src/ops/conv.rs:443-577): w is [C, O, kh, kw] ([C, O, kw]
+    for NCW input); padding None / [top, left, bottom, right] ([left, right]) /
+    "same"."""
+    ctx = ctx or default_context()
+    nd = x.dim()
+    mode, pads = _padding(padding, nd)
+    strides = list(strides or ([1, 1] if nd == 4 else [1]))
+    xd, wd = describe(x), describe(w)
+    os_ = (C.c_int64 * 4)()
+    ond = C.c_int32()
+    check(lib().rtenhip_conv_transpose_output_shape(C.byref(xd), C.byref(wd), C.c_int(mode),
+                                                    _i64(pads), _i64(strides), os_, C.byref(ond)))
+    y = _empty(tuple(os_[i] for i in range(ond.value)), x)
+    yd = describe(y)
+    check(lib().rtenhip_conv_transpose_f32(
+        C.c_void_p(ctx.ptr), C.byref(xd), C.byref(wd),
+        C.c_void_p(bias.data_ptr() if bias is not None else None), C.c_int(mode), _i64(pads),
+        _i64(strides), C.byref(yd)))
     return y
 
 

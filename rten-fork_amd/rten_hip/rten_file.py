@@ -36,7 +36,7 @@ OP_TYPES = [
     "GatherND", "Gelu", "Einsum", "If"]
 
 # sg::OperatorAttrs union ids (schema.fbs OperatorAttrs, NONE = 0).
-ATTRS_AVERAGE_POOL, ATTRS_BATCH_NORM, ATTRS_CONV, ATTRS_FLATTEN = 2, 3, 7, 9
+ATTRS_AVERAGE_POOL, ATTRS_BATCH_NORM, ATTRS_CONV, ATTRS_CONV_TRANSPOSE, ATTRS_FLATTEN = 2, 3, 7, 8, 9
 ATTRS_GEMM, ATTRS_MAX_POOL, ATTRS_RESHAPE, ATTRS_SOFTMAX = 11, 15, 17, 20
 ATTRS_TRANSPOSE, ATTRS_LAYER_NORM, ATTRS_GELU = 21, 30, 37
 NODE_OPERATOR, NODE_CONSTANT, NODE_VALUE = 1, 2, 3
@@ -166,6 +166,9 @@ def _op_attrs(op_type: str, a: dict):
             (2, "u32", int(a.get("groups", 1))),
             (3, "ref", _u32v(a.get("strides", [1, 1]))),
             (4, "ref", _u32v(a.get("dilations", [1, 1])))])
+    if op_type == "ConvTranspose":
+        return ATTRS_CONV_TRANSPOSE, Table([(0, "ref", _u32v(a.get("strides", [1, 1])))] +
+                                           [(f[0] + 1, f[1], f[2]) for f in padding((0, 1))])
     if op_type in ("MaxPool", "AveragePool"):
         f = [(0, "ref", _u32v(a["kernel_size"]))] + padding((1, 2)) + [
             (3, "ref", _u32v(a.get("strides", [1, 1])))]

@@ -190,3 +190,34 @@ def test_fused_attention_bitexact(rh, S, D, scale_op, mask_shape, out_t):
         if not _bits_equal(got, exp):
             d = np.abs(got.astype(np.float64) - exp)
             pytest.fail(f"attention differs: max abs {d.max():.3g}, {(d > 0).sum()} elems")
+
+
+def test_conv_transpose_graph_and_file_bitexact(rh):
+    """A decoder-style graph (Conv -> Relu -> ConvTranspose s2 -> Relu ->
+    ConvTranspose Same), run from a ModelSpec and from its .rten file."""
+    import torch
+    import graph_runner
+    from rten_hip import rten_file
+    from rten_hip.graph import ModelSpec
+
+    rng = np.random.default_rng(21)
+    m = ModelSpec("decoder")
+    x = m.value("x")
+    m.inputs = ["x"]
+    w0 = m.const("w0", rng.uniform(-0.2, 0.2, (32, 16, 3, 3)).astype(np.float32))
+    b0 = m.const("b0", rng.uniform(-0.1, 0.1, (32,)).astype(np.float32))
+    h = m.op("Relu", [m.op("Conv", [x, w0, b0], {"pads": [1, 1, 1, 1], "strides": [1, 1]})])
+    w1 = m.const("w1", rng.uniform(-0.2, 0.2, (32, 16, 2, 2)).astype(np.float32))
+    b1 = m.const("b1", rng.uniform(-0.1, 0.1, (16,)).astype(np.float32))
+    h = m.op("Relu", [m.op("ConvTranspose", [h, w1, b1], {"strides": [2, 2], "pads": [0, 0, 0, 0]})])
+    w2 = m.const("w2", rng.uniform(-0.2, 0.2, (16, 8, 3, 3)).astype(np.float32))
+    m.outputs = [m.op("ConvTranspose", [h, w2], {"strides": [2, 2], "auto_pad": "same"})]
+    xin = rng.random((2, 16, 20, 20), dtype=np.float32)
+    exp = graph_runner.run(m, {"x": xin})[m.outputs[0]]
+    assert exp.shape == (2, 8, 80, 80)
+    for g in (m.to_graph(), rten_file.load_model(rten_file.to_rten_bytes(m))):
+        out = None
+        for _ in range(2):
+            out = g.run({g.input_ids[0]: torch.from_numpy(xin).cuda()}, g.output_ids, out=out)
+            torch.cuda.synchronize()
+            assert _bits_equal(out[0].cpu().numpy(), exp)

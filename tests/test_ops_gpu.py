@@ -291,6 +291,51 @@ def test_layer_norm_bitexact(rh, oracle, shape):
 
 
 # --------------------------------------------------------------------------
+# ConvTranspose (src/ops/conv.rs:329-577)
+# --------------------------------------------------------------------------
+
+CT_CASES = {
+    "s2-k2": ((2, 8, 7, 9), (8, 4, 2, 2), (2, 2), (0, 0, 0, 0), True),
+    "s2-k3-pads": ((2, 16, 10, 10), (16, 8, 3, 3), (2, 2), (1, 1, 1, 1), True),
+    "s3x2-k4x3-uneven": ((1, 5, 6, 7), (5, 3, 4, 3), (3, 2), (1, 2, 0, 1), False),
+    "same-odd-pad": ((2, 6, 5, 5), (6, 4, 4, 3), (2, 2), "same", True),
+    "K300-gemm-blocks": ((2, 300, 6, 6), (300, 16, 2, 2), (2, 2), (0, 0, 0, 0), True),
+    "s1-k3": ((1, 32, 12, 12), (32, 32, 3, 3), (1, 1), (1, 1, 1, 1), True),
+    "single-out-gemv": ((2, 9, 4, 4), (9, 1, 1, 1), (1, 1), (0, 0, 0, 0), False),
+}
+
+
+@pytest.mark.parametrize("case", list(CT_CASES), ids=list(CT_CASES))
+def test_conv_transpose_bitexact(rh, oracle, case):
+    xs, ws, st, pads, has_b = CT_CASES[case]
+    x = rnd(oracle, 131, *xs)
+    w = rnd(oracle, 132, *ws, scale=0.2)
+    b = rnd(oracle, 133, ws[1]) if has_b else None
+    same = pads == "same"
+    exp = oracle.conv_transpose(x, w, b, pads=(0, 0, 0, 0) if same else pads, strides=st,
+                                padding="same" if same else "fixed")
+    got = host(rh.conv_transpose(dev(x), dev(w), dev(b) if has_b else None,
+                                 padding="same" if same else pads, strides=st))
+    assert_bits(got, exp, f"conv_transpose {case}")
+
+
+def test_conv_transpose_1d_and_errors(rh, oracle):
+    x = rnd(oracle, 134, 2, 6, 11)
+    w = rnd(oracle, 135, 6, 5, 3, scale=0.2)
+    b = rnd(oracle, 136, 5)
+    exp = oracle.conv_transpose(x, w, b, pads=(1, 2), strides=(2,))
+    assert_bits(host(rh.conv_transpose(dev(x), dev(w), dev(b), padding=(1, 2), strides=(2,))), exp,
+                "conv_transpose 1d")
+    with pytest.raises(rh.OpError, match="Input channels does not match kernel input channels"):
+        rh.conv_transpose(dev(rnd(oracle, 1, 1, 3, 4, 4)), dev(rnd(oracle, 2, 4, 2, 2, 2)))
+    with pytest.raises(rh.OpError, match="Strides must be > 0"):
+        rh.conv_transpose(dev(rnd(oracle, 1, 1, 3, 4, 4)), dev(rnd(oracle, 2, 3, 2, 2, 2)), strides=(0, 0))
+    with pytest.raises(rh.OpError, match="Input is too small"):
+        rh.conv_transpose(dev(rnd(oracle, 1, 1, 3, 4, 4)), dev(rnd(oracle, 2, 3, 2, 3, 3)),
+                          padding=(4, 4, 4, 4))
+
+
+# --------------------------------------------------------------------------
 # Gemm / MatMul operators
 # --------------------------------------------------------------------------
 

@@ -423,3 +423,48 @@ def test_oracle_matches_committed_fixtures(oracle):
         exp = data[name]
         assert got.shape == exp.shape, name
         assert np.array_equal(got.view(np.uint32), exp.view(np.uint32)), name
+
+
+@pytest.mark.parametrize("case", KATS["conv_transpose"], ids=lambda c: c["source"])
+def test_kat_conv_transpose(oracle, case):
+    """ConvTranspose known answers (PyTorch values in the reference's tests)."""
+    x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+    w = np.array(case["w"], np.float32).reshape(case["w_shape"])
+    b = np.array(case["bias"], np.float32) if case["bias"] else None
+    y = oracle.conv_transpose(x, w, b, pads=case["pads"], strides=case["strides"],
+                              padding=case["padding"])
+    assert list(y.shape) == case["y_shape"]
+    if case["y"] is not None:
+        # expect_equal: atol 1e-8 + rtol 1e-5 (rten-tensor/src/test_util.rs:46-62)
+        np.testing.assert_allclose(y.reshape(-1), case["y"], rtol=1e-5, atol=1e-8)
+
+
+def test_kat_conv_transpose_output_size(oracle):
+    for c in KATS["conv_transpose_output_size"]["cases"]:
+        if "error" in c:
+            with pytest.raises(oracle.OpError, match=c["error"]):
+                oracle.conv_transpose_output_size(c["in"], c["k"], c["strides"], c["padding"], c["pads"])
+        else:
+            out, pads = oracle.conv_transpose_output_size(c["in"], c["k"], c["strides"], c["padding"],
+                                                          c["pads"])
+            assert list(out) == c["out"] and list(pads) == c["pads_out"]
+
+
+@pytest.mark.parametrize("shape", [((2, 5, 7, 6), (5, 3, 3, 4), (2, 3), (1, 2, 0, 1)),
+                                   ((1, 4, 5, 5), (4, 2, 2, 2), (2, 2), (0, 0, 0, 0)),
+                                   ((3, 8, 4, 9), (8, 6, 5, 3), (1, 2), (2, 1, 2, 1))])
+def test_conv_transpose_vs_torch(oracle, shape):
+    """The oracle against torch's conv_transpose2d (fp tolerance: different
+    summation order) on random shapes, fixed padding as output cropping."""
+    torch = pytest.importorskip("torch")
+    import torch.nn.functional as F
+
+    xs, ws, st, pads = shape
+    x = oracle.xorshift(11, int(np.prod(xs))).reshape(xs) - np.float32(0.5)
+    w = oracle.xorshift(12, int(np.prod(ws))).reshape(ws) - np.float32(0.5)
+    b = oracle.xorshift(13, ws[1])
+    got = oracle.conv_transpose(x, w, b, pads=pads, strides=st)
+    full = F.conv_transpose2d(torch.from_numpy(x), torch.from_numpy(w), torch.from_numpy(b),
+                              stride=st).numpy()
+    ref = full[:, :, pads[0]:full.shape[2] - pads[2], pads[1]:full.shape[3] - pads[3]]
+    np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
