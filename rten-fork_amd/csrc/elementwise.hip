@@ -177,27 +177,32 @@ rtenhip_status launch_batch_norm(const float* x, float* y, int64_t N, int64_t C,
 // Zero-bordered copy of an NCHW tensor: out [N, C, H+pt+pb, W+pl+pr].  Gives
 // the DMA GEMM a conv input that needs no bounds checks (the border holds the
 // zeros the reference's im2col would insert, im2col.rs:236-248).
-__global__ void pad_nchw_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t planes,
-                                int H, int W, int Hp, int Wp, int pt, int pl) {
-  const int64_t total = planes * Hp * Wp;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int xw = (int)(i % Wp) - pl;
-    const int yh = (int)((i / Wp) % Hp) - pt;
-    const int64_t plane = i / ((int64_t)Hp * Wp);
-    float v = 0.f;
-    if ((unsigned)xw < (unsigned)W && (unsigned)yh < (unsigned)H) v = x[(plane * H + yh) * W + xw];
-    y[i] = v;
+// One padded row per wave, lanes over its columns (coalesced); the row's
+// source and validity are computed once per row, no per-element division.
+__global__ __launch_bounds__(256) void pad_nchw_kernel(const float* __restrict__ x,
+                                                       float* __restrict__ y, int rows, int H,
+                                                       int W, int Hp, int Wp, int pt, int pl) {
+  const int r = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int plane = r / Hp;
+  const int yh = r - plane * Hp - pt;
+  const bool in = (unsigned)yh < (unsigned)H;
+  const float* xr = x + ((int64_t)plane * H + (in ? yh : 0)) * W;
+  float* yr = y + (int64_t)r * Wp;
+  for (int c = threadIdx.x & 63; c < Wp; c += 64) {
+    const int xw = c - pl;
+    yr[c] = (in && (unsigned)xw < (unsigned)W) ? xr[xw] : 0.f;
   }
 }
 
 rtenhip_status launch_pad_nchw(const float* x, float* y, int64_t planes, int H, int W, int pt,
                                int pl, int pb, int pr, hipStream_t s) {
   const int Hp = H + pt + pb, Wp = W + pl + pr;
-  const int64_t total = planes * Hp * Wp;
-  if (total == 0) return RTENHIP_OK;
-  hipLaunchKernelGGL(pad_nchw_kernel, stream_grid(total, 1), dim3(256), 0, s, x, y, planes, H, W,
-                     Hp, Wp, pt, pl);
+  const int64_t rows = planes * Hp;
+  if (rows == 0 || Wp == 0) return RTENHIP_OK;
+  if (rows >= (int64_t(1) << 31)) return fail(RTENHIP_UNSUPPORTED_VALUE, "padded input too large");
+  hipLaunchKernelGGL(pad_nchw_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, y,
+                     (int)rows, H, W, Hp, Wp, pt, pl);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

@@ -791,50 +791,67 @@ namespace rtenhip {
 // contiguous in the packed layout -- written with float4 stores.
 
 __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a, int64_t lda,
-                                                     int M, int K, int BM, int BK, int il,
-                                                     int tiles_k, int kcw, int vec,
+                                                     int M, int K, int lbm, int BK, int lil,
+                                                     int tiles_k, int lkcw, int vec,
                                                      float* __restrict__ out) {
   extern __shared__ float sh[];  // [kcw][BM + 1]
+  const int BM = 1 << lbm, kcw = 1 << lkcw;
   const int ld = BM + 1;
   const int mt = blockIdx.x, kc = blockIdx.y;
   const int k0 = kc * kcw;
   const int64_t m0 = (int64_t)mt * BM;
-  const int q4 = kcw / 4;  // float4s per row segment (8 or 16)
-  for (int idx = threadIdx.x; idx < BM * q4; idx += blockDim.x) {
-    const int r = idx / q4, c = (idx - r * q4) * 4;
-    const int64_t m = m0 + r;
-    const int k = k0 + c;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (m < M) {
-      const float* src = a + m * lda + k;
-      if (vec && k + 3 < K) {
-        v = *(const float4*)src;
-      } else {
-        if (k < K) v.x = src[0];
-        if (k + 1 < K) v.y = src[1];
-        if (k + 2 < K) v.z = src[2];
-        if (k + 3 < K) v.w = src[3];
+  // BM rows x kcw/4 float4s: 2..8 per thread (a multiple of 256 in total),
+  // all loads issued before the LDS stores.
+  const int lq4 = lkcw - 2;
+  const int per = (BM << lq4) >> 8;
+  float4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j < per) {
+      const int idx = threadIdx.x + j * 256;
+      const int r = idx >> lq4, c = (idx & ((1 << lq4) - 1)) * 4;
+      const int64_t m = m0 + r;
+      const int k = k0 + c;
+      if (m < M) {
+        const float* src = a + m * lda + k;
+        if (vec && k + 3 < K) {
+          v[j] = *(const float4*)src;
+        } else {
+          if (k < K) v[j].x = src[0];
+          if (k + 1 < K) v[j].y = src[1];
+          if (k + 2 < K) v[j].z = src[2];
+          if (k + 3 < K) v[j].w = src[3];
+        }
       }
     }
-    sh[(c + 0) * ld + r] = v.x;
-    sh[(c + 1) * ld + r] = v.y;
-    sh[(c + 2) * ld + r] = v.z;
-    sh[(c + 3) * ld + r] = v.w;
   }
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    if (j < per) {
+      const int idx = threadIdx.x + j * 256;
+      const int r = idx >> lq4, c = (idx & ((1 << lq4) - 1)) * 4;
+      sh[(c + 0) * ld + r] = v[j].x;
+      sh[(c + 1) * ld + r] = v[j].y;
+      sh[(c + 2) * ld + r] = v[j].z;
+      sh[(c + 3) * ld + r] = v[j].w;
+    }
   __syncthreads();
   const int kt0 = k0 / BK;
   const int nkt = min(kcw / BK, tiles_k - kt0);
   float* o = out + ((int64_t)mt * tiles_k + kt0) * (int64_t)(BK * BM);
-  const int slab = 32 * il;
+  // Slab interleave: position q of a 32*il-row slab holds row (q % il) * 32 +
+  // q / il; BM, il and the slab are powers of two, so shifts and masks.
+  const int slab_mask = (32 << lil) - 1, il_mask = (1 << lil) - 1;
   const int n = nkt * BK * BM;  // floats; BM % 4 == 0
-  for (int i = threadIdx.x * 4; i < n; i += blockDim.x * 4) {
-    const int kk = i / BM, pos = i - kk * BM;  // kk counts across the chunk's tiles
+  for (int i = threadIdx.x * 4; i < n; i += 1024) {
+    const int kk = i >> lbm, pos = i & (BM - 1);  // kk counts across the chunk's tiles
     float vals[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-      const int q = (pos + e) % slab;
-      const int mm = (pos + e - q) + (q % il) * 32 + q / il;
-      vals[e] = sh[kk * ld + mm];
+      const int p = pos + e;
+      const int q = p & slab_mask;
+      vals[e] = sh[kk * ld + (p - q) + ((q & il_mask) << 5) + (q >> lil)];
     }
     *(float4*)(o + i) = make_float4(vals[0], vals[1], vals[2], vals[3]);
   }
@@ -851,15 +868,17 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
   const int tiles_m = (M + t.bm - 1) / t.bm;
   if ((int64_t)tiles_m * tiles_k == 0) return RTENHIP_OK;
   const int kcw = t.bm >= 256 ? 32 : 64;
-  if (kcw % t.bk != 0 || t.bm % 4 != 0 || tiles_m > 0x7fffffff)
+  auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+  if (kcw % t.bk != 0 || !pow2(t.bm) || t.bm < 32 || t.bm > 256 || !pow2(t.il) ||
+      tiles_m > 0x7fffffff)
     return fail(RTENHIP_UNSUPPORTED_VALUE, "unsupported A pack shape");
   // packed output chunks are 16-byte aligned (BK * BM % 4 == 0); float4 reads
   // need 16-byte aligned rows
   const int vec = ((uintptr_t)a % 16 == 0 && lda % 4 == 0) ? 1 : 0;
   const size_t lds = (size_t)kcw * (t.bm + 1) * sizeof(float);
   dim3 grid((unsigned)tiles_m, (unsigned)((K + kcw - 1) / kcw));
-  hipLaunchKernelGGL(pack_a_kernel, grid, dim3(256), lds, s, a, lda, M, K, t.bm, t.bk, t.il,
-                     tiles_k, kcw, vec, out);
+  hipLaunchKernelGGL(pack_a_kernel, grid, dim3(256), lds, s, a, lda, M, K, __builtin_ctz(t.bm),
+                     t.bk, __builtin_ctz(t.il), tiles_k, __builtin_ctz(kcw), vec, out);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

@@ -453,6 +453,45 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       continue;
     if (!ce.g.one_d && conv_takes_dma(ce.g)) p.convs[op] = ce;
   }
+  // Gemm with a constant transposed weight (the classifier layer) runs as a
+  // pointwise conv over B images of [K, 1, 1]: out[b, o] keeps its k-ordered
+  // chain per KC block, and beta = 1 over C[o] folds like a conv bias (C +
+  // block 0, then the later blocks; gemm.rs:941-1050).  B = 1 stays on the
+  // reference's gemv (gemm.rs:651-704), whose order differs.
+  for (int op : p.ops) {
+    const Node& n = nodes[op];
+    if (n.op_type != "Gemm" || n.inputs.size() < 2 || !n.input_perm.empty()) continue;
+    const Shape* xs = shape_of(n.inputs[0]);
+    const Shape* ws = shape_of(n.inputs[1]);
+    if (!xs || !ws || xs->size() != 2 || ws->size() != 2) continue;
+    if (nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
+    if (n.attrs.num("alpha", 1.0) != 1.0 || n.attrs.num("transA", 0) != 0 ||
+        n.attrs.num("transB", 0) != 1)
+      continue;
+    const int64_t B = (*xs)[0], K = (*xs)[1], O = (*ws)[0];
+    if (B < 2 || O < 1 || K < 16 || (*ws)[1] != K) continue;
+    if (n.inputs.size() > 2 && n.inputs[2] >= 0) {
+      // C present: only beta = 1 with a constant row vector (beta = 0 keeps
+      // the general path, which ignores C).
+      const Shape* cs = shape_of(n.inputs[2]);
+      if (n.attrs.num("beta", 1.0) != 1.0 || !cs || nodes[n.inputs[2]].kind != NodeKind::Constant)
+        continue;
+      if (!(*cs == Shape{O} || *cs == Shape{1, O})) continue;
+    }
+    if (n.fused_residual >= 0 || n.fused_act) continue;
+    ConvExec ce;
+    ConvPlan& g = ce.g;
+    g = ConvPlan{};
+    g.N = B;
+    g.C = K;
+    g.H = g.W = 1;
+    g.O = O;
+    g.KC = K;
+    g.kh = g.kw = g.sh = g.sw = g.dh = g.dw = g.oh = g.ow = g.groups = 1;
+    g.one_d = false;
+    ce.fc = true;
+    if (conv_takes_dma(g)) p.convs[op] = ce;
+  }
   // MatMuls that run on the dense DMA GEMM: A contiguous (batch folds into
   // M), B 2-D (or with unit batch dims) with unit column stride.
   for (int op : p.ops) {
@@ -493,6 +532,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       if (nodes[op].fused_residual >= 0) readers[nodes[op].fused_residual].push_back(op);
     }
     for (auto& kv : p.convs) {
+      if (kv.second.fc) continue;
       const int v = nodes[kv.first].outputs[0];
       if (outset.count(v) || !readers.count(v)) continue;
       bool ok = true;
@@ -541,7 +581,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     for (size_t i = 0; i < order.size(); i++) {
       const int op = order[i];
       auto cit = p.convs.find(op);
-      if (cit == p.convs.end()) continue;
+      if (cit == p.convs.end() || cit->second.fc) continue;
       const Node& n = nodes[op];
       const ConvPlan& g = cit->second.g;
       const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
@@ -820,6 +860,8 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   }
   if (t == "GlobalAveragePool") return rtenhip_global_average_pool_f32(c, &x, &y);
   if (t == "Gemm") {
+    auto cit = p.convs.find(op_id);
+    if (cit != p.convs.end() && ctx->use_dma) return exec_conv_dma(p, op_id, cit->second);
     rtenhip_tensor b = T(n.inputs[1]);
     rtenhip_tensor cc{};
     bool has_c = n.inputs.size() > 2 && n.inputs[2] >= 0;

@@ -94,6 +94,9 @@ struct ConvExec {
   float* ws = nullptr;      // its workspace and arrival counters, plan-owned
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
+  // A Gemm (FC layer) run as this conv: x [B, K] as B images of [K, 1, 1],
+  // W [O, K] (transB) as O pointwise filters, C [O] as the bias.
+  bool fc = false;
 };
 
 // A MatMul the plan runs on the dense LDS-DMA GEMM: [batch.., M, K] @ [K, N]

@@ -13,7 +13,9 @@
 #include "common.h"
 #include "vecmath.h"
 
+#include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 
 namespace rtenhip {
 
@@ -157,10 +159,131 @@ __global__ __launch_bounds__(256) void layer_norm_kernel(const float* __restrict
     }
 }
 
+// 0 + p[0] + p[s] + ... + p[(n-1)s] in index order, loads issued 8 ahead.
+__device__ __forceinline__ float strided_sum(const float* p, int s, int n) {
+  float acc = 0.f;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = p[(i + j) * s];
+#pragma unroll
+    for (int j = 0; j < 8; j++) acc = __fadd_rn(acc, v[j]);
+  }
+  for (; i < n; i++) acc = __fadd_rn(acc, p[i * s]);
+  return acc;
+}
+
+// LayerNorm for len % 8 == 0 on 16-byte aligned rows, R rows per workgroup:
+// the rows are staged in LDS with 16-byte copies, the 8-element chunk sums and
+// the 4-element groups of squares are formed in parallel into LDS as
+// [chunk][row], and thread r runs row r's two serial folds -- one VALU
+// instruction advances R rows' chains, where layer_norm_kernel spends a whole
+// wave instruction per add of one row.  Same operations in the same order.
+__global__ __launch_bounds__(256) void layer_norm_rows_kernel(
+    const float* __restrict__ x, float* __restrict__ y, int64_t rows, int len, int R,
+    const float* __restrict__ scale, const float* __restrict__ bias, float eps) {
+  extern __shared__ float4 lds4[];
+  const int q = len >> 2;              // float4s per row
+  const int nchunks = len >> 3;
+  const int ngroups = (len - 1) >> 2;  // >= nchunks for len >= 8
+  const int ps = R + 1;                // [chunk][row] stride
+  float* xs = reinterpret_cast<float*>(lds4);
+  float* part = xs + R * len;
+  float* stat = part + ngroups * ps;   // mean[R], inv[R]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row0 = (int64_t)blockIdx.x * R;
+  const int64_t left = rows - row0;
+  const int nr = left < R ? (int)left : R;
+  const float4* x4 = reinterpret_cast<const float4*>(x + row0 * len);
+  for (int t = threadIdx.x; t < nr * q; t += 256) lds4[t] = x4[t];
+  __syncthreads();
+  // slice_sum: chunk c = ((x0 + x4) + (x1 + x5)) + (x2 + x6)) + (x3 + x7)
+  for (int r = wave; r < nr; r += 4)
+    for (int c = lane; c < nchunks; c += 64) {
+      const float4 a = lds4[r * q + 2 * c], b = lds4[r * q + 2 * c + 1];
+      const float z0 = __fadd_rn(a.x, b.x), z1 = __fadd_rn(a.y, b.y);
+      const float z2 = __fadd_rn(a.z, b.z), z3 = __fadd_rn(a.w, b.w);
+      part[c * ps + r] = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
+    }
+  __syncthreads();
+  if ((int)threadIdx.x < nr) {
+    const int r = threadIdx.x;
+    stat[r] = __fdiv_rn(strided_sum(part + r, ps, nchunks), (float)len);
+  }
+  __syncthreads();
+  // iter_sum of (x - mean)^2: groups of 4, then the tail.
+  for (int r = wave; r < nr; r += 4) {
+    const float mean = stat[r];
+    for (int g = lane; g < ngroups; g += 64) {
+      const float4 v = lds4[r * q + g];
+      const float d0 = __fsub_rn(v.x, mean), d1 = __fsub_rn(v.y, mean);
+      const float d2 = __fsub_rn(v.z, mean), d3 = __fsub_rn(v.w, mean);
+      const float ab = __fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1));
+      const float cd = __fadd_rn(__fmul_rn(d2, d2), __fmul_rn(d3, d3));
+      part[g * ps + r] = __fadd_rn(ab, cd);
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nr) {
+    const int r = threadIdx.x;
+    const float mean = stat[r];
+    float sum = strided_sum(part + r, ps, ngroups);
+    for (int i = 4 * ngroups; i < len; i++) {
+      const float d = __fsub_rn(xs[r * len + i], mean);
+      sum = __fadd_rn(sum, __fmul_rn(d, d));
+    }
+    const float ms = __fdiv_rn(sum, (float)len);
+    stat[R + r] = __fdiv_rn(1.f, sqrt_rn(__fadd_rn(ms, eps)));
+  }
+  __syncthreads();
+  float4* y4 = reinterpret_cast<float4*>(y + row0 * len);
+  const float4* s4 = reinterpret_cast<const float4*>(scale);
+  const float4* b4 = reinterpret_cast<const float4*>(bias);
+  for (int r = wave; r < nr; r += 4) {
+    const float mean = stat[r], inv = stat[R + r];
+    for (int c = lane; c < q; c += 64) {
+      const float4 v = lds4[r * q + c], sc = s4[c];
+      float4 o;
+      o.x = __fmul_rn(__fmul_rn(__fsub_rn(v.x, mean), inv), sc.x);
+      o.y = __fmul_rn(__fmul_rn(__fsub_rn(v.y, mean), inv), sc.y);
+      o.z = __fmul_rn(__fmul_rn(__fsub_rn(v.z, mean), inv), sc.z);
+      o.w = __fmul_rn(__fmul_rn(__fsub_rn(v.w, mean), inv), sc.w);
+      if (bias) {
+        const float4 bb = b4[c];
+        o.x = __fadd_rn(o.x, bb.x);
+        o.y = __fadd_rn(o.y, bb.y);
+        o.z = __fadd_rn(o.z, bb.z);
+        o.w = __fadd_rn(o.w, bb.w);
+      }
+      y4[r * q + c] = o;
+    }
+  }
+}
+
 rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s) {
   if (rows == 0 || len == 0) return RTENHIP_OK;
+  const bool rows_ok = len % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
+                       (uintptr_t)scale % 16 == 0 && (!bias || (uintptr_t)bias % 16 == 0);
+  if (rows_ok) {
+    static const int env_rows = [] {
+      const char* e = getenv("RTENHIP_LN_ROWS");  // tuning experiments
+      return e ? atoi(e) : 0;
+    }();
+    const int R = env_rows > 0 ? std::min(env_rows, 64)
+                               : (int)std::max<int64_t>(1, std::min<int64_t>(16, 6144 / len));
+    const int64_t ngroups = (len - 1) / 4;
+    const size_t rshm = ((size_t)R * len + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float);
+    if (rshm <= 64 * 1024) {
+      const int64_t rblocks = (rows + R - 1) / R;
+      hipLaunchKernelGGL(layer_norm_rows_kernel, dim3((unsigned)rblocks), dim3(256), rshm, s, x, y,
+                         rows, (int)len, R, scale, bias, eps);
+      RTENHIP_LAUNCH_CHECK();
+      return RTENHIP_OK;
+    }
+  }
   size_t shmem = (size_t)ROWS_PER_BLOCK * ln_part_stride((int)len) * sizeof(float);
   if (shmem > 160 * 1024) return fail(RTENHIP_UNSUPPORTED_VALUE, "LayerNorm row too long");
   int64_t blocks = (rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;

@@ -161,6 +161,8 @@ def _attention_spec(S, D, H=3, scale_op="Div", mask_shape="b11s", out_transpose=
 
 @pytest.mark.parametrize("S,D,scale_op,mask_shape,out_t", [
     (40, 64, "Div", "b11s", True),     # attention.hip
+    (2, 64, "Div", "b11s", True),      # attention.hip, one key pair
+    (96, 64, "Mul", "b1ss", True),     # attention.hip, three 32-key tiles
     (128, 64, "Mul", "b1ss", False),   # attention.hip, full mask, no transpose
     (64, 16, "Div", "b11s", True),     # head dim 16: unfused sequence
     (130, 64, "Mul", None, True),      # S > 128: unfused sequence
@@ -221,3 +223,38 @@ def test_conv_transpose_graph_and_file_bitexact(rh):
             out = g.run({g.input_ids[0]: torch.from_numpy(xin).cuda()}, g.output_ids, out=out)
             torch.cuda.synchronize()
             assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("B,K,O,c_kind", [
+    (2, 2048, 1000, "vec"),   # ResNet-50 classifier at batch 2
+    (64, 2048, 1000, "row"),  # bench batch, C as [1, O]
+    (3, 17, 10, None),        # short K, no C
+    (5, 300, 130, "vec"),     # two KC blocks, the second partial
+    (1, 2048, 1000, "vec"),   # batch 1: the reference's gemv order (general path)
+])
+def test_gemm_fc_bitexact(rh, B, K, O, c_kind):
+    """Gemm with a constant transposed weight (the classifier layer): batch >= 2
+    runs on the DMA GEMM as a pointwise conv over B images of [K, 1, 1], with C
+    folded like a conv bias (C + block 0, then the later KC blocks)."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    rng = np.random.default_rng(B * 7919 + K)
+    m = ModelSpec(f"fc_{B}_{K}_{O}")
+    x = m.value("x")
+    m.inputs = ["x"]
+    ins = [x, m.const("w", rng.uniform(-0.05, 0.05, (O, K)).astype(np.float32))]
+    if c_kind:
+        shape = (O,) if c_kind == "vec" else (1, O)
+        ins.append(m.const("c", rng.uniform(-0.1, 0.1, shape).astype(np.float32)))
+    m.outputs = [m.op("Gemm", ins, {"alpha": 1.0, "beta": 1.0, "transA": 0, "transB": 1})]
+    xin = rng.random((B, K), dtype=np.float32) - np.float32(0.5)
+    exp = graph_runner.run(m, {"x": xin})[m.outputs[0]]
+    g = m.to_graph()
+    out = None
+    for _ in range(2):  # eager (tuning), then hipGraph replay
+        out = g.run({g.input_ids[0]: torch.from_numpy(xin).cuda()}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        got = out[0].cpu().numpy()
+        assert _bits_equal(got, exp), f"max abs {np.abs(got.astype(np.float64) - exp).max():.3g}"
