@@ -41,6 +41,8 @@ constexpr int KS = AT_D + 1;     // K rows [j][k]: odd stride, conflict-free col
 constexpr int VS = AT_D;         // V rows [k][n]: each half-wave reads one row
 constexpr int AT_THREADS = 256;  // 4 waves
 
+// FULL: S == AT_S, every key and row guard folds away at compile time.
+template <bool FULL>
 __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   __shared__ float Ks[AT_S * KS];
   __shared__ float Vs[AT_S * VS];
@@ -48,7 +50,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   const int h = lane >> 5, l32 = lane & 31;
   const int bh = blockIdx.x;
   const int b = bh / d.H, hd = bh - b * d.H;
-  const int S = d.S;
+  const int S = FULL ? AT_S : d.S;
 
   const float* q = d.q + b * d.q_b + hd * d.q_h;
   const float* kt = d.k + b * d.k_b + hd * d.k_h;
@@ -61,7 +63,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   for (int t = tid; t < AT_S * (AT_D / 4); t += AT_THREADS) {
     const int j = t >> 4, c = (t & 15) * 4;
     float4 kk = make_float4(0.f, 0.f, 0.f, 0.f), w = kk;
-    if (j < S) {
+    if (FULL || j < S) {
       const float* vp = v + (int64_t)j * d.v_s + c;
       w = v4 ? *(const float4*)vp : make_float4(vp[0], vp[1], vp[2], vp[3]);
       if (k4) {
@@ -83,7 +85,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   const int i0 = wave * 32;
   if (i0 >= S) return;  // no barrier follows
   const int i = i0 + l32;  // this lane's query row
-  const bool row_ok = i < S;
+  const bool row_ok = FULL || i < S;
 
   // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand).
   float qf[AT_D / 2];
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
         x = __fdiv_rn(x, d.scale);
       else if (d.scale_op == 2)
         x = __fmul_rn(x, d.scale);
-      if (j < S) {
+      if (FULL || j < S) {
         if (mrow) x = __fadd_rn(x, mrow[(int64_t)j * d.m_j]);
         m = rust_max(m, x);
       }
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
     for (int g = 0; g < 4; g++)
 #pragma unroll
       for (int c = 0; c < 4; c++)
-        if (32 * t + 8 * g + 4 * h + c < S) {
+        if (FULL || 32 * t + 8 * g + 4 * h + c < S) {
           const float ex = vm_exp(__fsub_rn(acc[t][4 * g + c], m));
           acc[t][4 * g + c] = ex;
           part[c] = __fadd_rn(part[c], ex);
@@ -156,7 +158,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   for (int t = 0; t < 4; t++)
 #pragma unroll
     for (int e = 0; e < 16; e++)
-      if (32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) acc[t][e] = __fdiv_rn(acc[t][e], sum);
+      if (FULL || 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) acc[t][e] = __fdiv_rn(acc[t][e], sum);
 
   // out[i][n] = sum over k < S of P[i][k] V[k][n] in k order.  Keys kb + 0..3
   // of an 8-key group are in half 0, kb + 4..7 in half 1; MFMA step k needs
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
     for (int g = 0; g < 4; g++) {
       const int kb = 32 * t + 8 * g;
-      if (kb < S) {
+      if (FULL || kb < S) {
         const float s01 = __shfl_xor(h ? acc[t][4 * g] : acc[t][4 * g + 1], 32);
         const float s23 = __shfl_xor(h ? acc[t][4 * g + 2] : acc[t][4 * g + 3], 32);
         const float a[4] = {h ? s01 : acc[t][4 * g], h ? s23 : acc[t][4 * g + 2],
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const int k = kb + 2 * u;  // S even: k < S implies k + 1 < S
-          if (k < S) {
+          if (FULL || k < S) {
             const float* vr = Vs + (k + h) * VS + l32;
             o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], vr[0], o[0], 0, 0, 0);
             o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], vr[32], o[1], 0, 0, 0);
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       const int r = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (r < S) dst[(int64_t)r * d.o_s + 32 * n2] = o[n2][e];
+      if (FULL || r < S) dst[(int64_t)r * d.o_s + 32 * n2] = o[n2][e];
     }
 }
 
@@ -202,7 +204,10 @@ bool attention_fast_ok(const AttnDesc& d) {
 
 rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s) {
   if (!attention_fast_ok(d)) return fail(RTENHIP_UNSUPPORTED_VALUE, "attention shape not supported");
-  hipLaunchKernelGGL(attention_kernel, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, d);
+  if (d.S == AT_S)
+    hipLaunchKernelGGL(attention_kernel<true>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, d);
+  else
+    hipLaunchKernelGGL(attention_kernel<false>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, d);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }
