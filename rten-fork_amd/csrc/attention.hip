@@ -30,6 +30,7 @@
 #include "vecmath.h"
 
 #include <cfloat>
+#include <cmath>
 
 namespace rtenhip {
 
@@ -204,10 +205,19 @@ bool attention_fast_ok(const AttnDesc& d) {
 
 rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s) {
   if (!attention_fast_ok(d)) return fail(RTENHIP_UNSUPPORTED_VALUE, "attention shape not supported");
+  // x / 2^k and x * 2^-k are the same correctly rounded value (both scale
+  // the exact x by an exact power of two), so a power-of-two divisor -- BERT's
+  // sqrt(64) = 8 -- becomes a multiply: bit-identical, no division per score.
+  AttnDesc e = d;
+  int ex = 0;
+  if (d.scale_op == 1 && std::frexp(d.scale, &ex) == 0.5f && ex > -120 && ex < 120) {
+    e.scale_op = 2;
+    e.scale = std::ldexp(1.f, 1 - ex);
+  }
   if (d.S == AT_S)
-    hipLaunchKernelGGL(attention_kernel<true>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, d);
+    hipLaunchKernelGGL(attention_kernel<true>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, e);
   else
-    hipLaunchKernelGGL(attention_kernel<false>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, d);
+    hipLaunchKernelGGL(attention_kernel<false>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, e);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }
