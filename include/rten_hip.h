@@ -53,6 +53,15 @@ typedef struct {
   int64_t strides[RTENHIP_MAX_DIMS]; /* element strides */
 } rtenhip_tensor;
 
+/* int32 tensor view (Input::IntTensor / Output::IntTensor, src/ops/mod.rs:177-180);
+ * same layout as rtenhip_tensor. */
+typedef struct {
+  int32_t* data;                     /* device pointer */
+  int32_t ndim;
+  int64_t shape[RTENHIP_MAX_DIMS];
+  int64_t strides[RTENHIP_MAX_DIMS]; /* element strides */
+} rtenhip_tensor_i32;
+
 /* Fused epilogue applied after bias (and residual) by GEMM / Conv. */
 typedef enum {
   RTENHIP_ACT_NONE = 0,
@@ -252,6 +261,35 @@ const char* rtenhip_model_describe(const uint8_t* bytes, size_t len);
 int32_t rtenhip_model_input_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
 int32_t rtenhip_model_output_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
 int32_t rtenhip_graph_node_id(rtenhip_graph* g, const char* name);
+
+/* ---- Index / select / convert (BERT embedding and mask path) ---- */
+
+/* Gather (src/ops/gather.rs:21-76): y = x taken along `axis` at `indices`
+ * (negative entries count from the end); y has shape x[:axis] + indices +
+ * x[axis+1:].  Errors: "Axis is invalid", "Entry in `indices` is out of range".
+ * The index check runs on the device, so rtenhip_gather_f32 synchronizes the
+ * context's stream to report it. */
+rtenhip_status rtenhip_gather_output_shape(const rtenhip_tensor* x,
+                                           const rtenhip_tensor_i32* indices, int64_t axis,
+                                           int64_t* out_shape, int32_t* out_ndim);
+rtenhip_status rtenhip_gather_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                  const rtenhip_tensor_i32* indices, int64_t axis,
+                                  rtenhip_tensor* y);
+/* Where (src/ops/binary_elementwise.rs:850-929): out = cond != 0 ? x : y, all
+ * three broadcast to one shape ("Cannot broadcast inputs"). */
+rtenhip_status rtenhip_where_output_shape(const rtenhip_tensor_i32* cond, const rtenhip_tensor* x,
+                                          const rtenhip_tensor* y, int64_t* out_shape,
+                                          int32_t* out_ndim);
+rtenhip_status rtenhip_where_f32(rtenhip_ctx* ctx, const rtenhip_tensor_i32* cond,
+                                 const rtenhip_tensor* x, const rtenhip_tensor* y,
+                                 rtenhip_tensor* out);
+/* Cast (src/ops/convert.rs:6-17): f32 -> i32 as Rust `as` (truncation toward
+ * zero, saturating, NaN -> 0); i32 -> f32 rounded to nearest even.  y has x's
+ * shape and is contiguous. */
+rtenhip_status rtenhip_cast_f32_to_i32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
+                                       rtenhip_tensor_i32* y);
+rtenhip_status rtenhip_cast_i32_to_f32(rtenhip_ctx* ctx, const rtenhip_tensor_i32* x,
+                                       rtenhip_tensor* y);
 
 #ifdef __cplusplus
 }

@@ -311,3 +311,46 @@ def matmul(a, b):
     _check(lib().orc_matmul(_f(a), _shape(a.shape), C.c_int(a.ndim), _f(b), _shape(b.shape),
                             C.c_int(b.ndim), _f(out), os_, C.byref(ond)))
     return out
+
+
+# ---------------------------------------------------------------------------
+# Index / select / convert: numpy restatements (exact data movement)
+# ---------------------------------------------------------------------------
+
+def gather(x, indices, axis):
+    """gather (src/ops/gather.rs:21-76): numpy.take along the resolved axis;
+    negative entries count from the end (SliceItem::Index)."""
+    x = np.asarray(x)
+    idx = np.asarray(indices, np.int64)
+    if not -x.ndim <= axis < x.ndim:
+        raise OpError(5, "Axis is invalid")
+    axis = axis % x.ndim
+    n = x.shape[axis]
+    res = np.where(idx < 0, idx + n, idx)
+    if ((res < 0) | (res >= n)).any():
+        raise OpError(5, "Entry in `indices` is out of range")
+    return np.take(x, res, axis=axis)
+
+
+def where(cond, x, y):
+    """where_op (src/ops/binary_elementwise.rs:850-929)."""
+    cond, x, y = np.asarray(cond), np.asarray(x), np.asarray(y)
+    try:
+        shape = np.broadcast_shapes(cond.shape, np.broadcast_shapes(x.shape, y.shape))
+    except ValueError:
+        raise OpError(3, "Cannot broadcast inputs") from None
+    return np.where(np.broadcast_to(cond, shape) != 0, np.broadcast_to(x, shape),
+                    np.broadcast_to(y, shape)).astype(x.dtype)
+
+
+def cast_f32_to_i32(x):
+    """Cast to Int32 (src/ops/convert.rs:10): Rust `as i32` -- truncation toward
+    zero, saturating at the i32 range, NaN -> 0."""
+    x = np.asarray(x, np.float32).astype(np.float64)
+    out = np.where(np.isnan(x), 0.0, np.clip(np.trunc(x), -2.0 ** 31, 2.0 ** 31 - 1))
+    return out.astype(np.int32)
+
+
+def cast_i32_to_f32(x):
+    """Cast to Float (src/ops/convert.rs:14): `as f32`, round to nearest even."""
+    return np.asarray(x, np.int32).astype(np.float32)

@@ -101,7 +101,9 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_timing_report", "rtenhip_model_load", "rtenhip_model_load_with_options",
     "rtenhip_model_describe", "rtenhip_last_error_code", "rtenhip_model_input_ids",
     "rtenhip_model_output_ids", "rtenhip_graph_node_id", "rtenhip_graph_set_io",
-    "rtenhip_graph_plan",
+    "rtenhip_graph_plan", "rtenhip_gather_output_shape", "rtenhip_gather_f32",
+    "rtenhip_where_output_shape", "rtenhip_where_f32", "rtenhip_cast_f32_to_i32",
+    "rtenhip_cast_i32_to_f32",
 ]
 
 
@@ -178,6 +180,73 @@ def default_context() -> Context:
         _default_ctx = Context(0)
     _default_ctx.sync_stream()
     return _default_ctx
+
+
+def describe_i32(t) -> Tensor:
+    """rtenhip_tensor_i32 view of an int32 device torch tensor (same layout as
+    rtenhip_tensor; Input::IntTensor, src/ops/mod.rs:177-180)."""
+    torch = _torch()
+    if t.dtype != torch.int32:
+        raise OpError(1, "IncorrectInputType: expected int32")
+    if not t.is_cuda:
+        raise OpError(1, "tensor must be on the GPU (HIP device)")
+    if t.dim() > MAX_DIMS:
+        raise OpError(6, "too many dims")
+    d = Tensor()
+    d.data = t.data_ptr() if t.numel() else None
+    d.ndim = t.dim()
+    for i, (s, st) in enumerate(zip(t.shape, t.stride())):
+        d.shape[i] = s
+        d.strides[i] = st
+    return d
+
+
+def gather(x, indices, axis=0, ctx=None):
+    """Gather (src/ops/gather.rs:21-76): x float32, indices int32."""
+    ctx = ctx or default_context()
+    xd, idd = describe(x), describe_i32(indices)
+    os_ = (C.c_int64 * MAX_DIMS)()
+    ond = C.c_int32()
+    check(lib().rtenhip_gather_output_shape(C.byref(xd), C.byref(idd), C.c_int64(axis), os_,
+                                            C.byref(ond)))
+    y = _empty(tuple(os_[i] for i in range(ond.value)), x)
+    yd = describe(y)
+    check(lib().rtenhip_gather_f32(C.c_void_p(ctx.ptr), C.byref(xd), C.byref(idd),
+                                   C.c_int64(axis), C.byref(yd)))
+    return y
+
+
+def where(cond, x, y, ctx=None):
+    """Where (src/ops/binary_elementwise.rs:850-929): cond int32, x/y float32."""
+    ctx = ctx or default_context()
+    cd, xd, yd = describe_i32(cond), describe(x), describe(y)
+    os_ = (C.c_int64 * MAX_DIMS)()
+    ond = C.c_int32()
+    check(lib().rtenhip_where_output_shape(C.byref(cd), C.byref(xd), C.byref(yd), os_,
+                                           C.byref(ond)))
+    out = _empty(tuple(os_[i] for i in range(ond.value)), x)
+    od = describe(out)
+    check(lib().rtenhip_where_f32(C.c_void_p(ctx.ptr), C.byref(cd), C.byref(xd), C.byref(yd),
+                                  C.byref(od)))
+    return out
+
+
+def cast(x, to, ctx=None):
+    """Cast (src/ops/convert.rs:6-17): to = "int32" (from float32) or "float"
+    (from int32)."""
+    torch = _torch()
+    ctx = ctx or default_context()
+    if to == "int32":
+        y = torch.empty(tuple(x.shape), dtype=torch.int32, device=x.device)
+        xd, yd = describe(x), describe_i32(y)
+        check(lib().rtenhip_cast_f32_to_i32(C.c_void_p(ctx.ptr), C.byref(xd), C.byref(yd)))
+    elif to == "float":
+        y = torch.empty(tuple(x.shape), dtype=torch.float32, device=x.device)
+        xd, yd = describe_i32(x), describe(y)
+        check(lib().rtenhip_cast_i32_to_f32(C.c_void_p(ctx.ptr), C.byref(xd), C.byref(yd)))
+    else:
+        raise OpError(6, f"unsupported cast target {to!r}")
+    return y
 
 
 def _empty(shape, like):

@@ -438,3 +438,63 @@ def test_conv_bitexact_general_kernel(rh, oracle, case):
         test_conv_bitexact(rh, oracle, case)
     finally:
         lib.rtenhip_debug_set_dma(ctypes.c_void_p(ctx.ptr), 1)
+
+
+# --------------------------------------------------------------------------
+# Gather / Where / Cast (gather.rs:21-76, binary_elementwise.rs:850-929,
+# convert.rs:6-17): exact data movement, compared bit for bit
+# --------------------------------------------------------------------------
+
+def _idev(a):
+    import torch
+
+    # np.array keeps 0-d (scalar) indices 0-d; ascontiguousarray would make them 1-d
+    return torch.from_numpy(np.array(a, dtype=np.int32, order="C")).cuda()
+
+
+def test_gather_bitexact(rh, oracle):
+    for case in KATS["gather"]["cases"]:
+        x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+        idx = np.array(case["indices"], np.int32).reshape(case["indices_shape"])
+        assert_bits(host(rh.gather(dev(x), _idev(idx), case["axis"])),
+                    oracle.gather(x, idx, case["axis"]), case["source"] if "source" in case else "gather")
+    rng = np.random.default_rng(5)
+    # embedding lookup: [vocab, hidden] table, [batch, seq] ids (negative ids count from the end)
+    table = rnd(oracle, 71, 1000, 768)
+    ids = rng.integers(-1000, 1000, (32, 128)).astype(np.int32)
+    assert_bits(host(rh.gather(dev(table), _idev(ids), 0)), oracle.gather(table, ids, 0), "embedding")
+    # strided input view, inner axis, scalar index
+    x = rnd(oracle, 72, 6, 50, 7)
+    xt = dev(x).transpose(0, 2)
+    idx = rng.integers(0, 50, (3, 4)).astype(np.int32)
+    assert_bits(host(rh.gather(xt, _idev(idx), 1)), oracle.gather(x.transpose(2, 1, 0), idx, 1), "strided")
+    assert_bits(host(rh.gather(dev(x), _idev(np.array(3, np.int32)), -1)), oracle.gather(x, np.array(3), -1), "scalar")
+    for case in KATS["gather"]["errors"]:
+        x = np.zeros(case["x_shape"], np.float32)
+        idx = np.array(case["indices"], np.int32).reshape(case["indices_shape"])
+        with pytest.raises(rh.OpError) as e:
+            rh.gather(dev(x), _idev(idx), case["axis"])
+        assert e.value.code == case["code"] and str(e.value) == case["message"]
+
+
+def test_where_and_cast_bitexact(rh, oracle):
+    for case in KATS["where"]["cases"]:
+        c = np.array(case["cond"], np.int32).reshape(case["cond_shape"])
+        x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+        y = np.array(case["y"], np.float32).reshape(case["y_shape"])
+        assert_bits(host(rh.where(_idev(c), dev(x), dev(y))), oracle.where(c, x, y), "where")
+    rng = np.random.default_rng(6)
+    mask = (rng.random((2, 1, 1, 128)) > 0.3).astype(np.int32)  # BERT mask broadcast
+    s = rnd(oracle, 73, 2, 12, 128, 128)
+    fill = np.array(-10000.0, np.float32)
+    assert_bits(host(rh.where(_idev(mask), dev(s), dev(fill))), oracle.where(mask, s, fill), "mask")
+    for case in KATS["where"]["errors"]:
+        with pytest.raises(rh.OpError) as e:
+            rh.where(_idev(np.array(case["cond"], np.int32)), dev(np.array(case["x"], np.float32)),
+                     dev(np.array(case["y"], np.float32)))
+        assert e.value.code == case["code"] and str(e.value) == case["message"]
+    vals = np.array([0.5, -0.5, 1.9999, -1.9999, 3e9, -3e9, np.nan, np.inf, -np.inf, 2147483520.0,
+                     -2147483648.0, 123456789.0, -3.4028235e38, 3.4028235e38], np.float32)
+    assert np.array_equal(host(rh.cast(dev(vals), "int32")), oracle.cast_f32_to_i32(vals))
+    ints = np.array([0, 1, -1, 16777217, -16777217, 2 ** 31 - 1, -2 ** 31, 123456789], np.int32)
+    assert_bits(host(rh.cast(_idev(ints), "float")), oracle.cast_i32_to_f32(ints), "cast i32->f32")

@@ -468,3 +468,53 @@ def test_conv_transpose_vs_torch(oracle, shape):
                               stride=st).numpy()
     ref = full[:, :, pads[0]:full.shape[2] - pads[2], pads[1]:full.shape[3] - pads[3]]
     np.testing.assert_allclose(got, ref, rtol=1e-5, atol=1e-5)
+
+
+# --------------------------------------------------------------------------
+# Gather / Where / Cast (gather.rs, binary_elementwise.rs, convert.rs)
+# --------------------------------------------------------------------------
+
+def _f32_vals(v):
+    return np.array([{"f32::MIN": -3.4028235e38, "f32::MAX": 3.4028235e38}.get(e, e) for e in v],
+                    np.float32)
+
+
+def test_kat_gather(oracle):
+    c = KATS["gather"]
+    for case in c["cases"]:
+        x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+        idx = np.array(case["indices"], np.int32).reshape(case["indices_shape"])
+        y = oracle.gather(x, idx, case["axis"])
+        assert list(y.shape) == case["y_shape"]
+        assert np.array_equal(y.ravel(), np.array(case["y"], np.float32)), case
+    r = c["rand_case"]
+    x = oracle.xorshift(r["seed"], int(np.prod(r["x_shape"]))).reshape(r["x_shape"])
+    y = oracle.gather(x, np.array(r["indices"], np.int32).reshape(r["indices_shape"]), r["axis"])
+    assert list(y.shape) == r["y_shape"] and np.array_equal(y.reshape(4, 10), x[r["indices"]])
+    for case in c["errors"]:
+        x = np.zeros(case["x_shape"], np.float32)
+        idx = np.array(case["indices"], np.int32).reshape(case["indices_shape"])
+        with pytest.raises(oracle.OpError) as e:
+            oracle.gather(x, idx, case["axis"])
+        assert e.value.code == case["code"] and str(e.value) == case["message"]
+
+
+def test_kat_where_and_cast(oracle):
+    c = KATS["where"]
+    for case in c["cases"]:
+        out = oracle.where(np.array(case["cond"], np.int32).reshape(case["cond_shape"]),
+                           np.array(case["x"], np.float32).reshape(case["x_shape"]),
+                           np.array(case["y"], np.float32).reshape(case["y_shape"]))
+        assert list(out.shape) == case["out_shape"]
+        assert np.array_equal(out.ravel(), np.array(case["out"], np.float32)), case
+    for case in c["errors"]:
+        with pytest.raises(oracle.OpError) as e:
+            oracle.where(np.array(case["cond"], np.int32), np.array(case["x"], np.float32),
+                         np.array(case["y"], np.float32))
+        assert e.value.code == case["code"] and str(e.value) == case["message"]
+    for case in KATS["cast"]["i32_to_f32"]:
+        y = oracle.cast_i32_to_f32(np.array(case["x"], np.int32))
+        assert np.array_equal(y, np.array(case["y"], np.float32))
+    for case in KATS["cast"]["f32_to_i32"]:
+        y = oracle.cast_f32_to_i32(_f32_vals(case["x"]))
+        assert np.array_equal(y, np.array(case["y"], np.int32))
