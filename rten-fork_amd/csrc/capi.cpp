@@ -59,6 +59,10 @@ Ctx::~Ctx() {
 float* Ctx::scratch_floats(size_t n, size_t slot) {
   size_t need = n * sizeof(float);
   if (slot >= (size_t)NSLOTS) return nullptr;
+  if (scratch_log) {
+    size_t& m = (*scratch_log)[slot];
+    m = std::max(m, n);
+  }
   if (need > slot_cap[slot] || !slots[slot]) {
     void* p = nullptr;
     size_t cap = need + (need >> 2) + 256;
@@ -67,11 +71,16 @@ float* Ctx::scratch_floats(size_t n, size_t slot) {
     if (slots[slot]) (void)hipFree(slots[slot]);
     slots[slot] = p;
     slot_cap[slot] = cap;
+    scratch_gen++;
   }
   return static_cast<float*>(slots[slot]);
 }
 
 int* Ctx::split_counters(size_t n) {
+  if (scratch_log) {
+    size_t& m = (*scratch_log)[NSLOTS];
+    m = std::max(m, n);
+  }
   if (n > counters_cap || !counters) {
     if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
     if (counters) (void)hipFree(counters);
@@ -82,8 +91,20 @@ int* Ctx::split_counters(size_t n) {
     // ordered with a non-blocking stream.
     if (hipMemsetAsync(counters, 0, cap * sizeof(int), stream) != hipSuccess) return nullptr;
     counters_cap = cap;
+    scratch_gen++;
   }
   return counters;
+}
+
+bool Ctx::reserve_scratch(const std::map<size_t, size_t>& need) {
+  for (auto& kv : need) {
+    if (kv.first == (size_t)NSLOTS) {
+      if (!split_counters(kv.second)) return false;
+    } else if (!scratch_floats(kv.second, kv.first)) {
+      return false;
+    }
+  }
+  return true;
 }
 
 const int* Ctx::dtab(int C, int H, int W, int kh, int kw, int dh, int dw) {

@@ -43,6 +43,18 @@ struct Ctx {
   int* split_counters(size_t n);
   int* counters = nullptr;
   size_t counters_cap = 0;
+  // Bumped whenever scratch_floats / split_counters reallocate: a captured
+  // hipGraph that baked in an older scratch pointer must be re-captured
+  // (Graph::run compares it with the generation stored at capture).
+  uint64_t scratch_gen = 0;
+  // While set, every scratch request is recorded as (slot -> max floats);
+  // slot NSLOTS stands for the split counters.  Graph::run records a plan's
+  // needs during its eager runs and reserves them before capturing, so no
+  // scratch buffer grows (and synchronizes) inside a capture.
+  std::map<size_t, size_t>* scratch_log = nullptr;
+  // Grow scratch slots (and the split counters) to the recorded needs.
+  // Returns false on an allocation failure.
+  bool reserve_scratch(const std::map<size_t, size_t>& need);
   // Device table of VirtualIm2Col row offsets for one conv geometry.
   const int2* ktab(int C, int H, int W, int kh, int kw, int dh, int dw);
   // Device table of per-k input offsets c*H*W + ky*dh*W + kx*dw (DMA GEMM).

@@ -78,6 +78,8 @@ Plan::~Plan() {
     if (kv.second.counters) (void)hipFree(kv.second.counters);
   }
   if (mm_pack) (void)hipFree(mm_pack);
+  for (auto& kv : conv_unfused)
+    if (kv.second.first) (void)hipFree(kv.second.first);
   for (auto& kv : side_events) {
     if (kv.second.first) (void)hipEventDestroy(kv.second.first);
     if (kv.second.second) (void)hipEventDestroy(kv.second.second);
@@ -322,7 +324,10 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
     auto perm = op.attrs.ints("perm", {});
     if (perm.empty())
       for (int64_t i = (int64_t)x.size() - 1; i >= 0; i--) perm.push_back(i);
-    if (perm.size() != x.size()) return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
+    // Out-of-range or repeated axes are rejected like the reference's
+    // transpose (layout.rs:479-498), before anything indexes the shape.
+    if (perm.size() != x.size() || !valid_perm(perm, x.size()))
+      return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
     outs[0].clear();
     for (auto p : perm) outs[0].push_back(x[p]);
   } else {
@@ -420,6 +425,20 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       else
         outs[0].assign(bs, bs + bn);
     }
+    if (!st && nodes[op].op_type == "Conv" && nodes[op].fused_residual >= 0) {
+      // Conv -> Add(other): fused in the conv's epilogue only when the other
+      // input has the conv output's shape; otherwise the Add broadcasts and
+      // runs unfused after the conv (binary_elementwise.rs:65-439).
+      const Shape* rs = shape_of(nodes[op].fused_residual);
+      int64_t bs[RTENHIP_MAX_DIMS];
+      int bn;
+      if (!rs || !broadcast_shapes(outs[0].data(), (int)outs[0].size(), rs->data(), (int)rs->size(), bs, &bn)) {
+        st = fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast inputs");
+      } else if (*rs != outs[0]) {
+        p.conv_unfused[op] = {nullptr, outs[0]};
+        outs[0].assign(bs, bs + bn);
+      }
+    }
     if (st) {
       std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
       set_error(st, msg);
@@ -451,7 +470,14 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (plan_conv(&xt, &wt, ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(), ca.groups,
                   ce.g) != RTENHIP_OK)
       continue;
-    if (!ce.g.one_d && conv_takes_dma(ce.g)) p.convs[op] = ce;
+    if (!ce.g.one_d && conv_takes_dma(ce.g) && !p.conv_unfused.count(op)) p.convs[op] = ce;
+  }
+  for (auto& kv : p.conv_unfused) {
+    const size_t bytes = (size_t)std::max<int64_t>(1, prod(kv.second.second)) * sizeof(float);
+    if (hipMalloc(&kv.second.first, bytes) != hipSuccess) {
+      kv.second.first = nullptr;
+      return fail(RTENHIP_HIP_ERROR, "hipMalloc failed");
+    }
   }
   // Gemm with a constant transposed weight (the classifier layer) runs as a
   // pointwise conv over B images of [K, 1, 1]: out[b, o] keeps its k-ordered
@@ -745,7 +771,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       b.refs = -1;
       release(b.off, b.size);
     }
-    if (n.fused_residual >= 0 && n.op_type == "Conv") {
+    if (n.fused_residual >= 0 && n.op_type == "Conv" && !p.conv_unfused.count(op)) {
       const Shape* rs = shape_of(n.fused_residual);
       if (!rs || *rs != os)
         return fail(RTENHIP_UNSUPPORTED_VALUE, "Fused residual must match the Conv output shape");
@@ -812,6 +838,20 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       return fail(RTENHIP_UNSUPPORTED_VALUE, "zero-bordered value needs the DMA conv path");
     rtenhip_tensor w = T(n.inputs[1]);
     ConvAttrs ca = conv_attrs(n, x.ndim == 3);
+    auto uf = p.conv_unfused.find(op_id);
+    if (uf != p.conv_unfused.end()) {
+      // Broadcasting Add after the conv: conv -> Add -> activation, unfused.
+      rtenhip_tensor cy = desc(uf->second.first, uf->second.second);
+      rtenhip_status st = conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(),
+                                    ca.dil.data(), ca.groups, nullptr, RTENHIP_ACT_NONE, 0.f, 0.f, &cy);
+      if (st) return st;
+      rtenhip_tensor r = T(n.fused_residual);
+      if ((st = rtenhip_binary_f32(c, RTENHIP_BINARY_ADD, &cy, &r, &y))) return st;
+      if (n.fused_act == RTENHIP_ACT_RELU) return rtenhip_unary_f32(c, RTENHIP_UNARY_RELU, &y, 0.f, 0.f, &y);
+      if (n.fused_act == RTENHIP_ACT_CLIP)
+        return rtenhip_unary_f32(c, RTENHIP_UNARY_CLIP, &y, n.act_lo, n.act_hi, &y);
+      return RTENHIP_OK;
+    }
     return conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(),
                      ca.groups, ptr_of(p, n.fused_residual), n.fused_act, n.act_lo, n.act_hi, &y);
   }
@@ -894,6 +934,8 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     auto perm = n.attrs.ints("perm", {});
     if (perm.empty())
       for (int64_t i = x.ndim - 1; i >= 0; i--) perm.push_back(i);
+    if ((int)perm.size() != x.ndim || !valid_perm(perm, (size_t)x.ndim))
+      return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
     rtenhip_tensor v = x;
     for (int i = 0; i < x.ndim; i++) {
       v.shape[i] = x.shape[perm[i]];
@@ -1459,10 +1501,29 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     RTENHIP_HIP_CHECK(hipMalloc(&arena, plan->arena_bytes));
     arena_cap = plan->arena_bytes;
   }
+  const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
+  if (replay) {
+    // The ctx scratch buffers a capture bakes in must not move afterwards:
+    // grow them to this plan's recorded needs now (outside any capture), and
+    // re-capture when any of them was reallocated since this plan's capture
+    // (another plan or a per-op call may have grown and freed them).
+    bool grow = false;
+    for (auto& kv : plan->scratch_need)
+      grow |= kv.first == (size_t)Ctx::NSLOTS
+                  ? kv.second > ctx->counters_cap || !ctx->counters
+                  : kv.second * sizeof(float) > ctx->slot_cap[kv.first] || !ctx->slots[kv.first];
+    if (grow) {
+      RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
+      RTENHIP_HIP_CHECK(hipStreamSynchronize(side_stream));
+      if (!ctx->reserve_scratch(plan->scratch_need))
+        return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    }
+  }
   std::vector<float*> bin, bout;
   for (int i = 0; i < n_in; i++) bin.push_back(ins[i].data);
   for (int i = 0; i < n_out; i++) bout.push_back(outs[i].data);
-  bool same_binding = plan->exec && bin == plan->bound_in && bout == plan->bound_out;
+  bool same_binding = plan->exec && bin == plan->bound_in && bout == plan->bound_out &&
+                      plan->scratch_gen == ctx->scratch_gen;
   plan->bound_in = bin;
   plan->bound_out = bout;
 
@@ -1510,7 +1571,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, plan->side_events[d].second, 0));
     return RTENHIP_OK;
   };
-  const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
   plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
   if (replay) {
     if (!same_binding) {
@@ -1531,6 +1591,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         ctx->stream = exec_stream;
         hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
         if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&plan->exec, g, nullptr, nullptr, 0);
+        plan->scratch_gen = ctx->scratch_gen;
         if (g) (void)hipGraphDestroy(g);
         if (!st && e2 != hipSuccess) st = hip_fail(e2, "hipGraph capture");
       } else {
@@ -1543,6 +1604,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
   } else {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
+    ctx->scratch_log = &plan->scratch_need;
     for (int op : plan->ops) {
       hipEvent_t a = nullptr, b = nullptr;
       st = before_op(op);
@@ -1564,6 +1626,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         break;
       }
     }
+    ctx->scratch_log = nullptr;
     ctx->stream = exec_stream;
     if (!st) st = join_all();
     plan->eager_runs++;

@@ -126,6 +126,10 @@ struct Plan {
   std::map<int, ConvExec> convs;      // op id -> DMA conv state
   std::map<int, PaddedValue> padded;  // value id -> zero-bordered storage
   std::map<int, MatMulExec> matmuls;  // op id -> dense DMA MatMul state
+  // Conv -> Add fusions whose Add broadcasts (the other input is not the conv
+  // output's shape): the conv runs into this plan-owned buffer, then the Add
+  // and the activation run as the unfused graph would.  op id -> (buffer, shape).
+  std::map<int, std::pair<float*, Shape>> conv_unfused;
   float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
   int64_t mm_pack_floats = 0;
   // What mm_pack holds during a run: the A value it was packed from (value
@@ -145,6 +149,8 @@ struct Plan {
   // hipGraph replay state: valid for these exact input/output pointers.
   hipGraphExec_t exec = nullptr;
   std::vector<float*> bound_in, bound_out;
+  uint64_t scratch_gen = 0;                // Ctx::scratch_gen when exec was captured
+  std::map<size_t, size_t> scratch_need;   // ctx scratch slot -> floats (eager runs)
   int eager_runs = 0;
 };
 

@@ -8,6 +8,7 @@
 // graph is then optimized unless the caller opts out (ModelOptions::
 // with_optimize, model.rs:156-162).
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -320,7 +321,13 @@ PModel parse(const uint8_t* bytes, size_t len) {
         std::vector<uint32_t> shape;
         if (!data.vec_of(0, shape)) throw LoadError{RTENHIP_INVALID_VALUE, "parse error: missing required field `shape`"};
         pn.shape.assign(shape.begin(), shape.end());
-        const size_t count = (size_t)prod(pn.shape);
+        // Element count and byte size with overflow checks: a file whose dims
+        // multiply past 2^62 elements is malformed, not a huge allocation.
+        uint64_t count64 = 1;
+        for (uint32_t dim : shape)
+          if (__builtin_mul_overflow(count64, (uint64_t)dim, &count64) || count64 > (UINT64_MAX >> 2))
+            throw LoadError{RTENHIP_INVALID_VALUE, "graph error: constant shape is too large"};
+        const size_t count = (size_t)count64;
         if (data.has(4)) {
           // External data in the tensor segment (model.rs:477-503).
           if (!v2) throw LoadError{RTENHIP_INVALID_VALUE, "graph error: tensor data section missing"};
@@ -422,6 +429,11 @@ rtenhip_graph* rtenhip_model_load_with_options(rtenhip_ctx* ctx, const uint8_t* 
   } catch (const LoadError& e) {
     set_error(e.code, e.msg);
     return nullptr;
+  } catch (const std::exception& e) {
+    // bad_alloc / length_error from a malformed size: a load error, never an
+    // exception across the C ABI.
+    set_error(RTENHIP_INVALID_VALUE, std::string("read error: ") + e.what());
+    return nullptr;
   }
   rtenhip_graph* g = rtenhip_graph_create(ctx);
   for (size_t i = 0; i < pm.nodes.size(); i++) {
@@ -468,6 +480,9 @@ const char* rtenhip_model_describe(const uint8_t* bytes, size_t len) {
     out = describe(parse(bytes, len));
   } catch (const LoadError& e) {
     set_error(e.code, e.msg);
+    return nullptr;
+  } catch (const std::exception& e) {
+    set_error(RTENHIP_INVALID_VALUE, std::string("read error: ") + e.what());
     return nullptr;
   }
   return out.c_str();

@@ -258,3 +258,99 @@ def test_gemm_fc_bitexact(rh, B, K, O, c_kind):
         torch.cuda.synchronize()
         got = out[0].cpu().numpy()
         assert _bits_equal(got, exp), f"max abs {np.abs(got.astype(np.float64) - exp).max():.3g}"
+
+
+def _pad_conv_spec(C=3, O=32):
+    """Conv 3x3 pad 1 on a graph input (padded through the context's scratch
+    slot) -> Relu."""
+    from rten_hip.graph import ModelSpec
+
+    rng = np.random.default_rng(5)
+    m = ModelSpec("padconv")
+    x = m.value("x")
+    m.inputs = ["x"]
+    w = m.const("w", rng.uniform(-0.3, 0.3, (O, C, 3, 3)).astype(np.float32))
+    b = m.const("b", rng.uniform(-0.1, 0.1, (O,)).astype(np.float32))
+    m.outputs = [m.op("Relu", [m.op("Conv", [x, w, b], {"pads": [1, 1, 1, 1], "strides": [1, 1]})])]
+    return m
+
+
+def test_replay_after_scratch_grows(rh):
+    """A captured plan that baked in a context scratch buffer is re-captured
+    when another plan grows (and frees) that buffer: batch 1 twice (eager,
+    capture), batch 8 (grows the padded-input scratch), batch 1 again with the
+    same input/output buffers -- bit-exact every time."""
+    import torch
+    import graph_runner
+
+    spec = _pad_conv_spec()
+    g = spec.to_graph()
+    rng = np.random.default_rng(11)
+    x1 = rng.random((1, 3, 40, 40), dtype=np.float32)
+    x8 = rng.random((8, 3, 40, 40), dtype=np.float32)
+    e1 = graph_runner.run(spec, {"x": x1})[spec.outputs[0]]
+    e8 = graph_runner.run(spec, {"x": x8})[spec.outputs[0]]
+    d1 = torch.from_numpy(x1).cuda()
+    out1 = None
+    for _ in range(2):
+        out1 = g.run({g.input_ids[0]: d1}, g.output_ids, out=out1)
+        torch.cuda.synchronize()
+        assert _bits_equal(out1[0].cpu().numpy(), e1)
+    out8 = g.run({g.input_ids[0]: torch.from_numpy(x8).cuda()}, g.output_ids)
+    torch.cuda.synchronize()
+    assert _bits_equal(out8[0].cpu().numpy(), e8)
+    # fresh allocations that may land on the freed scratch memory
+    junk = [torch.full((1 << 20,), float("nan"), device="cuda") for _ in range(8)]
+    for _ in range(2):
+        out1 = g.run({g.input_ids[0]: d1}, g.output_ids, out=out1)
+        torch.cuda.synchronize()
+        assert _bits_equal(out1[0].cpu().numpy(), e1)
+    del junk
+
+
+@pytest.mark.parametrize("other", ["const_c11", "input_c11", "scalar"])
+def test_conv_add_broadcast_unfused(rh, other):
+    """Conv -> Add(x) -> Relu where x broadcasts ([1, C, 1, 1] constant or
+    input, or a scalar): the Add runs unfused after the conv, as in the
+    reference, instead of failing the plan."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    rng = np.random.default_rng(17)
+    m = ModelSpec("conv_add_bcast")
+    x = m.value("x")
+    m.inputs = ["x"]
+    w = m.const("w", rng.uniform(-0.3, 0.3, (16, 8, 1, 1)).astype(np.float32))
+    c = m.op("Conv", [x, w], {"pads": [0, 0, 0, 0], "strides": [1, 1]})
+    ins = {"x": rng.random((2, 8, 12, 12), dtype=np.float32)}
+    if other == "const_c11":
+        o = m.const("bias", rng.uniform(-1, 1, (1, 16, 1, 1)).astype(np.float32))
+    elif other == "scalar":
+        o = m.const("s", np.array(0.25, np.float32))
+    else:
+        o = m.value("bias")
+        m.inputs.append("bias")
+        ins["bias"] = rng.uniform(-1, 1, (1, 16, 1, 1)).astype(np.float32)
+    m.outputs = [m.op("Relu", [m.op("Add", [c, o])])]
+    exp = graph_runner.run(m, ins)[m.outputs[0]]
+    g = m.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
+    out = None
+    for _ in range(2):
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
+def test_transpose_invalid_perm(rh):
+    import torch
+    from rten_hip.graph import Graph
+
+    for perm in ([0, 0, 1], [0, 1, 3], [2, 1]):
+        g = Graph()
+        x = g.add_value("x")
+        y = g.add_value("y")
+        g.add_op("t", "Transpose", [x], [y], {"perm": perm})
+        with pytest.raises(rh.OpError, match="Permutation is invalid"):
+            g.run({x: torch.zeros(2, 3, 4, device="cuda")}, [y])

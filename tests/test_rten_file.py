@@ -237,3 +237,19 @@ def test_load_errors_on_device(gpu):
     m.outputs = [m.op("Cast", [x], name="cast")]
     with pytest.raises(OpError, match="operator error: operator Cast"):
         rten_file.load_model(rten_file.to_rten_bytes(m))
+
+
+@pytest.mark.parametrize("inline_max", [0, 10 ** 9])
+def test_constant_shape_overflow_is_a_load_error(monkeypatch, inline_max):
+    """Dims whose product overflows 64 bits are rejected as a load error
+    (checked count * 4), not a wrapped bounds check or a C++ exception."""
+    m = ModelSpec("huge")
+    x = m.value("x")
+    m.inputs = ["x"]
+    big = m.const("big", np.zeros((7, 7), np.float32))
+    m.outputs = [m.op("Add", [x, big], name="add")]
+    orig = rten_file._u32v
+    monkeypatch.setattr(rten_file, "_u32v",
+                        lambda v: orig([0xFFFFFFFF] * 3) if tuple(v) == (7, 7) else orig(v))
+    with pytest.raises(OpError, match="constant shape is too large"):
+        rten_file.describe_model(_model_bytes(m, inline_max=inline_max))
