@@ -35,16 +35,49 @@ typedef __attribute__((address_space(4))) const int const_int_t;
 
 constexpr int DKC = 256;
 
-// LDS-DMA helpers (buffer_load_dword{,x4} ... lds).  Kept out of the kernel
-// template: clang's host pass rejects the 16-byte form inside some template
-// instantiations (substitution failure, silently dropping the kernel stub).
-__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff,
-                                          uint32_t soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 16, voff, soff, 0, 0);
+// Timing experiments only (separate builds, never the shipped library):
+// 1 = no DMA inside the K loop, 2 = no MFMA, 3 = 1 without the per-tile
+// barrier, 4 = 3 without the per-tile LDS reads.  Results are wrong under all.
+#ifndef RTENHIP_DMA_EXPERIMENT
+#define RTENHIP_DMA_EXPERIMENT 0
+#endif
+
+// LDS-DMA helpers (buffer_load_dword{,x4} ... lds), issued as inline asm.
+// With the compiler builtin, the waitcnt pass treats every LDS read as
+// possibly aliasing every DMA still in flight; once a wave has more DMAs
+// outstanding than it can track individually (wave tiles above 32x32: 10+ per
+// K tile) it drains the whole ring with an s_waitcnt vmcnt(0) before each
+// tile's LDS reads, exposing the full DMA latency every K tile.  As asm the
+// DMAs are invisible to that pass; the kernel orders them itself with counted
+// s_waitcnt vmcnt + s_barrier (wait_dma) and drains them before the epilogue
+// reuses the LDS.  (Loads the compiler does track stay correctly waited for:
+// vmcnt retires in issue order, so extra untracked loads only make its waits
+// stricter.)  M0 holds the wave-uniform LDS destination; one wait state
+// separates the M0 write from the DMA.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 make_rsrc(const void* base, uint32_t num_records) {
+  const uint64_t a = (uint64_t)base;
+  return (u32x4){(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, num_records, 0x00020000u};
 }
-__device__ __forceinline__ void lds_dma4(__amdgpu_buffer_rsrc_t r, lds_void_t* dst, uint32_t voff,
-                                         uint32_t soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, dst, 4, voff, soff, 0, 0);
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void lds_dma16(u32x4 r, uint32_t dst, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(soff)
+               : "memory", "m0");
+}
+__device__ __forceinline__ void lds_dma4(u32x4 r, uint32_t dst, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %3 offen lds"
+               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(soff)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+__device__ __forceinline__ float f4_at(const float4& v, int j) {
+  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
 // One block computes a BM x BN tile with WAVES_M x WAVES_N waves, each owning
@@ -112,10 +145,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   const int kt_lo = kb_split >= 0 ? kb_split * TPB : 0;
   const int kt_hi = kb_split >= 0 ? min(tiles_k, kt_lo + TPB) : tiles_k;
 
-  const __amdgpu_buffer_rsrc_t ra =
-      __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb =
-      __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, d.x_bytes, 0x00020000);
+  const u32x4 ra = make_rsrc(d.apk, 0x7fffffffu);
+  const u32x4 rb = make_rsrc(d.x, d.x_bytes);
 
   // Per-lane B offsets: one per 64-column group this wave loads.
   constexpr int NG = BN / 64;
@@ -158,14 +189,37 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   const uint32_t va = (uint32_t)(wave * A_PER_W * A_CHUNK + lane * A_LB);
   const uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
   const_int_t* ktab4 = (const_int_t*)d.ktab4;
+  const uint32_t lds0 = lds_addr(lds);
+
+  // K-table offsets of the tile about to be issued, loaded at the start of
+  // the tile body that issues it, so the scalar load's latency hides under
+  // that body's first MFMAs.
+  constexpr int KPRE = BVEC ? 1 : B_PER_W;
+  uint32_t kpre[KPRE];
+  auto load_k = [&](int kt) __attribute__((always_inline)) {
+    if constexpr (!BVEC) {
+      kt = min(kt, tiles_k - 1);
+#pragma unroll
+      for (int i = 0; i < B_PER_W; i++) kpre[i] = (uint32_t)ktab4[kt * BK + (wave * B_PER_W + i) / NG];
+    }
+  };
+
+  // An empty asm reading the prefetched offsets, placed after the MFMAs:
+  // keeps the load from being sunk into the conditional issue block.
+  auto pin_k = [&]() __attribute__((always_inline)) {
+    if constexpr (!BVEC) {
+#pragma unroll
+      for (int i = 0; i < B_PER_W; i++) asm volatile("" ::"s"(kpre[i]));
+    }
+  };
 
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
-    float* As = lds + stage * STAGE;
-    float* Bs = As + BM * BK;
+    const uint32_t As = lds0 + (uint32_t)(stage * STAGE * 4);
+    const uint32_t Bs = As + BM * BK * 4;
     const uint32_t a_soff = a_row_base + (uint32_t)kt * (BM * BK * 4);
 #pragma unroll
     for (int i = 0; i < A_PER_W; i++) {
-      lds_void_t* dst = (lds_void_t*)(As + (wave * A_PER_W + i) * (A_CHUNK / 4));
+      const uint32_t dst = As + (uint32_t)((wave * A_PER_W + i) * A_CHUNK);
       if constexpr (A_LB == 16)
         lds_dma16(ra, dst, va + i * A_CHUNK, a_soff);
       else
@@ -176,15 +230,14 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
 #pragma unroll
       for (int i = 0; i < B_PER_W; i++) {
         const int gi = wave * B_PER_W + i;  // rows 4*gi .. 4*gi+3: 1 KB of LDS
-        lds_dma16(rb, (lds_void_t*)(Bs + gi * 256), vb4[i], b_soff);
+        lds_dma16(rb, Bs + gi * 1024, vb4[i], b_soff);
       }
     } else {
-      const_int_t* kt4 = ktab4 + kt * BK;
 #pragma unroll
       for (int i = 0; i < B_PER_W; i++) {
         const int gi = wave * B_PER_W + i;  // wave-uniform
         const int kl = gi / NG, g = gi % NG;
-        lds_dma4(rb, (lds_void_t*)(Bs + kl * BN + g * 64), vb[g], (uint32_t)kt4[kl]);
+        lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[i]);
       }
     }
   };
@@ -251,7 +304,10 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   // LDS read offsets of this lane (floats, relative to a stage): its MI A
   // values and NI B values of one k row are contiguous (see pack_a_kernel and
   // the B column permutation above).
-  const int a_lane = half * BM + wm + l32 * MI;
+  // A tiles are packed k-quad major (see pack_a_kernel): a lane's A values of
+  // 4 consecutive k steps (k = 2*(4*sq + j) + half, j = 0..3) are one float4,
+  // so each 32-row group costs one ds_read_b128 per 4 MFMA steps.
+  const int a_lane = (half * BM + wm + l32) * 4;
   const int b_lane = BM * BK + half * BN + wn + l32 * NI;
 
   // Software pipeline over K tiles.  A tile's operands are read from LDS
@@ -262,9 +318,9 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   // counted and the barrier is a raw s_barrier, so later tiles' DMAs stay in
   // flight across it (__syncthreads would drain vmcnt).
   constexpr int PER_TILE = A_PER_W + B_PER_W;
-  typedef float va_t __attribute__((ext_vector_type(MI)));
+  static_assert(KSTEPS % 4 == 0, "A k-quads");
   typedef float vb_t __attribute__((ext_vector_type(NI)));
-  va_t av[2][KSTEPS];
+  float4 av[2][KSTEPS / 4][MI];
   vb_t bv[2][KSTEPS];
 
   auto wait_dma = [&](int allowed_tiles) __attribute__((always_inline)) {
@@ -280,40 +336,54 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   };
   auto read_tile = [&](auto set_tag, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
+    if constexpr (RTENHIP_DMA_EXPERIMENT == 4) {
+      if (stage != 0) return;  // keep only the prologue's read
+    }
     const float* As = lds + stage * STAGE + a_lane;
     const float* Bs = lds + stage * STAGE + b_lane;
 #pragma unroll
     for (int s = 0; s < KSTEPS; s++) {
-      av[SET][s] = *(const va_t*)(As + 2 * s * BM);
+      if (s % 4 == 0) {
+#pragma unroll
+        for (int mi = 0; mi < MI; mi++) av[SET][s / 4][mi] = *(const float4*)(As + (s / 2 * BM + mi * 32) * 4);
+      }
       bv[SET][s] = *(const vb_t*)(Bs + 2 * s * BN);
     }
   };
   auto mfma_steps = [&](auto set_tag, auto s0_tag, auto s1_tag) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
+    if constexpr (RTENHIP_DMA_EXPERIMENT == 2) return;
 #pragma unroll
     for (int s = decltype(s0_tag)::value; s < decltype(s1_tag)::value; s++)
 #pragma unroll
       for (int mi = 0; mi < MI; mi++)
 #pragma unroll
         for (int ni = 0; ni < NI; ni++)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[SET][s][mi], bv[SET][s][ni],
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4_at(av[SET][s / 4][mi], s % 4), bv[SET][s][ni],
                                                              acc[mi][ni], 0, 0, 0);
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  constexpr int TAIL = KSTEPS >= 4 ? 2 : 1;
+#ifndef RTENHIP_DMA_TAIL
+#define RTENHIP_DMA_TAIL 2
+#endif
+  constexpr int TAIL = KSTEPS >= 2 * RTENHIP_DMA_TAIL ? RTENHIP_DMA_TAIL : (KSTEPS >= 4 ? 2 : 1);
   using IMid = std::integral_constant<int, KSTEPS - TAIL>;
   using IEnd = std::integral_constant<int, KSTEPS>;
 
   int stage = 0;  // stage holding tile kt
   auto body = [&](auto set_tag, int kt) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
+    load_k(kt + STAGES);  // unconditional (clamped): no phi, so no early wait
+    __builtin_amdgcn_sched_barrier(0);  // keep the scalar load ahead of the MFMAs
     mfma_steps(set_tag, I0{}, IMid{});
+    pin_k();
     if (kt + 1 < kt_hi) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       wait_dma(min(STAGES - 2, kt_hi - kt - 2));
-      __builtin_amdgcn_s_barrier();
-      if (kt + STAGES < kt_hi) issue(stage, kt + STAGES);
+      if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
+      if (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2)
+        if (kt + STAGES < kt_hi) issue(stage, kt + STAGES);
       stage = stage + 1 == STAGES ? 0 : stage + 1;
       read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
     }
@@ -329,11 +399,13 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   auto body_fast = [&](auto set_tag, auto stg_tag, int kt) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
     constexpr int STG = decltype(stg_tag)::value;
+    load_k(kt + STAGES);
+    __builtin_amdgcn_sched_barrier(0);
     mfma_steps(set_tag, I0{}, IMid{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
-    __builtin_amdgcn_s_barrier();
-    issue(STG, kt + STAGES);
+    if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
+    if constexpr (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2) issue(STG, kt + STAGES);
     read_tile(std::integral_constant<int, SET ^ 1>{}, (STG + 1) % STAGES);
     mfma_steps(set_tag, IMid{}, IEnd{});
   };
@@ -392,7 +464,10 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   // Prologue: fill every stage, wait for the first tile, read it.
 #pragma unroll
   for (int s = 0; s < STAGES; s++)
-    if (kt_lo + s < kt_hi) issue(s, kt_lo + s);
+    if (kt_lo + s < kt_hi) {
+      load_k(kt_lo + s);
+      issue(s, kt_lo + s);
+    }
   wait_dma(min(STAGES, kt_hi - kt_lo) - 1);
   __builtin_amdgcn_s_barrier();
   read_tile(I0{}, 0);
@@ -536,6 +611,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     // block is transposed through this wave's LDS slot so every lane stores
     // (and loads the residual as) 16-byte row segments: 4 dwordx4 per block
     // instead of 16 dword accesses.  Same per-element arithmetic as below.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land in the slots
     __syncthreads();  // every wave is done reading the K stages
     float* slot = lds + wave * 1024;
 #pragma unroll
@@ -660,6 +736,7 @@ static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
 // The wave tile is (BM/WAVES_M) x (BN/WAVES_N).  All configurations produce
 // bit-identical results (same KC-block summation order), so the choice is
 // purely a performance one: dma_default_cfg below, or plan-time tuning.
+#ifndef RTENHIP_DMA_CONFIGS  // (overridable for ISA inspection builds of one config)
 #define RTENHIP_DMA_CONFIGS(X)          \
   X(0, 512, 128, 128, 16, 4, 2, 2, 3)   \
   X(1, 256, 128, 128, 16, 2, 2, 2, 3)   \
@@ -680,6 +757,7 @@ static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   X(16, 512, 64, 128, 16, 2, 4, 4, 3)   \
   X(17, 128, 32, 64, 16, 1, 2, 4, 3)    \
   X(18, 1024, 128, 128, 16, 4, 4, 4, 3)
+#endif
 
 struct DmaCfgInfo {
   int nt, bm, bn, bk, waves_m, waves_n;
@@ -709,7 +787,7 @@ bool dma_cfg_bvec(int cfg) {
 
 DmaTile dma_cfg_tile(int cfg) {
   const DmaCfgInfo& c = kDmaCfgs[cfg];
-  return DmaTile{c.bm, c.bk, c.bm / c.waves_m / 32};
+  return DmaTile{c.bm, c.bk, 1};  // k-quad layout, independent of the wave tile
 }
 
 int dma_default_cfg(int M, int N, int K) {
@@ -783,19 +861,21 @@ extern "C" void rtenhip_debug_set_dma_mode(int mode) { rtenhip::g_dma_dbg = mode
 namespace rtenhip {
 
 // Pack A[M, K] (row stride lda, unit column stride) into
-// [tiles_m][tiles_k][BK][BM] tiles, zero padded, rows of each 32*il slab
-// interleaved: position l*il + mi holds row mi*32 + l.  One workgroup per
+// [tiles_m][tiles_k][BK/4][BM][4] tiles, zero padded: within a tile, float
+// (q * BM + r) * 4 + j holds row r, k = 8 * (q >> 1) + 2 * j + (q & 1), so
+// the lane owning row r and k parity (q & 1) reads the A operands of 4
+// consecutive 32x32x2 MFMA steps with one ds_read_b128.  One workgroup per
 // (m tile, kcw-wide k chunk; kcw = 64, or 32 for 256-row tiles so the LDS
 // stays under 64 KB): the BM rows are read as kcw*4-byte segments (float4 per
 // lane when aligned), transposed through LDS, and the chunk's kcw/BK tiles --
 // contiguous in the packed layout -- written with float4 stores.
 
 __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a, int64_t lda,
-                                                     int M, int K, int lbm, int BK, int lil,
+                                                     int M, int K, int lbm, int lbk,
                                                      int tiles_k, int lkcw, int vec,
                                                      float* __restrict__ out) {
   extern __shared__ float sh[];  // [kcw][BM + 1]
-  const int BM = 1 << lbm, kcw = 1 << lkcw;
+  const int BM = 1 << lbm, BK = 1 << lbk, kcw = 1 << lkcw;
   const int ld = BM + 1;
   const int mt = blockIdx.x, kc = blockIdx.y;
   const int k0 = kc * kcw;
@@ -840,20 +920,15 @@ __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a
   const int kt0 = k0 / BK;
   const int nkt = min(kcw / BK, tiles_k - kt0);
   float* o = out + ((int64_t)mt * tiles_k + kt0) * (int64_t)(BK * BM);
-  // Slab interleave: position q of a 32*il-row slab holds row (q % il) * 32 +
-  // q / il; BM, il and the slab are powers of two, so shifts and masks.
-  const int slab_mask = (32 << lil) - 1, il_mask = (1 << lil) - 1;
   const int n = nkt * BK * BM;  // floats; BM % 4 == 0
+  const int ltile = lbm + lbk;  // log2(BK * BM)
   for (int i = threadIdx.x * 4; i < n; i += 1024) {
-    const int kk = i >> lbm, pos = i & (BM - 1);  // kk counts across the chunk's tiles
-    float vals[4];
-#pragma unroll
-    for (int e = 0; e < 4; e++) {
-      const int p = pos + e;
-      const int q = p & slab_mask;
-      vals[e] = sh[kk * ld + (p - q) + ((q & il_mask) << 5) + (q >> lil)];
-    }
-    *(float4*)(o + i) = make_float4(vals[0], vals[1], vals[2], vals[3]);
+    const int t = i >> ltile;
+    const int rem4 = (i & ((1 << ltile) - 1)) >> 2;
+    const int q = rem4 >> lbm, r = rem4 & (BM - 1);
+    const int kb = t * BK + 8 * (q >> 1) + (q & 1);  // k of j = 0, within the chunk
+    *(float4*)(o + i) = make_float4(sh[kb * ld + r], sh[(kb + 2) * ld + r], sh[(kb + 4) * ld + r],
+                                    sh[(kb + 6) * ld + r]);
   }
 }
 
@@ -869,7 +944,7 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
   if ((int64_t)tiles_m * tiles_k == 0) return RTENHIP_OK;
   const int kcw = t.bm >= 256 ? 32 : 64;
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
-  if (kcw % t.bk != 0 || !pow2(t.bm) || t.bm < 32 || t.bm > 256 || !pow2(t.il) ||
+  if (kcw % t.bk != 0 || !pow2(t.bm) || t.bm < 32 || t.bm > 256 || !pow2(t.bk) || t.bk % 8 != 0 ||
       tiles_m > 0x7fffffff)
     return fail(RTENHIP_UNSUPPORTED_VALUE, "unsupported A pack shape");
   // packed output chunks are 16-byte aligned (BK * BM % 4 == 0); float4 reads
@@ -878,7 +953,7 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
   const size_t lds = (size_t)kcw * (t.bm + 1) * sizeof(float);
   dim3 grid((unsigned)tiles_m, (unsigned)((K + kcw - 1) / kcw));
   hipLaunchKernelGGL(pack_a_kernel, grid, dim3(256), lds, s, a, lda, M, K, __builtin_ctz(t.bm),
-                     t.bk, __builtin_ctz(t.il), tiles_k, __builtin_ctz(kcw), vec, out);
+                     __builtin_ctz(t.bk), tiles_k, __builtin_ctz(kcw), vec, out);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

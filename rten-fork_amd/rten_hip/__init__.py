@@ -22,7 +22,8 @@ from typing import Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "librten_hip.so")
+# RTENHIP_LIB: an alternative build (timing experiments); default the in-tree library.
+LIB_PATH = os.environ.get("RTENHIP_LIB") or os.path.join(_PKG, "librten_hip.so")
 
 MAX_DIMS = 8
 
