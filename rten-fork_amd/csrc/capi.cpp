@@ -206,6 +206,7 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
         d.counters = a.counters;
       }
     }
+    d.persist_k = a.persist_k;
     rtenhip_status st = launch_gemm_dma(d, cfg, c->stream);
     if (st) return st;
   }
@@ -627,6 +628,7 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
       d.counters = cnt;
     }
   }
+  d.persist_k = a.persist_k;
   return launch_gemm_dma(d, cfg, s);
 }
 

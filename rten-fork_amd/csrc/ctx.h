@@ -81,6 +81,7 @@ struct ConvDmaArgs {
   int64_t ws_cap;
   int* counters;
   int64_t cnt_cap;
+  int persist_k;  // persistent launch: resident blocks per CU (0: one block per item)
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
 bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, int64_t groups,
@@ -142,6 +143,7 @@ struct DenseDmaArgs {
   int64_t ws_cap;
   int* counters;
   int64_t cnt_cap;
+  int persist_k;   // persistent launch (see ConvDmaArgs::persist_k)
 };
 bool dense_dma_eligible(int64_t M, int64_t N, int64_t K, int64_t a_cs, int64_t b_rs, int64_t b_cs);
 rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a);

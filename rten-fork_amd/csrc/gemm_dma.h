@@ -55,12 +55,18 @@ struct DmaDesc {
   float* ws;
   int* counters;
   int n_full;               // set by launch_gemm_dma
+  // Persistent launch: persist_k resident blocks per CU (0: one block per work
+  // item), enforced with LDS padding so that every CU holds exactly that many;
+  // items are dealt out statically per XCD (see gemm_dma_kernel).
+  int persist_k;
   int bvec;                 // B copied 16 bytes per lane (dma_cfg_bvec(cfg) and pointwise:
                             // koff(k) = k * kstride, P % 4 == 0, K % BK == 0)
   int kstride;              // elements between consecutive k rows of B (bvec)
   int vec4;                 // outputs/residual row-contiguous with P % 4 == 0, unpadded:
                             // 16-byte epilogue accesses (no cin)
   int dbg;                  // tuning experiments only: 1 = no K-loop DMA, 2 = no MFMA
+  unsigned long long* stamps;  // placement experiment builds only (RTENHIP_DMA_EXPERIMENT 5):
+                               // per block {hw ids, start, end, block}; null otherwise
 };
 
 // KC split plan for one configuration (split_tiles == 0: not worth it).

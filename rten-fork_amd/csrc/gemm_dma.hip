@@ -1,763 +1,10 @@
-// f32 MFMA GEMM with LDS-DMA staging for gfx950 — the fast path of the
-// implicit-GEMM engine (see gemm_mfma.hip for the general kernel and the
-// summation-order contract it shares: KC = 256 blocks, fma chains from +0,
-// bias after block 0, src/gemm.rs:733-1050).
-//
-// Why a second kernel: v_mfma_f32_32x32x2_f32 issues at the f32 VALU rate and
-// PMC counters show it never co-executes with VALU instructions
-// (SQ_VALU_MFMA_COEXEC_CYCLES = 0), so every address/bounds instruction of a
-// register-staged im2col gather is taken straight out of MFMA time.  This
-// kernel issues NO per-element VALU work in its K loop:
-//   - A (weights) is pre-packed once into [tiles_m][tiles_k][BK][BM] tiles
-//     (zero padded), copied into LDS by buffer_load_dwordx4 ... lds;
-//   - B is gathered with buffer_load_dword ... lds where each lane's VGPR
-//     offset (its output pixel's input corner) is fixed for the whole kernel
-//     and the k-dependent part is a scalar offset from a per-k table.  This
-//     is exact for convolutions whose input needs no bounds checks: pointwise
-//     and unpadded strided convs, and padded convs whose input the graph
-//     executor materialised with its zero border.  Out-of-range n / k are
-//     pushed past the buffer's num_records and read as 0 by the hardware.
-#include <type_traits>
-
-#include "common.h"
-#include "gemm_dma.h"
-#include "fastdiv_dev.h"
-#include "vecmath.h"
+// Host side of the LDS-DMA GEMM (kernel template: gemm_dma_kernel.h; the
+// tile configurations are instantiated in gemm_dma_p*.hip): configuration
+// table, default choice, KC split plan, launch dispatch, and the A pack
+// kernel.
+#include "gemm_dma_kernel.h"
 
 namespace rtenhip {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __attribute__((address_space(3))) void lds_void_t;
-// Constant address space: uniform loads through it become s_load (SMEM,
-// lgkmcnt) instead of vector loads that would drain vmcnt and with it the
-// whole DMA pipeline.
-typedef __attribute__((address_space(4))) const int const_int_t;
-
-constexpr int DKC = 256;
-
-// Timing experiments only (separate builds, never the shipped library):
-// 1 = no DMA inside the K loop, 2 = no MFMA, 3 = 1 without the per-tile
-// barrier, 4 = 3 without the per-tile LDS reads.  Results are wrong under all.
-#ifndef RTENHIP_DMA_EXPERIMENT
-#define RTENHIP_DMA_EXPERIMENT 0
-#endif
-
-// LDS-DMA helpers (buffer_load_dword{,x4} ... lds), issued as inline asm.
-// With the compiler builtin, the waitcnt pass treats every LDS read as
-// possibly aliasing every DMA still in flight; once a wave has more DMAs
-// outstanding than it can track individually (wave tiles above 32x32: 10+ per
-// K tile) it drains the whole ring with an s_waitcnt vmcnt(0) before each
-// tile's LDS reads, exposing the full DMA latency every K tile.  As asm the
-// DMAs are invisible to that pass; the kernel orders them itself with counted
-// s_waitcnt vmcnt + s_barrier (wait_dma) and drains them before the epilogue
-// reuses the LDS.  (Loads the compiler does track stay correctly waited for:
-// vmcnt retires in issue order, so extra untracked loads only make its waits
-// stricter.)  M0 holds the wave-uniform LDS destination; one wait state
-// separates the M0 write from the DMA.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4 make_rsrc(const void* base, uint32_t num_records) {
-  const uint64_t a = (uint64_t)base;
-  return (u32x4){(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, num_records, 0x00020000u};
-}
-__device__ __forceinline__ uint32_t lds_addr(const float* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
-}
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void lds_dma16(u32x4 r, uint32_t dst, uint32_t voff, uint32_t soff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(soff)
-               : "memory", "m0");
-}
-__device__ __forceinline__ void lds_dma4(u32x4 r, uint32_t dst, uint32_t voff, uint32_t soff) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %3 offen lds"
-               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(soff)
-               : "memory", "m0");
-}
-#pragma clang diagnostic pop
-
-__device__ __forceinline__ float f4_at(const float4& v, int j) {
-  return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
-}
-
-// One block computes a BM x BN tile with WAVES_M x WAVES_N waves, each owning
-// a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA accumulators.
-template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES,
-          bool MULTI_KB, bool BVEC>
-__global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles_m, int tiles_n) {
-  static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
-  constexpr int NW = NT / 64;
-  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
-  constexpr int MI = WM / 32, NI = WN / 32;
-  // A tile copy: dwordx4 per lane when there is enough data for every wave,
-  // else dword.
-  constexpr int A_LB = BM * BK * 4 >= NT * 16 ? 16 : 4;  // bytes per lane
-  constexpr int A_CHUNK = 64 * A_LB;                     // bytes per wave-instruction
-  constexpr int A_INSTR = BM * BK * 4 / A_CHUNK;
-  // B tile copy: dword per lane (one k row of 64 columns per instruction), or
-  // with BVEC dwordx4 (4 k rows x 64 columns per instruction; pointwise convs
-  // whose 4-pixel groups are contiguous and whose k stride is linear).
-  constexpr int B_INSTR = BVEC ? BK * BN / 256 : BK * (BN / 64);
-  constexpr int A_PER_W = A_INSTR / NW;
-  constexpr int B_PER_W = B_INSTR / NW;
-  constexpr int STAGE = (BM + BN) * BK;      // floats per stage
-  constexpr int KSTEPS = BK / 2;
-  static_assert(WAVES_M * WAVES_N == NW, "wave grid");
-  static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "even DMA split");
-  static_assert(BN % 64 == 0 && DKC % BK == 0 && BK <= DMA_KTAB_PAD, "tile shape");
-  static_assert(MI >= 1 && NI >= 1, "wave tile");
-  static_assert(!BVEC || (NI == 1 && BN == 64 && BK % 4 == 0),
-                "BVEC needs the identity B column layout and 64-column rows");
-
-  __shared__ float lds[STAGES * STAGE];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (wave / WAVES_N) * WM;
-  const int wn = (wave % WAVES_N) * WN;
-
-  // Blocks [0, n_full) each own a whole tile (XCD-aware bijective remap, see
-  // gemm_mfma.hip).  With a KC split (d.split_tiles > 0) the remaining tiles
-  // -- the ones that would leave CUs idle in a last partial round -- are cut
-  // at the reference's KC = 256 boundaries: block n_full + t*nkb + kb computes
-  // only K block kb of split tile t and the last of the nkb blocks to finish
-  // folds them in order (see below).
-  const int bid = blockIdx.x;
-  const int n_full = d.n_full;
-  int wg, kb_split = -1, split_idx = -1;
-  if (bid < n_full) {
-    const int nwg = n_full;
-    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-    wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  } else {
-    const int u = bid - n_full;
-    split_idx = u / d.nkb;
-    kb_split = u - split_idx * d.nkb;
-    wg = n_full + split_idx;
-  }
-  const int tmi = wg % tiles_m;
-  const int tm = tmi * BM;
-  const int tn = (wg / tiles_m) * BN;
-  const int M = d.M, N = d.N, K = d.K;
-  const int tiles_k = (K + BK - 1) / BK;
-  constexpr int TPB = DKC / BK;  // K tiles per KC block
-  const int kt_lo = kb_split >= 0 ? kb_split * TPB : 0;
-  const int kt_hi = kb_split >= 0 ? min(tiles_k, kt_lo + TPB) : tiles_k;
-
-  const u32x4 ra = make_rsrc(d.apk, 0x7fffffffu);
-  const u32x4 rb = make_rsrc(d.x, d.x_bytes);
-
-  // Per-lane B offsets: one per 64-column group this wave loads.
-  constexpr int NG = BN / 64;
-  uint32_t vb[NG];
-#pragma unroll
-  for (int g = 0; g < NG; g++) {
-    // LDS position p of a B row holds column wn' + ni*32 + l where p = wn' + l*NI + ni,
-    // so a lane's NI B values for one k are adjacent (one ds_read).
-    const int pos = g * 64 + lane;
-    const int q = pos % WN;
-    const int n = tn + (pos - q) + (q % NI) * 32 + q / NI;
-    uint32_t off = DMA_OOB;
-    if (n < N) {
-      const int img = fdiv(n, d.fdP);
-      const int p = n - img * d.P;
-      const int oy = fdiv(p, d.fdOW);
-      const int ox = p - oy * d.OW;
-      off = (uint32_t)(((int64_t)img * d.x_img + (int64_t)oy * d.ystride + (int64_t)ox * d.xstride) * 4);
-    }
-    vb[g] = off;
-  }
-  // BVEC: instruction i of this wave covers k rows 4*(wave*B_PER_W+i) .. +3 of
-  // the tile; lane -> row (lane >> 4), columns 4*(lane & 15) .. +3.
-  uint32_t vb4[BVEC ? B_PER_W : 1];
-  if constexpr (BVEC) {
-#pragma unroll
-    for (int i = 0; i < B_PER_W; i++) {
-      const int gi = wave * B_PER_W + i;
-      const int kk = gi * 4 + (lane >> 4);
-      const int n = tn + (lane & 15) * 4;
-      uint32_t off = DMA_OOB;
-      if (n < N) {
-        const int img = fdiv(n, d.fdP);
-        const int p = n - img * d.P;
-        off = (uint32_t)(((int64_t)img * d.x_img + p) * 4 + (int64_t)kk * d.kstride * 4);
-      }
-      vb4[i] = off;
-    }
-  }
-  const uint32_t va = (uint32_t)(wave * A_PER_W * A_CHUNK + lane * A_LB);
-  const uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
-  const_int_t* ktab4 = (const_int_t*)d.ktab4;
-  const uint32_t lds0 = lds_addr(lds);
-
-  // K-table offsets of the tile about to be issued, loaded at the start of
-  // the tile body that issues it, so the scalar load's latency hides under
-  // that body's first MFMAs.
-  constexpr int KPRE = BVEC ? 1 : B_PER_W;
-  uint32_t kpre[KPRE];
-  auto load_k = [&](int kt) __attribute__((always_inline)) {
-    if constexpr (!BVEC) {
-      kt = min(kt, tiles_k - 1);
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) kpre[i] = (uint32_t)ktab4[kt * BK + (wave * B_PER_W + i) / NG];
-    }
-  };
-
-  // An empty asm reading the prefetched offsets, placed after the MFMAs:
-  // keeps the load from being sunk into the conditional issue block.
-  auto pin_k = [&]() __attribute__((always_inline)) {
-    if constexpr (!BVEC) {
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) asm volatile("" ::"s"(kpre[i]));
-    }
-  };
-
-  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
-    const uint32_t As = lds0 + (uint32_t)(stage * STAGE * 4);
-    const uint32_t Bs = As + BM * BK * 4;
-    const uint32_t a_soff = a_row_base + (uint32_t)kt * (BM * BK * 4);
-#pragma unroll
-    for (int i = 0; i < A_PER_W; i++) {
-      const uint32_t dst = As + (uint32_t)((wave * A_PER_W + i) * A_CHUNK);
-      if constexpr (A_LB == 16)
-        lds_dma16(ra, dst, va + i * A_CHUNK, a_soff);
-      else
-        lds_dma4(ra, dst, va + i * A_CHUNK, a_soff);
-    }
-    if constexpr (BVEC) {
-      const uint32_t b_soff = (uint32_t)kt * (uint32_t)(BK * d.kstride * 4);
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) {
-        const int gi = wave * B_PER_W + i;  // rows 4*gi .. 4*gi+3: 1 KB of LDS
-        lds_dma16(rb, Bs + gi * 1024, vb4[i], b_soff);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) {
-        const int gi = wave * B_PER_W + i;  // wave-uniform
-        const int kl = gi / NG, g = gi % NG;
-        lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[i]);
-      }
-    }
-  };
-
-  f32x16 acc[MI][NI];
-#pragma unroll
-  for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-    for (int ni = 0; ni < NI; ni++) acc[mi][ni] = (f32x16){0};
-
-  const int half = lane >> 5;
-  const int l32 = lane & 31;
-  const int m_lim = M - 1 - tm;
-  const int n_lim = N - 1 - tn;
-  auto lrow = [&](int mi, int j) __attribute__((always_inline)) { return wm + mi * 32 + (j & 3) + 8 * (j >> 2) + 4 * half; };
-
-  // Bias of accumulator row j: when the wave's 32-row group is inside M and
-  // 16-byte aligned, the 16 rows a lane needs (4 runs of 4) come from 4
-  // float4 loads instead of 16 scalar ones.
-  constexpr bool BIAS_VEC = MI == 1;  // keeps the 16 extra registers off 64-row waves
-  float4 bias4[MI][4];
-  bool bias_vec[MI];
-#pragma unroll
-  for (int mi = 0; mi < MI; mi++) {
-    const int r0 = tm + wm + mi * 32;
-    bias_vec[mi] = BIAS_VEC && d.bias && r0 + 31 < M && ((uintptr_t)(d.bias + r0) % 16) == 0;
-  }
-  auto load_bias = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++)
-      if (bias_vec[mi]) {
-#pragma unroll
-        for (int q4 = 0; q4 < 4; q4++)
-          bias4[mi][q4] = *(const float4*)(d.bias + tm + wm + mi * 32 + 8 * q4 + 4 * half);
-      }
-  };
-  auto bias_row = [&](int mi, int j, int ml) __attribute__((always_inline)) {
-    if (bias_vec[mi]) {
-      const float4 b = bias4[mi][j >> 2];
-      const int e = j & 3;
-      return e == 0 ? b.x : e == 1 ? b.y : e == 2 ? b.z : b.w;
-    }
-    return d.bias[tm + ml];
-  };
-
-  // End of K block 0: v = alpha*acc (+ beta*C) + bias (gemm.rs:1004-1050).
-  auto first_block = [&](f32x16& v, const f32x16& a, int mi, int ni) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const int ml = min(lrow(mi, j), m_lim);
-      float x;
-      if (d.cin) {
-        const int nl = min(wn + ni * 32 + l32, n_lim);
-        const float c = d.cin[(int64_t)(tm + ml) * d.out_c + tn + nl];
-        x = __fmaf_rn(a[j], d.alpha, __fmul_rn(c, d.beta));
-      } else {
-        x = d.alpha == 1.f ? a[j] : __fmul_rn(a[j], d.alpha);  // x * 1 == x exactly
-      }
-      if (d.bias) x = __fadd_rn(x, bias_row(mi, j, ml));
-      v[j] = x;
-    }
-  };
-
-  // LDS read offsets of this lane (floats, relative to a stage): its MI A
-  // values and NI B values of one k row are contiguous (see pack_a_kernel and
-  // the B column permutation above).
-  // A tiles are packed k-quad major (see pack_a_kernel): a lane's A values of
-  // 4 consecutive k steps (k = 2*(4*sq + j) + half, j = 0..3) are one float4,
-  // so each 32-row group costs one ds_read_b128 per 4 MFMA steps.
-  const int a_lane = (half * BM + wm + l32) * 4;
-  const int b_lane = BM * BK + half * BN + wn + l32 * NI;
-
-  // Software pipeline over K tiles.  A tile's operands are read from LDS
-  // into one of two register sets in a single burst; the next tile's burst is
-  // issued before the last two MFMA steps of the current one, so LDS latency
-  // hides behind MFMAs.  As soon as every wave holds its operands of tile kt
-  // (barrier), tile kt's stage is refilled with tile kt+STAGES.  Waits are
-  // counted and the barrier is a raw s_barrier, so later tiles' DMAs stay in
-  // flight across it (__syncthreads would drain vmcnt).
-  constexpr int PER_TILE = A_PER_W + B_PER_W;
-  static_assert(KSTEPS % 4 == 0, "A k-quads");
-  typedef float vb_t __attribute__((ext_vector_type(NI)));
-  float4 av[2][KSTEPS / 4][MI];
-  vb_t bv[2][KSTEPS];
-
-  auto wait_dma = [&](int allowed_tiles) __attribute__((always_inline)) {
-    if (STAGES >= 4 && allowed_tiles >= 3) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * 3) : "memory");
-    } else if (STAGES >= 3 && allowed_tiles >= 2) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * 2) : "memory");
-    } else if (allowed_tiles >= 1) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  };
-  auto read_tile = [&](auto set_tag, int stage) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_tag)::value;
-    if constexpr (RTENHIP_DMA_EXPERIMENT == 4) {
-      if (stage != 0) return;  // keep only the prologue's read
-    }
-    const float* As = lds + stage * STAGE + a_lane;
-    const float* Bs = lds + stage * STAGE + b_lane;
-#pragma unroll
-    for (int s = 0; s < KSTEPS; s++) {
-      if (s % 4 == 0) {
-#pragma unroll
-        for (int mi = 0; mi < MI; mi++) av[SET][s / 4][mi] = *(const float4*)(As + (s / 2 * BM + mi * 32) * 4);
-      }
-      bv[SET][s] = *(const vb_t*)(Bs + 2 * s * BN);
-    }
-  };
-  auto mfma_steps = [&](auto set_tag, auto s0_tag, auto s1_tag) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_tag)::value;
-    if constexpr (RTENHIP_DMA_EXPERIMENT == 2) return;
-#pragma unroll
-    for (int s = decltype(s0_tag)::value; s < decltype(s1_tag)::value; s++)
-#pragma unroll
-      for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-        for (int ni = 0; ni < NI; ni++)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4_at(av[SET][s / 4][mi], s % 4), bv[SET][s][ni],
-                                                             acc[mi][ni], 0, 0, 0);
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-#ifndef RTENHIP_DMA_TAIL
-#define RTENHIP_DMA_TAIL 2
-#endif
-  constexpr int TAIL = KSTEPS >= 2 * RTENHIP_DMA_TAIL ? RTENHIP_DMA_TAIL : (KSTEPS >= 4 ? 2 : 1);
-  using IMid = std::integral_constant<int, KSTEPS - TAIL>;
-  using IEnd = std::integral_constant<int, KSTEPS>;
-
-  int stage = 0;  // stage holding tile kt
-  auto body = [&](auto set_tag, int kt) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_tag)::value;
-    load_k(kt + STAGES);  // unconditional (clamped): no phi, so no early wait
-    __builtin_amdgcn_sched_barrier(0);  // keep the scalar load ahead of the MFMAs
-    mfma_steps(set_tag, I0{}, IMid{});
-    pin_k();
-    if (kt + 1 < kt_hi) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_dma(min(STAGES - 2, kt_hi - kt - 2));
-      if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
-      if (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2)
-        if (kt + STAGES < kt_hi) issue(stage, kt + STAGES);
-      stage = stage + 1 == STAGES ? 0 : stage + 1;
-      read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
-    }
-    mfma_steps(set_tag, IMid{}, IEnd{});
-  };
-  // Steady state (STAGES = 2 or 4, whose ring period divides both the
-  // register-set period 2 and the KC block): a group of STAGES tiles with
-  // compile-time stage and register-set indices, fixed DMA wait counts and
-  // no bounds tests -- LDS addresses become immediates and the per-tile
-  // scalar/vector bookkeeping disappears.  Valid while every tile of the
-  // group still has a refill to issue (kt + STAGES - 1 + STAGES < kt_hi).
-  constexpr bool FAST = STAGES == 2 || STAGES == 4;
-  auto body_fast = [&](auto set_tag, auto stg_tag, int kt) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_tag)::value;
-    constexpr int STG = decltype(stg_tag)::value;
-    load_k(kt + STAGES);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_steps(set_tag, I0{}, IMid{});
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
-    if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
-    if constexpr (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2) issue(STG, kt + STAGES);
-    read_tile(std::integral_constant<int, SET ^ 1>{}, (STG + 1) % STAGES);
-    mfma_steps(set_tag, IMid{}, IEnd{});
-  };
-  // Tiles [kt0, kt1) with kt0 even (register set = tile parity) and
-  // (kt0 - kt_lo) % STAGES == 0 (stage of tile kt0 is 0).
-  auto run = [&](int kt0, int kt1) __attribute__((always_inline)) {
-    int kt = kt0;
-    if constexpr (FAST) {
-      for (; kt + STAGES <= kt1 && kt + 2 * STAGES - 1 < kt_hi; kt += STAGES) {
-        body_fast(I0{}, std::integral_constant<int, 0>{}, kt);
-        body_fast(I1{}, std::integral_constant<int, 1>{}, kt + 1);
-        if constexpr (STAGES == 4) {
-          body_fast(I0{}, std::integral_constant<int, 2>{}, kt + 2);
-          body_fast(I1{}, std::integral_constant<int, 3>{}, kt + 3);
-        }
-      }
-    }
-    for (; kt < kt1; kt += 2) {
-      body(I0{}, kt);
-      if (kt + 1 < kt1) body(I1{}, kt + 1);
-    }
-  };
-
-  // Vectorised epilogue geometry (see the epilogue) and, for small wave
-  // tiles, the residual prefetched now so its latency hides under the K loop
-  // (it does not depend on the GEMM).
-  constexpr bool VEC_FITS = NW * 1024 <= STAGES * STAGE;
-  constexpr bool RES_PRE = VEC_FITS && MI * NI == 1 && BK == 16;
-  const int rr = lane >> 3;        // row within an 8-row group
-  const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
-  float4 rpre[RES_PRE ? MI : 1][RES_PRE ? NI : 1][4];
-  if constexpr (RES_PRE) {
-    if (d.vec4 && d.residual) {
-#pragma unroll
-      for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-        for (int ni = 0; ni < NI; ni++) {
-          const int n = tn + wn + ni * 32 + c4;
-          const bool ncol_ok = n <= N - 1;
-          const int nn = ncol_ok ? n : 0;
-          const int img = fdiv(nn, d.fdP);
-          const int64_t rbase = (int64_t)img * d.res_img + (nn - img * d.P);
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int m = tm + wm + mi * 32 + i * 8 + rr;
-            rpre[mi][ni][i] = (ncol_ok && m < M)
-                                  ? *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-        }
-    }
-  }
-
-  load_bias();
-
-  // Prologue: fill every stage, wait for the first tile, read it.
-#pragma unroll
-  for (int s = 0; s < STAGES; s++)
-    if (kt_lo + s < kt_hi) {
-      load_k(kt_lo + s);
-      issue(s, kt_lo + s);
-    }
-  wait_dma(min(STAGES, kt_hi - kt_lo) - 1);
-  __builtin_amdgcn_s_barrier();
-  read_tile(I0{}, 0);
-
-  f32x16 sum[MULTI_KB ? MI : 1][MULTI_KB ? NI : 1];
-  if constexpr (!MULTI_KB) {
-    run(0, tiles_k);
-  } else if (kb_split >= 0) {
-    // One KC block of a split tile: its chain goes to the workspace; the
-    // last of the tile's nkb blocks to arrive folds all chains in K order
-    // exactly as the whole-tile path does, then runs the epilogue.
-    run(kt_lo, kt_hi);
-    // Hand-off without L2 write-back fences (MI355X guide, Guideline 16 /
-    // "Valid forms" row 1): chains are stored write-through (sc1, as 8-byte
-    // agent-scope atomic stores), every storing wave drains (vmcnt(0)) before
-    // the workgroup barrier, one lane adds to the tile's counter (agent scope)
-    // and the workgroup whose add returns nkb-1 reads the chains with sc1
-    // loads only.
-    constexpr int CH = MI * NI * 16 * NT;  // floats per chain (whole block)
-    // 8-byte granules, stored and loaded as agent-scope relaxed atomics
-    // (global_store/load_dwordx2 sc1).  Layout per chain: [(mi*NI+ni)*8 + jp][tid].
-    // (__float_as_uint, not __builtin_bit_cast: clang 22 folds a bit_cast of
-    // an ext_vector element to element 0.)
-    unsigned long long* wsq =
-        reinterpret_cast<unsigned long long*>(d.ws + (int64_t)split_idx * d.nkb * CH);
-    auto qidx = [&](int kb, int mi, int ni, int jp) {
-      return ((int64_t)kb * (CH / 2)) + (((mi * NI + ni) * 8 + jp) * NT + tid);
-    };
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-      for (int ni = 0; ni < NI; ni++)
-#pragma unroll
-        for (int jp = 0; jp < 8; jp++) {
-          const unsigned long long q =
-              (unsigned long long)__float_as_uint(acc[mi][ni][2 * jp]) |
-              ((unsigned long long)__float_as_uint(acc[mi][ni][2 * jp + 1]) << 32);
-          __hip_atomic_store(wsq + qidx(kb_split, mi, ni, jp), q, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        }
-    __shared__ int last_arrival;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      const int prev = __hip_atomic_fetch_add(d.counters + split_idx, 1, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-      last_arrival = prev == d.nkb - 1;
-    }
-    __syncthreads();
-    if (!last_arrival) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
-    auto ldq = [&](int kb, int mi, int ni, int jp) {
-      return __hip_atomic_load(wsq + qidx(kb, mi, ni, jp), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    };
-    auto lo = [](unsigned long long q) { return __uint_as_float((unsigned)(q & 0xffffffffu)); };
-    auto hi = [](unsigned long long q) { return __uint_as_float((unsigned)(q >> 32)); };
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-      for (int ni = 0; ni < NI; ni++) {
-        f32x16 c;
-#pragma unroll
-        for (int jp = 0; jp < 8; jp++) {
-          const unsigned long long q = ldq(0, mi, ni, jp);
-          c[2 * jp] = lo(q);
-          c[2 * jp + 1] = hi(q);
-        }
-        first_block(sum[mi][ni], c, mi, ni);
-      }
-    // Remaining chains in K order; loads of a group of blocks are issued
-    // together so the fold is not latency-bound.
-    constexpr int G = MI * NI == 1 ? 2 : 1;
-    for (int kb0 = 1; kb0 < d.nkb; kb0 += G) {
-      f32x16 cg[G][MI][NI];
-#pragma unroll
-      for (int gi = 0; gi < G; gi++) {
-        if (kb0 + gi >= d.nkb) break;
-#pragma unroll
-        for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-          for (int ni = 0; ni < NI; ni++)
-#pragma unroll
-            for (int jp = 0; jp < 8; jp++) {
-              const unsigned long long q = ldq(kb0 + gi, mi, ni, jp);
-              cg[gi][mi][ni][2 * jp] = lo(q);
-              cg[gi][mi][ni][2 * jp + 1] = hi(q);
-            }
-      }
-#pragma unroll
-      for (int gi = 0; gi < G; gi++) {
-        if (kb0 + gi >= d.nkb) break;
-#pragma unroll
-        for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-          for (int ni = 0; ni < NI; ni++)
-#pragma unroll
-            for (int j = 0; j < 16; j++)
-              sum[mi][ni][j] = __fmaf_rn(cg[gi][mi][ni][j], d.alpha, sum[mi][ni][j]);
-      }
-    }
-    if (tid == 0)
-      __hip_atomic_store(d.counters + split_idx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    // K > DKC: block 0 is peeled so the bias/beta fold sits outside the loop.
-    static_assert(TPB % 2 == 0, "register-set parity across K blocks");
-    run(0, TPB);
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-      for (int ni = 0; ni < NI; ni++) {
-        first_block(sum[mi][ni], acc[mi][ni], mi, ni);
-        acc[mi][ni] = (f32x16){0};
-      }
-    for (int kt = TPB; kt < tiles_k; kt += TPB) {
-      run(kt, min(kt + TPB, tiles_k));
-#pragma unroll
-      for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-        for (int ni = 0; ni < NI; ni++) {
-#pragma unroll
-          for (int j = 0; j < 16; j++) sum[mi][ni][j] = __fmaf_rn(acc[mi][ni][j], d.alpha, sum[mi][ni][j]);
-          acc[mi][ni] = (f32x16){0};
-        }
-    }
-  }
-
-  // ---- epilogue ----
-  auto apply_act = [&](float x) __attribute__((always_inline)) {
-    if (d.act == RTENHIP_ACT_RELU) {
-      x = fmaxf(x, 0.f);
-    } else if (d.act == RTENHIP_ACT_CLIP) {
-      x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
-    } else if (d.act == RTENHIP_ACT_GELU) {
-      x = vm_gelu(x);
-    }
-    return x;
-  };
-  if (VEC_FITS && d.vec4) {
-    // Row-contiguous outputs (P % 4 == 0, unpadded): each 32x32 accumulator
-    // block is transposed through this wave's LDS slot so every lane stores
-    // (and loads the residual as) 16-byte row segments: 4 dwordx4 per block
-    // instead of 16 dword accesses.  Same per-element arithmetic as below.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land in the slots
-    __syncthreads();  // every wave is done reading the K stages
-    float* slot = lds + wave * 1024;
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-      for (int ni = 0; ni < NI; ni++) {
-        f32x16 v;
-        if constexpr (MULTI_KB) {
-          v = sum[mi][ni];
-        } else {
-          first_block(v, acc[mi][ni], mi, ni);
-        }
-#pragma unroll
-        for (int j = 0; j < 16; j++) slot[((j & 3) + 8 * (j >> 2) + 4 * half) * 32 + l32] = v[j];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const int n = tn + wn + ni * 32 + c4;
-        const bool ncol_ok = n <= N - 1;  // N % 4 == 0: the whole segment is in range
-        const int nn = ncol_ok ? n : 0;
-        const int img = fdiv(nn, d.fdP);
-        const int p = nn - img * d.P;
-        const int64_t obase = (int64_t)img * d.out_img + p;
-        const int64_t rbase = (int64_t)img * d.res_img + p;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-          const int row = i * 8 + rr;
-          const int m = tm + wm + mi * 32 + row;
-          const bool ok = ncol_ok && m < M;
-          float4 x = *(const float4*)(slot + row * 32 + c4);
-          if (d.colbias && ok) {
-            const float4 cb = *(const float4*)(d.colbias + p);
-            x.x = __fadd_rn(x.x, cb.x);
-            x.y = __fadd_rn(x.y, cb.y);
-            x.z = __fadd_rn(x.z, cb.z);
-            x.w = __fadd_rn(x.w, cb.w);
-          }
-          if (d.residual && ok) {
-            float4 r;
-            if constexpr (RES_PRE)
-              r = rpre[mi][ni][i];
-            else
-              r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
-            x.x = __fadd_rn(x.x, r.x);
-            x.y = __fadd_rn(x.y, r.y);
-            x.z = __fadd_rn(x.z, r.z);
-            x.w = __fadd_rn(x.w, r.w);
-          }
-          x.x = apply_act(x.x);
-          x.y = apply_act(x.y);
-          x.z = apply_act(x.z);
-          x.w = apply_act(x.w);
-          if (ok) *(float4*)(d.out + obase + (int64_t)m * d.out_c) = x;
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      }
-    return;
-  }
-  const bool full_tile = m_lim >= BM - 1 && n_lim >= BN - 1;
-#pragma unroll
-  for (int ni = 0; ni < NI; ni++) {
-    const int nl = wn + ni * 32 + l32;
-    const bool ncol_ok = nl <= n_lim;
-    const int n = tn + min(nl, n_lim);
-    const int img = fdiv(n, d.fdP);
-    const int p = n - img * d.P;
-    const int oy = fdiv(p, d.fdOW);
-    const int ox = p - oy * d.OW;
-    const int64_t obase = (int64_t)img * d.out_img + (int64_t)oy * d.out_row + ox + d.out_off;
-    const int64_t rbase = (int64_t)img * d.res_img + p;
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++) {
-      f32x16 v;
-      if constexpr (MULTI_KB) {
-        v = sum[mi][ni];
-      } else {
-        first_block(v, acc[mi][ni], mi, ni);
-      }
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const int ml = lrow(mi, j);
-        const bool ok = full_tile || (ncol_ok && ml <= m_lim);
-        float x = v[j];
-        if (d.colbias) x = __fadd_rn(x, d.colbias[p]);
-        if (d.residual) x = __fadd_rn(x, d.residual[ok ? rbase + (int64_t)(tm + ml) * d.res_c : 0]);
-        x = apply_act(x);
-        if (ok) d.out[obase + (int64_t)(tm + ml) * d.out_c] = x;
-      }
-    }
-  }
-}
-
-// Whether a configuration has a BVEC (16-byte B copy) variant.
-template <int NT, int BM, int BN, int BK, int WM_, int WN_>
-constexpr bool dma_bvec_ok() {
-  return BN == 64 && BN / WN_ == 32 && (BK * BN / 256) % (NT / 64) == 0 && BK % 4 == 0;
-}
-
-template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES>
-static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
-  const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
-  dim3 grid(d.n_full + d.split_tiles * d.nkb), block(NT);
-  if constexpr (dma_bvec_ok<NT, BM, BN, BK, WM_, WN_>()) {
-    if (d.bvec) {
-      if (d.K > DKC)
-        hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true, true>),
-                           grid, block, 0, s, d, tiles_m, tiles_n);
-      else
-        hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false, true>),
-                           grid, block, 0, s, d, tiles_m, tiles_n);
-      return;
-    }
-  }
-  if (d.K > DKC)
-    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true, false>),
-                       grid, block, 0, s, d, tiles_m, tiles_n);
-  else
-    hipLaunchKernelGGL((gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false, false>),
-                       grid, block, 0, s, d, tiles_m, tiles_n);
-}
-
-// DMA tile configurations:
-//   X(id, threads, BM, BN, BK, WAVES_M, WAVES_N, min waves/SIMD, stages)
-// The wave tile is (BM/WAVES_M) x (BN/WAVES_N).  All configurations produce
-// bit-identical results (same KC-block summation order), so the choice is
-// purely a performance one: dma_default_cfg below, or plan-time tuning.
-#ifndef RTENHIP_DMA_CONFIGS  // (overridable for ISA inspection builds of one config)
-#define RTENHIP_DMA_CONFIGS(X)          \
-  X(0, 512, 128, 128, 16, 4, 2, 2, 3)   \
-  X(1, 256, 128, 128, 16, 2, 2, 2, 3)   \
-  X(2, 256, 64, 256, 16, 1, 4, 2, 3)    \
-  X(3, 128, 128, 64, 16, 2, 1, 2, 3)    \
-  X(4, 128, 64, 128, 16, 1, 2, 2, 3)    \
-  X(5, 64, 64, 64, 16, 1, 1, 2, 3)      \
-  X(6, 512, 256, 128, 16, 4, 2, 2, 3)   \
-  X(7, 256, 64, 64, 16, 2, 2, 4, 3)     \
-  X(8, 128, 64, 64, 16, 2, 1, 2, 3)     \
-  X(9, 256, 128, 64, 16, 4, 1, 2, 3)    \
-  X(10, 256, 64, 128, 16, 2, 2, 2, 3)   \
-  X(11, 512, 128, 128, 16, 4, 2, 2, 4)  \
-  X(12, 256, 128, 128, 16, 2, 2, 2, 4)  \
-  X(13, 256, 64, 64, 32, 2, 2, 3, 2)    \
-  X(14, 256, 64, 64, 16, 2, 2, 4, 4)    \
-  X(15, 512, 128, 64, 16, 4, 2, 4, 3)   \
-  X(16, 512, 64, 128, 16, 2, 4, 4, 3)   \
-  X(17, 128, 32, 64, 16, 1, 2, 4, 3)    \
-  X(18, 1024, 128, 128, 16, 4, 4, 4, 3)
-#endif
 
 struct DmaCfgInfo {
   int nt, bm, bn, bk, waves_m, waves_n;
@@ -770,6 +17,8 @@ static const DmaCfgInfo kDmaCfgs[] = {
 constexpr int kNumDmaCfgs = sizeof(kDmaCfgs) / sizeof(kDmaCfgs[0]);
 static int g_dma_cfg = -1;
 static int g_dma_dbg = 0;
+static unsigned long long* g_dma_stamps = nullptr;
+static int g_dma_persist = -1;  // debug override of DmaDesc::persist_k (-1: none)
 
 int dma_num_cfgs() { return kNumDmaCfgs; }
 
@@ -829,6 +78,8 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
     return fail(RTENHIP_INVALID_VALUE, "A packed for another tile shape");
   DmaDesc dd = d;
   dd.dbg = g_dma_dbg;
+  dd.stamps = g_dma_stamps;
+  if (g_dma_persist >= 0) dd.persist_k = g_dma_persist;
   const DmaCfgInfo& ci = kDmaCfgs[cfg];
   const int tiles = ((d.M + ci.bm - 1) / ci.bm) * ((d.N + ci.bn - 1) / ci.bn);
   if (d.split_tiles > 0) {
@@ -839,16 +90,14 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
   } else {
     dd.n_full = tiles;
   }
-  switch (cfg) {
-#define RTENHIP_DMA_CASE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) \
-  case id:                                                    \
-    launch_dma_cfg<NT, BM, BN, BK, WMW, WNW, MINW, ST>(dd, s); \
-    break;
-    RTENHIP_DMA_CONFIGS(RTENHIP_DMA_CASE)
-#undef RTENHIP_DMA_CASE
-    default:
-      return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
+  bool launched = false;
+  switch (cfg % DMA_PARTS) {
+    case 0: launched = dma_launch_part<0>(cfg, dd, s); break;
+    case 1: launched = dma_launch_part<1>(cfg, dd, s); break;
+    case 2: launched = dma_launch_part<2>(cfg, dd, s); break;
+    default: launched = dma_launch_part<3>(cfg, dd, s); break;
   }
+  if (!launched) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }
@@ -857,6 +106,11 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
 
 extern "C" void rtenhip_debug_set_dma_config(int cfg) { rtenhip::g_dma_cfg = cfg; }
 extern "C" void rtenhip_debug_set_dma_mode(int mode) { rtenhip::g_dma_dbg = mode; }
+// Placement experiment builds only: device buffer of 4 u64 per block.
+extern "C" void rtenhip_debug_set_dma_persist(int k) { rtenhip::g_dma_persist = k; }
+extern "C" void rtenhip_debug_set_dma_stamps(void* buf) {
+  rtenhip::g_dma_stamps = static_cast<unsigned long long*>(buf);
+}
 
 namespace rtenhip {
 

@@ -1,0 +1,7 @@
+// Part 0 of the LDS-DMA GEMM's tile configurations (cfg % DMA_PARTS == 0),
+// compiled on its own so the configurations build in parallel.
+#include "gemm_dma_kernel.h"
+
+namespace rtenhip {
+template bool dma_launch_part<0>(int, const DmaDesc&, hipStream_t);
+}  // namespace rtenhip

@@ -1119,6 +1119,14 @@ rtenhip_status Graph::exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_
   return RTENHIP_OK;
 }
 
+// DMA GEMM launch modes the first-run tuner times: one block per work item
+// (0) or persistent with 3 to 6 resident blocks per CU (see gemm_dma_kernel.h).
+static const int kPersistModes[5] = {0, 3, 4, 5, 6};
+static const char* pers_tag(int k) {
+  static const char* tags[] = {"", " pers1", " pers2", " pers3", " pers4", " pers5", " pers6"};
+  return k >= 0 && k <= 6 ? tags[k] : " pers?";
+}
+
 // Dense DMA MatMul.  A is packed per run into the plan's shared buffer; on the
 // plan's first (eager) run the tile configuration and KC split are chosen by
 // timing the candidates on the real operands (all bit-identical).
@@ -1185,6 +1193,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     da.counters = e.counters;
     da.cnt_cap = e.n_counters;
     da.pk = p.mm_pack;
+    da.persist_k = e.persist;
   };
   if (me.cfg < 0) {
     int chosen = dma_default_cfg((int)me.M, (int)me.N, (int)me.K);
@@ -1198,11 +1207,16 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       if (kv.first != op_id && kv.second.cfg >= 0 && nodes[kv.first].inputs[0] == n.inputs[0] &&
           kv.second.M == me.M && kv.second.N == me.N && kv.second.K == me.K)
         twin = &kv.second;
+    int chosen_persist = 0;
     if (twin) {
       chosen = twin->cfg;
       chosen_split = twin->split;
+      chosen_persist = twin->persist;
     } else if (autotune && cs == hipStreamCaptureStatusNone && da.residual != da.out) {
-      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18};
+      // Candidates are timed alone: a side-stream branch still running would
+      // share the CUs and skew the choice.
+      RTENHIP_HIP_CHECK(hipDeviceSynchronize());
+      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
@@ -1215,8 +1229,12 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
         if (cfg >= dma_num_cfgs()) continue;
         rtenhip_status st = ensure_pack(cfg);
         if (st) return st;
-        for (int split = 0; split < 2; split++) {
+        for (int mode = 0; mode < 10; mode++) {
+          const int split = mode & 1;
           if (split && dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg).split_tiles == 0) continue;
+          // persistent launches with 2, 3 or 4 blocks per CU, or none
+          trial.persist = kPersistModes[mode >> 1];
+          if (persist_mode >= 0 && trial.persist != persist_mode) continue;
           st = set_split(trial, cfg, split != 0);
           if (st) return st;
           bind(trial, cfg);
@@ -1237,6 +1255,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
             best_ms = ms;
             chosen = cfg;
             chosen_split = split != 0;
+            chosen_persist = trial.persist;
           }
         }
       }
@@ -1251,6 +1270,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     st = set_split(me, chosen, chosen_split);
     if (st) return st;
     me.cfg = chosen;
+    me.persist = persist_mode >= 0 ? persist_mode : chosen_persist;
     p.mm_pack_value = -1;  // tuning overwrote the buffer
   }
   bind(me, me.cfg);
@@ -1353,14 +1373,19 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     a.ws_cap = e.ws_floats;
     a.counters = e.counters;
     a.cnt_cap = e.n_counters;
+    a.persist_k = e.persist;
   };
   if (ce.cfg < 0) {
     int chosen = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
     bool chosen_split = false;
+    int chosen_persist = 0;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
     if (autotune && cs == hipStreamCaptureStatusNone) {
-      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10};
+      // Candidates are timed alone: a side-stream branch still running would
+      // share the CUs and skew the choice.
+      RTENHIP_HIP_CHECK(hipDeviceSynchronize());
+      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19, 20, 21};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
@@ -1374,9 +1399,12 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         bufs.push_back(pk);
         rtenhip_status st = pack_conv_weights(ctx, w, g, cfg, pk);
         if (st) return st;
-        for (int split = 0; split < 2; split++) {
+        for (int mode = 0; mode < 10; mode++) {
+          const int split = mode & 1;
           if (split && dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg).split_tiles == 0)
             continue;
+          trial.persist = kPersistModes[mode >> 1];
+          if (persist_mode >= 0 && trial.persist != persist_mode) continue;
           st = set_split(trial, cfg, split != 0);
           if (st) return st;
           bind(trial);
@@ -1400,6 +1428,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
             best_ms = ms;
             chosen = cfg;
             chosen_split = split != 0;
+            chosen_persist = trial.persist;
           }
         }
       }
@@ -1416,6 +1445,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     st = set_split(ce, chosen, chosen_split);
     if (st) return st;
     ce.cfg = chosen;
+    ce.persist = persist_mode >= 0 ? persist_mode : chosen_persist;
   }
   a.packed_w = ce.packed;
   a.cfg = ce.cfg;
@@ -1675,9 +1705,29 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (it != plan->slots.end())
           for (size_t d = 0; d < it->second.shape.size(); d++)
             shp += (d ? "x" : "") + std::to_string(it->second.shape[d]);
-        snprintf(buf, sizeof buf, "op %-28s %-12s %-20s %9.4f ms\n", n.name.c_str(),
+        snprintf(buf, sizeof buf, "op %-28s %-12s %-20s %9.4f ms", n.name.c_str(),
                  n.op_type.c_str(), shp.c_str(), ms);
         os << buf;
+        // GEMM shape and the tuned DMA configuration of GEMM-backed ops.
+        auto ce = plan->convs.find(plan->ops[i]);
+        if (ce != plan->convs.end()) {
+          const ConvPlan& cg = ce->second.g;
+          const long long gm = cg.O, gn = cg.N * cg.oh * cg.ow, gk = cg.KC * cg.kh * cg.kw;
+          const double fl = 2.0 * gm * (double)gn * gk;
+          snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%d%s%s %.1f TF/s", gm, gn, gk,
+                   ce->second.cfg, ce->second.split ? " split" : "", pers_tag(ce->second.persist), ms > 0 ? fl / (ms * 1e9) : 0.0);
+          os << buf;
+        }
+        auto me = plan->matmuls.find(plan->ops[i]);
+        if (me != plan->matmuls.end()) {
+          const MatMulExec& m = me->second;
+          const double fl = 2.0 * m.M * (double)m.N * m.K;
+          snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%d%s%s %.1f TF/s", (long long)m.M,
+                   (long long)m.N, (long long)m.K, m.cfg, m.split ? " split" : "", pers_tag(m.persist),
+                   ms > 0 ? fl / (ms * 1e9) : 0.0);
+          os << buf;
+        }
+        os << "\n";
       }
       timing_report = os.str();
     }
@@ -1946,6 +1996,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
   if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->use_side_stream = s[0] != '0';
+  if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(6, atoi(s)));
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

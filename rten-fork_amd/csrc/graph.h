@@ -94,6 +94,7 @@ struct ConvExec {
   float* ws = nullptr;      // its workspace and arrival counters, plan-owned
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
+  int persist = 0;          // persistent launch, blocks per CU (0: one block per item); tuned
   // A Gemm (FC layer) run as this conv: x [B, K] as B images of [K, 1, 1],
   // W [O, K] (transB) as O pointwise filters, C [O] as the bias.
   bool fc = false;
@@ -108,6 +109,7 @@ struct MatMulExec {
   float* ws = nullptr;   // split workspace and arrival counters, plan-owned
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
+  int persist = 0;       // persistent launch, blocks per CU (0: one block per item); tuned
 };
 
 // A value stored with a zero border so the DMA convs reading it need no
@@ -170,6 +172,7 @@ struct Graph {
   bool timing = false;
   bool use_hip_graph = true;
   bool autotune = true;  // time DMA conv configurations on a plan's first run
+  int persist_mode = -1; // DMA GEMM launches: -1 tuned, 0 never persistent, k: always, k blocks/CU
   std::string timing_report;
   std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
 

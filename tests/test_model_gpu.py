@@ -63,12 +63,36 @@ def test_mobilenet_v2_bitexact(rh):
         assert _bits_equal(o, exp), np.abs(o - exp).max()
 
 
-def test_resnet50_batch64_full_size(rh):
-    """BASELINE config 2 (ResNet-50 f32, batch 64) end to end, bit-exact."""
+def test_resnet50_batch64_full_size(rh, monkeypatch):
+    """BASELINE config 2 (ResNet-50 f32, batch 64) end to end, bit-exact, with
+    the DMA GEMM's launches tuned, all persistent (work queues) and none."""
+    import torch
     from rten_hip import models
 
-    exp, outs = _run_both(rh, models.resnet50(), batch=64, runs=2, seed=7)
+    spec = models.resnet50()
+    exp, outs = _run_both(rh, spec, batch=64, runs=2, seed=7)
     assert np.isfinite(exp).all()
+    for o in outs:
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+    x = torch.from_numpy(np.random.default_rng(7).random((64, 3, 224, 224), dtype=np.float32)).cuda()
+    for mode in ("3", "0"):
+        monkeypatch.setenv("RTENHIP_PERSIST", mode)
+        g = spec.to_graph()
+        out = None
+        for _ in range(3):  # eager (tuning), capture, replay
+            out = g.run({g.input_ids[0]: x}, g.output_ids, out=out)
+            torch.cuda.synchronize()
+            assert _bits_equal(out[0].cpu().numpy(), exp), f"RTENHIP_PERSIST={mode}"
+
+
+@pytest.mark.parametrize("mode", ["2", "3", "0"])
+def test_resnet50_persistent_modes(rh, monkeypatch, mode):
+    """Persistent (per-XCD work queue) and one-block-per-tile DMA launches give
+    the oracle's bits at batch 2 (few tiles: queues shorter than the grid)."""
+    from rten_hip import models
+
+    monkeypatch.setenv("RTENHIP_PERSIST", mode)
+    exp, outs = _run_both(rh, models.resnet50(), batch=2, runs=4)
     for o in outs:
         assert _bits_equal(o, exp), np.abs(o - exp).max()
 
@@ -111,10 +135,15 @@ def _run_bert(rh, spec, batch, seq, hidden=768, runs=2, seed=99):
     return exp, outs
 
 
-def test_bert_two_layers_bitexact(rh):
+@pytest.mark.parametrize("persist", [None, "3"])
+def test_bert_two_layers_bitexact(rh, monkeypatch, persist):
     """BERT encoder (MatMul / Softmax / LayerNormalization / Gelu / Transpose)
-    at a small size: batch 2, seq 32, 2 layers."""
+    at a small size: batch 2, seq 32, 2 layers (MatMul launches tuned, and all
+    persistent)."""
     from rten_hip import models
+
+    if persist:
+        monkeypatch.setenv("RTENHIP_PERSIST", persist)
 
     exp, outs = _run_bert(rh, models.bert_encoder(layers=2, seq=32), batch=2, seq=32)
     for o in outs:
