@@ -436,10 +436,31 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
   };
 
-  // Vectorised epilogue geometry (see the epilogue).
+  // Vectorised epilogue geometry (see the epilogue) and, for short-K small
+  // wave tiles (memory-bound pointwise convs with a residual), the residual
+  // prefetched now so its latency hides under the K loop (it does not depend
+  // on the GEMM).  Not with MULTI_KB: held across the long K loop, its 16
+  // registers push the kernel into spills.
   constexpr bool VEC_FITS = NW * 1024 <= STAGES * STAGE;
+  constexpr bool RES_PRE = VEC_FITS && !MULTI_KB && MI * NI == 1 && BK == 16;
   const int rr = lane >> 3;        // row within an 8-row group
   const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
+  float4 rpre[RES_PRE ? 4 : 1];
+  if constexpr (RES_PRE) {
+    if (d.vec4 && d.residual) {
+      const int n = tn + wn + c4;
+      const bool ncol_ok = n <= N - 1;
+      const int nn = ncol_ok ? n : 0;
+      const int img = fdiv(nn, d.fdP);
+      const int64_t rbase = (int64_t)img * d.res_img + (nn - img * d.P);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int m = tm + wm + i * 8 + rr;
+        rpre[i] = (ncol_ok && m < M) ? *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c)
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
 
 
   // Prologue: fill every stage, wait for the first tile, read it.
@@ -628,7 +649,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
             x.w = __fadd_rn(x.w, cb.w);
           }
           if (d.residual && ok) {
-            const float4 r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
+            float4 r;
+            if constexpr (RES_PRE)
+              r = rpre[i];
+            else
+              r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
             x.x = __fadd_rn(x.x, r.x);
             x.y = __fadd_rn(x.y, r.y);
             x.z = __fadd_rn(x.z, r.z);
@@ -838,9 +863,7 @@ static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   X(16, 512, 64, 128, 16, 2, 4, 4, 3)   \
   X(17, 128, 32, 64, 16, 1, 2, 4, 3)    \
   X(18, 1024, 128, 128, 16, 4, 4, 4, 3) \
-  X(19, 256, 64, 64, 16, 2, 2, 5, 3)    \
-  X(20, 256, 64, 64, 16, 2, 2, 6, 3)    \
-  X(21, 256, 64, 64, 16, 2, 2, 6, 2)
+  X(19, 256, 64, 64, 16, 2, 2, 5, 3)
 #endif
 
 // Launch configuration cfg if it belongs to part PART of the split build
