@@ -240,6 +240,33 @@ rtenhip_status rtenhip_graph_plan(rtenhip_graph* g, const int32_t* input_ids,
                                   const rtenhip_tensor* inputs, int32_t n_inputs,
                                   const int32_t* output_ids, int32_t n_outputs, int64_t* shapes,
                                   int32_t* ndims);
+/* Element types of graph values, in sg::DataType / ConstantDataType order
+ * (schema.fbs:136-139, 475-478): Input::IntTensor / FloatTensor
+ * (src/ops/mod.rs:177-180).  Int32 values use the same descriptor
+ * (rtenhip_tensor, 4-byte elements). */
+typedef enum {
+  RTENHIP_DTYPE_INT32 = 0,
+  RTENHIP_DTYPE_FLOAT32 = 1,
+} rtenhip_dtype;
+/* Constant int32 tensor from HOST data (a .rten IntData / Int32 constant). */
+int32_t rtenhip_graph_add_constant_i32(rtenhip_graph* g, const char* name, const int32_t* host_data,
+                                       const int64_t* shape, int32_t ndim);
+/* rtenhip_graph_run / _plan with each input's element type (input_dtypes[i],
+ * NULL = all float32); the plan infers every value's type (Cast, Gather,
+ * Where, shape ops carry int32; the f32 kernels reject int32 inputs with
+ * RTENHIP_INCORRECT_INPUT_TYPE).  output_dtypes (may be NULL) receives the
+ * outputs' types.  A plan with a Gather on non-constant indices reports an
+ * out-of-range index ("Entry in `indices` is out of range") when the run
+ * completes, so such runs end with a stream synchronization. */
+rtenhip_status rtenhip_graph_run_typed(rtenhip_graph* g, const int32_t* input_ids,
+                                       const rtenhip_tensor* inputs, const int32_t* input_dtypes,
+                                       int32_t n_inputs, const int32_t* output_ids,
+                                       rtenhip_tensor* outputs, int32_t n_outputs);
+rtenhip_status rtenhip_graph_plan_typed(rtenhip_graph* g, const int32_t* input_ids,
+                                        const rtenhip_tensor* inputs, const int32_t* input_dtypes,
+                                        int32_t n_inputs, const int32_t* output_ids,
+                                        int32_t n_outputs, int64_t* shapes, int32_t* ndims,
+                                        int32_t* output_dtypes);
 /* Output shape of a value after the last run (or -1). */
 int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape);
 /* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled. */

@@ -69,13 +69,36 @@ def run_op(node, ins):
         return x.reshape(shape)
     if t == "Identity":
         return x
+    if t == "Gather":
+        return O.gather(x, ins[1], int(a.get("axis", 0)))
+    if t == "Where":
+        return O.where(x, ins[1], ins[2])
+    if t == "Cast":
+        # CastAttrs::to: 0 = Int32, 1 = Float (schema.fbs DataType)
+        to_int = int(a.get("to", 1)) == 0
+        if to_int:
+            return x.astype(np.int32) if x.dtype == np.int32 else O.cast_f32_to_i32(x)
+        return x.astype(np.float32) if x.dtype == np.float32 else O.cast_i32_to_f32(x)
+    if t == "Unsqueeze":
+        # unsqueeze_in_place (src/ops/layout.rs:522-548)
+        nd = x.ndim + np.asarray(ins[1]).size
+        axes = sorted(int(v) % nd for v in np.asarray(ins[1]).reshape(-1))
+        out = x
+        for ax in axes:
+            out = np.expand_dims(out, ax)
+        return out
+    if t == "Squeeze":
+        if len(ins) > 1 and ins[1] is not None:
+            return np.squeeze(x, axis=tuple(int(v) % x.ndim for v in np.asarray(ins[1]).reshape(-1)))
+        return np.squeeze(x)
     raise NotImplementedError(t)
 
 
 def run(spec, inputs: dict, outputs=None):
     """inputs: {value name: np.ndarray}; returns {output name: np.ndarray}."""
     env = {n.name: n.data for n in spec.nodes if n.kind == "const"}
-    env.update({k: np.ascontiguousarray(v, np.float32) for k, v in inputs.items()})
+    env.update({k: np.ascontiguousarray(v, np.int32 if np.asarray(v).dtype == np.int32 else np.float32)
+                for k, v in inputs.items()})
     for n in spec.nodes:
         if n.kind != "op":
             continue

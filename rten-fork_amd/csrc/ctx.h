@@ -160,4 +160,9 @@ rtenhip_status conv_transpose_output_shape(const rtenhip_tensor* x, const rtenhi
 // broadcast_shapes (src/ops/binary_elementwise.rs:23-45).
 bool broadcast_shapes(const int64_t* a, int an, const int64_t* b, int bn, int64_t* out, int* on);
 
+// Gather launch for the graph executor (indexing.hip): out-of-range indices
+// set *flag (device int) instead of synchronizing.
+rtenhip_status launch_gather(const rtenhip_tensor* x, const rtenhip_tensor_i32* indices, int64_t axis,
+                             rtenhip_tensor* y, int* flag, hipStream_t s);
+
 }  // namespace rtenhip

@@ -66,6 +66,7 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 }
 
 Plan::~Plan() {
+  if (gather_flag) (void)hipFree(gather_flag);
   for (auto& kv : convs) {
     if (kv.second.packed) (void)hipFree(kv.second.packed);
     if (kv.second.ws) (void)hipFree(kv.second.ws);
@@ -330,12 +331,73 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
       return fail(RTENHIP_INVALID_VALUE, "Permutation is invalid");
     outs[0].clear();
     for (auto p : perm) outs[0].push_back(x[p]);
+  } else if (t == "Gather") {
+    // gather (src/ops/gather.rs:21-76): x[:axis] + indices + x[axis+1:].
+    if ((st = need(1))) return st;
+    const Shape& ix = *in(1);
+    int64_t axis = (int64_t)op.attrs.num("axis", 0);
+    if (axis < -(int64_t)x.size() || axis >= (int64_t)x.size()) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+    if (axis < 0) axis += (int64_t)x.size();
+    outs[0].assign(x.begin(), x.begin() + axis);
+    outs[0].insert(outs[0].end(), ix.begin(), ix.end());
+    outs[0].insert(outs[0].end(), x.begin() + axis + 1, x.end());
+    if (outs[0].size() > RTENHIP_MAX_DIMS) return fail(RTENHIP_UNSUPPORTED_VALUE, "Gather output has too many dims");
+  } else if (t == "Where") {
+    // Where (src/ops/binary_elementwise.rs:850-929): cond, x, y broadcast together.
+    if ((st = need(1)) || (st = need(2))) return st;
+    int64_t xy[RTENHIP_MAX_DIMS], os[RTENHIP_MAX_DIMS];
+    int nxy, on;
+    if (!broadcast_shapes(in(1)->data(), (int)in(1)->size(), in(2)->data(), (int)in(2)->size(), xy, &nxy) ||
+        !broadcast_shapes(x.data(), (int)x.size(), xy, nxy, os, &on))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast inputs");
+    outs[0].assign(os, os + on);
+  } else if (t == "Unsqueeze") {
+    // unsqueeze_in_place (src/ops/layout.rs:522-548): axes resolved against
+    // ndim + len(axes), sorted, unique, inserted in order.
+    std::vector<float> av;
+    if (!const_values(*this, op.inputs.size() > 1 ? op.inputs[1] : -1, av))
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Unsqueeze needs constant axes");
+    const int64_t nd = (int64_t)(x.size() + av.size());
+    std::vector<int64_t> axes;
+    for (float f : av) {
+      int64_t a = (int64_t)f;
+      if (a < -nd || a >= nd) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+      axes.push_back(a < 0 ? a + nd : a);
+    }
+    std::sort(axes.begin(), axes.end());
+    for (size_t i = 1; i < axes.size(); i++)
+      if (axes[i] == axes[i - 1]) return fail(RTENHIP_INVALID_VALUE, "Axes must be unique");
+    if (nd > RTENHIP_MAX_DIMS) return fail(RTENHIP_UNSUPPORTED_VALUE, "Too many dims");
+    outs[0] = x;
+    for (int64_t a : axes) outs[0].insert(outs[0].begin() + a, 1);
+  } else if (t == "Squeeze") {
+    // squeeze_in_place (src/ops/layout.rs:386-421): the given axes (must be
+    // size 1), or every size-1 axis when there are none.
+    std::vector<float> av;
+    const int ai = op.inputs.size() > 1 ? op.inputs[1] : -1;
+    if (ai >= 0 && !const_values(*this, ai, av))
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Squeeze needs constant axes");
+    std::vector<bool> drop(x.size(), false);
+    if (ai < 0) {
+      for (size_t i = 0; i < x.size(); i++) drop[i] = x[i] == 1;
+    } else {
+      for (float f : av) {
+        int64_t a = (int64_t)f;
+        if (a < -(int64_t)x.size() || a >= (int64_t)x.size()) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+        if (a < 0) a += (int64_t)x.size();
+        if (x[a] != 1) return fail(RTENHIP_INVALID_VALUE, "Can only remove dimensions of size 1");
+        drop[a] = true;
+      }
+    }
+    outs[0].clear();
+    for (size_t i = 0; i < x.size(); i++)
+      if (!drop[i]) outs[0].push_back(x[i]);
   } else {
     // Shape-preserving ops: unary activations, BatchNormalization,
-    // LayerNormalization, Softmax, Identity.
+    // LayerNormalization, Softmax, Identity, Cast.
     static const std::set<std::string> same = {
         "Relu", "Clip", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu", "BatchNormalization",
-        "LayerNormalization", "Softmax", "Identity"};
+        "LayerNormalization", "Softmax", "Identity", "Cast"};
     if (!same.count(t)) {
       std::string msg = "Unsupported operator type: " + t;
       set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
@@ -346,16 +408,61 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
   return RTENHIP_OK;
 }
 
+// Element types (Input::FloatTensor / IntTensor, src/ops/mod.rs:177-180):
+// Cast converts, Gather / Where / shape ops carry their data input's type,
+// every other operator here computes in f32 and takes only f32 data.
+rtenhip_status Graph::infer_dtypes(int op_id, const std::vector<int>& ins, std::vector<int>& outs) {
+  const Node& op = nodes[op_id];
+  const std::string& t = op.op_type;
+  auto dt = [&](size_t i) { return i < ins.size() ? ins[i] : -1; };  // -1: absent input
+  outs.assign(std::max<size_t>(1, op.outputs.size()), RTENHIP_DTYPE_FLOAT32);
+  const rtenhip_status incorrect = RTENHIP_INCORRECT_INPUT_TYPE;
+  if (t == "Cast") {
+    // CastAttrs::to (op_registry.rs:421-428): Int32, else Float.
+    outs[0] = op.attrs.num("to", RTENHIP_DTYPE_FLOAT32) == RTENHIP_DTYPE_INT32 ? RTENHIP_DTYPE_INT32
+                                                                               : RTENHIP_DTYPE_FLOAT32;
+    return RTENHIP_OK;
+  }
+  if (t == "Gather") {
+    if (dt(1) != RTENHIP_DTYPE_INT32) return fail(incorrect, "Input 1 has incorrect type");
+    outs[0] = dt(0);
+    return RTENHIP_OK;
+  }
+  if (t == "Where") {
+    if (dt(0) != RTENHIP_DTYPE_INT32) return fail(incorrect, "Input 0 has incorrect type");
+    if (dt(1) != dt(2)) return fail(incorrect, "Input 2 has incorrect type");
+    outs[0] = dt(1);
+    return RTENHIP_OK;
+  }
+  // Shape ops move 4-byte elements of either type; their extra inputs (shape,
+  // axes) are int32 in the reference.
+  if (t == "Identity" || t == "Flatten" || t == "Transpose" || t == "Reshape" || t == "Unsqueeze" ||
+      t == "Squeeze") {
+    outs[0] = dt(0);
+    return RTENHIP_OK;
+  }
+  for (size_t i = 0; i < ins.size(); i++)
+    if (ins[i] == RTENHIP_DTYPE_INT32) {
+      // The reference runs integer Add/Sub/Mul/Div; the device kernels are f32.
+      if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div")
+        return fail(RTENHIP_UNSUPPORTED_VALUE, "int32 arithmetic is not supported on the device");
+      return fail(incorrect, ("Input " + std::to_string(i) + " has incorrect type").c_str());
+    }
+  return RTENHIP_OK;
+}
+
 static bool is_unary(const std::string& t) {
   return t == "Relu" || t == "Clip" || t == "Gelu" || t == "Erf" || t == "Sigmoid" ||
          t == "Tanh" || t == "Exp" || t == "Silu";
 }
 
 rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vector<Shape>& in_shapes,
-                                const std::vector<int>& out_ids, Plan& p) {
+                                const std::vector<int>& in_dtypes, const std::vector<int>& out_ids,
+                                Plan& p) {
   p.input_ids = in_ids;
   p.output_ids = out_ids;
   p.input_shapes = in_shapes;
+  p.input_dtypes = in_dtypes;
   // Producer of each value.
   std::map<int, int> producer;
   for (int i = 0; i < (int)nodes.size(); i++)
@@ -392,9 +499,16 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (st) return st;
   }
 
-  // Shapes.
+  // Shapes and element types.
   std::map<int, Shape> shapes;
   for (size_t i = 0; i < in_ids.size(); i++) shapes[in_ids[i]] = in_shapes[i];
+  for (size_t i = 0; i < in_ids.size(); i++) p.dtypes[in_ids[i]] = in_dtypes[i];
+  auto dtype_of = [&](int v) -> int {
+    if (v < 0) return -1;
+    if (nodes[v].kind == NodeKind::Constant) return nodes[v].dtype;
+    auto it = p.dtypes.find(v);
+    return it == p.dtypes.end() ? RTENHIP_DTYPE_FLOAT32 : it->second;
+  };
   auto shape_of = [&](int v) -> const Shape* {
     if (v < 0) return nullptr;
     if (nodes[v].kind == NodeKind::Constant) return &nodes[v].shape;
@@ -414,7 +528,11 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       ins[idx] = &permuted[idx];
     }
     std::vector<Shape> outs;
-    rtenhip_status st = infer_shapes(op, ins, outs);
+    std::vector<int> in_dt, out_dt;
+    for (int i : nodes[op].inputs) in_dt.push_back(dtype_of(i));
+    if (nodes[op].fused_residual >= 0) in_dt.push_back(dtype_of(nodes[op].fused_residual));
+    rtenhip_status st = infer_dtypes(op, in_dt, out_dt);
+    if (!st) st = infer_shapes(op, ins, outs);
     if (!st && nodes[op].op_type == "MatMul" && nodes[op].fused_residual >= 0) {
       // MatMul -> [Add(bias)] -> Add(residual): the Add broadcasts.
       const Shape* rs = shape_of(nodes[op].fused_residual);
@@ -444,7 +562,14 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       set_error(st, msg);
       return st;
     }
-    for (size_t k = 0; k < nodes[op].outputs.size(); k++) shapes[nodes[op].outputs[k]] = outs[k];
+    for (size_t k = 0; k < nodes[op].outputs.size(); k++) {
+      shapes[nodes[op].outputs[k]] = outs[k];
+      p.dtypes[nodes[op].outputs[k]] = out_dt[std::min(k, out_dt.size() - 1)];
+    }
+    if (nodes[op].op_type == "Gather" && !p.gather_flag) {
+      RTENHIP_HIP_CHECK(hipMalloc(&p.gather_flag, sizeof(int)));
+      RTENHIP_HIP_CHECK(hipMemset(p.gather_flag, 0, sizeof(int)));
+    }
   }
 
   // Refcounts over the plan (graph.rs:844-862), counting fused residuals.
@@ -711,7 +836,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     size_t bytes = (size_t)prod(os) * sizeof(float);
     Slot s;
     s.shape = os;
-    bool alias = n.op_type == "Flatten" || n.op_type == "Reshape" || n.op_type == "Identity";
+    bool alias = n.op_type == "Flatten" || n.op_type == "Reshape" || n.op_type == "Identity" ||
+                 n.op_type == "Unsqueeze" || n.op_type == "Squeeze";
     n.alias_input0 = alias;
     int in0 = n.inputs.empty() ? -1 : n.inputs[0];
     if (p.padded.count(out)) {
@@ -830,6 +956,31 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       RTENHIP_HIP_CHECK(hipMemcpyAsync(y.data, x.data, (size_t)numel(y) * 4,
                                        hipMemcpyDeviceToDevice, ctx->stream));
     return RTENHIP_OK;
+  }
+  if (t == "Gather") {
+    rtenhip_tensor ix = T(n.inputs[1]);
+    return launch_gather(&x, reinterpret_cast<const rtenhip_tensor_i32*>(&ix), (int64_t)n.attrs.num("axis", 0),
+                         &y, p.gather_flag, ctx->stream);
+  }
+  if (t == "Where") {
+    // 4-byte element moves: the f32 kernel serves int32 data as well.
+    rtenhip_tensor a = T(n.inputs[1]), b = T(n.inputs[2]);
+    return rtenhip_where_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &a, &b, &y);
+  }
+  if (t == "Cast") {
+    const int from = p.dtypes.count(n.inputs[0]) ? p.dtypes[n.inputs[0]]
+                     : nodes[n.inputs[0]].kind == NodeKind::Constant ? nodes[n.inputs[0]].dtype
+                                                                       : RTENHIP_DTYPE_FLOAT32;
+    const int to = p.dtypes[out];
+    if (from == to) {
+      if (y.data != x.data)
+        RTENHIP_HIP_CHECK(hipMemcpyAsync(y.data, x.data, (size_t)numel(y) * 4, hipMemcpyDeviceToDevice,
+                                         ctx->stream));
+      return RTENHIP_OK;
+    }
+    if (to == RTENHIP_DTYPE_INT32)
+      return rtenhip_cast_f32_to_i32(c, &x, reinterpret_cast<rtenhip_tensor_i32*>(&y));
+    return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
   }
   if (t == "Conv") {
     auto cit = p.convs.find(op_id);
@@ -1485,23 +1636,29 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
 }
 
 rtenhip_status Graph::find_plan(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
-                                const int32_t* out_ids, int n_out, Plan** out) {
+                                const int32_t* in_dt, const int32_t* out_ids, int n_out, Plan** out) {
   std::vector<int> iv(in_ids, in_ids + n_in), ov(out_ids, out_ids + n_out);
   std::vector<Shape> ishapes;
+  std::vector<int> idt;
   for (int i = 0; i < n_in; i++) {
     if (iv[i] < 0 || iv[i] >= (int)nodes.size()) return fail(RTENHIP_INVALID_VALUE, "Invalid input id");
     if (!is_contiguous(ins[i])) return fail(RTENHIP_UNSUPPORTED_VALUE, "Graph inputs must be contiguous");
     ishapes.emplace_back(ins[i].shape, ins[i].shape + ins[i].ndim);
+    const int dt = in_dt ? in_dt[i] : RTENHIP_DTYPE_FLOAT32;
+    if (dt != RTENHIP_DTYPE_FLOAT32 && dt != RTENHIP_DTYPE_INT32)
+      return fail(RTENHIP_INVALID_VALUE, "Unknown input data type");
+    idt.push_back(dt);
   }
   for (int o : ov)
     if (o < 0 || o >= (int)nodes.size()) return fail(RTENHIP_INVALID_VALUE, "Invalid output id");
   for (auto& pl : plans)
-    if (pl->input_ids == iv && pl->output_ids == ov && pl->input_shapes == ishapes) {
+    if (pl->input_ids == iv && pl->output_ids == ov && pl->input_shapes == ishapes &&
+        pl->input_dtypes == idt) {
       *out = pl.get();
       return RTENHIP_OK;
     }
   auto np = std::make_unique<Plan>();
-  rtenhip_status st = make_plan(iv, ishapes, ov, *np);
+  rtenhip_status st = make_plan(iv, ishapes, idt, ov, *np);
   if (st) return st;
   plans.push_back(std::move(np));
   *out = plans.back().get();
@@ -1510,11 +1667,17 @@ rtenhip_status Graph::find_plan(const int32_t* in_ids, const rtenhip_tensor* ins
 
 rtenhip_status Graph::plan_shapes(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
                                   const int32_t* out_ids, int n_out, int64_t* shapes,
-                                  int32_t* ndims) {
+                                  int32_t* ndims, const int32_t* in_dt, int32_t* out_dt) {
   Plan* plan = nullptr;
-  rtenhip_status st = find_plan(in_ids, ins, n_in, out_ids, n_out, &plan);
+  rtenhip_status st = find_plan(in_ids, ins, n_in, in_dt, out_ids, n_out, &plan);
   if (st) return st;
   for (int i = 0; i < n_out; i++) {
+    if (out_dt) {
+      const int o = out_ids[i];
+      out_dt[i] = nodes[o].kind == NodeKind::Constant ? nodes[o].dtype
+                  : plan->dtypes.count(o)             ? plan->dtypes[o]
+                                                      : RTENHIP_DTYPE_FLOAT32;
+    }
     const Shape* s = nullptr;
     if (nodes[out_ids[i]].kind == NodeKind::Constant) s = &nodes[out_ids[i]].shape;
     for (int k = 0; !s && k < n_in; k++)
@@ -1527,10 +1690,11 @@ rtenhip_status Graph::plan_shapes(const int32_t* in_ids, const rtenhip_tensor* i
 }
 
 rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
-                          const int32_t* out_ids, rtenhip_tensor* outs, int n_out) {
+                          const int32_t* out_ids, rtenhip_tensor* outs, int n_out,
+                          const int32_t* in_dt) {
   Plan* plan = nullptr;
   {
-    rtenhip_status st = find_plan(in_ids, ins, n_in, out_ids, n_out, &plan);
+    rtenhip_status st = find_plan(in_ids, ins, n_in, in_dt, out_ids, n_out, &plan);
     if (st) return st;
   }
   std::vector<int> ov(out_ids, out_ids + n_out);
@@ -1764,6 +1928,15 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
   }
   ctx->stream = caller;
+  if (!st && plan->gather_flag) {
+    // Gather's index check (gather.rs:52-60) completes with the run: read and
+    // clear the flag the kernels set on an out-of-range index.
+    int bad = 0;
+    RTENHIP_HIP_CHECK(hipMemcpyAsync(&bad, plan->gather_flag, sizeof(int), hipMemcpyDeviceToHost, exec_stream));
+    RTENHIP_HIP_CHECK(hipMemsetAsync(plan->gather_flag, 0, sizeof(int), exec_stream));
+    RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
+    if (bad) st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+  }
   RTENHIP_HIP_CHECK(hipEventRecord(ev_out, exec_stream));
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
   return st;
@@ -2060,6 +2233,30 @@ int32_t rtenhip_graph_add_constant(rtenhip_graph* g, const char* name, const flo
   return G_(g)->add_node(std::move(n));
 }
 
+int32_t rtenhip_graph_add_constant_i32(rtenhip_graph* g, const char* name, const int32_t* host_data,
+                                       const int64_t* shape, int32_t ndim) {
+  Node n;
+  n.kind = NodeKind::Constant;
+  n.name = name ? name : "";
+  n.dtype = RTENHIP_DTYPE_INT32;
+  n.shape.assign(shape, shape + ndim);
+  size_t count = (size_t)prod(n.shape);
+  if (hipMalloc(&n.dev, std::max<size_t>(4, count * 4)) != hipSuccess) {
+    set_error(RTENHIP_HIP_ERROR, "hipMalloc failed for constant");
+    return -1;
+  }
+  if (count && hipMemcpy(n.dev, host_data, count * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    set_error(RTENHIP_HIP_ERROR, "hipMemcpy failed for constant");
+    (void)hipFree(n.dev);
+    return -1;
+  }
+  // Host copy for shape-like uses (Reshape shape, Unsqueeze axes): exact as
+  // floats for the magnitudes such tensors hold.
+  if (count <= 64)
+    for (size_t i = 0; i < count; i++) n.host_small.push_back((float)host_data[i]);
+  return G_(g)->add_node(std::move(n));
+}
+
 int32_t rtenhip_graph_add_op(rtenhip_graph* g, const char* name, const char* op_type,
                              const char* attrs, const int32_t* inputs, int32_t n_inputs,
                              const int32_t* outputs, int32_t n_outputs) {
@@ -2115,6 +2312,22 @@ rtenhip_status rtenhip_graph_plan(rtenhip_graph* g, const int32_t* input_ids,
                                   const int32_t* output_ids, int32_t n_outputs, int64_t* shapes,
                                   int32_t* ndims) {
   return G_(g)->plan_shapes(input_ids, inputs, n_inputs, output_ids, n_outputs, shapes, ndims);
+}
+
+rtenhip_status rtenhip_graph_plan_typed(rtenhip_graph* g, const int32_t* input_ids,
+                                        const rtenhip_tensor* inputs, const int32_t* input_dtypes,
+                                        int32_t n_inputs, const int32_t* output_ids,
+                                        int32_t n_outputs, int64_t* shapes, int32_t* ndims,
+                                        int32_t* output_dtypes) {
+  return G_(g)->plan_shapes(input_ids, inputs, n_inputs, output_ids, n_outputs, shapes, ndims,
+                            input_dtypes, output_dtypes);
+}
+
+rtenhip_status rtenhip_graph_run_typed(rtenhip_graph* g, const int32_t* input_ids,
+                                       const rtenhip_tensor* inputs, const int32_t* input_dtypes,
+                                       int32_t n_inputs, const int32_t* output_ids,
+                                       rtenhip_tensor* outputs, int32_t n_outputs) {
+  return G_(g)->run(input_ids, inputs, n_inputs, output_ids, outputs, n_outputs, input_dtypes);
 }
 
 rtenhip_status rtenhip_graph_run(rtenhip_graph* g, const int32_t* input_ids,

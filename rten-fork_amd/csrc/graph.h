@@ -58,7 +58,8 @@ struct Node {
   // Constant: device data + host copy for small tensors (scalar attrs).
   float* dev = nullptr;
   Shape shape;
-  std::vector<float> host_small;
+  std::vector<float> host_small;   // values of small constants (int32 ones converted, exact)
+  int dtype = RTENHIP_DTYPE_FLOAT32;  // constants: element type
   bool owns_dev = true;
   // Operator
   std::string op_type;
@@ -148,6 +149,12 @@ struct Plan {
   size_t arena_bytes = 0;
   std::vector<int> input_ids, output_ids;
   std::vector<Shape> input_shapes;
+  std::vector<int> input_dtypes;
+  std::map<int, int> dtypes;          // value id -> element type (RTENHIP_DTYPE_*)
+  // Gathers with non-constant indices record an out-of-range index here; the
+  // run reads and clears it when it completes (graph-capturable: no sync
+  // inside the ops).
+  int* gather_flag = nullptr;
   // hipGraph replay state: valid for these exact input/output pointers.
   hipGraphExec_t exec = nullptr;
   std::vector<float*> bound_in, bound_out;
@@ -178,19 +185,24 @@ struct Graph {
 
   ~Graph();
   int add_node(Node n);
+  // in_dt: element type per input (RTENHIP_DTYPE_*), nullptr = all float32.
   rtenhip_status run(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
-                     const int32_t* out_ids, rtenhip_tensor* outs, int n_out);
+                     const int32_t* out_ids, rtenhip_tensor* outs, int n_out,
+                     const int32_t* in_dt = nullptr);
   rtenhip_status optimize();
   rtenhip_status plan_shapes(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
-                             const int32_t* out_ids, int n_out, int64_t* shapes, int32_t* ndims);
+                             const int32_t* out_ids, int n_out, int64_t* shapes, int32_t* ndims,
+                             const int32_t* in_dt = nullptr, int32_t* out_dt = nullptr);
 
  private:
   rtenhip_status find_plan(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
-                           const int32_t* out_ids, int n_out, Plan** out);
+                           const int32_t* in_dt, const int32_t* out_ids, int n_out, Plan** out);
   rtenhip_status make_plan(const std::vector<int>& in_ids, const std::vector<Shape>& in_shapes,
-                           const std::vector<int>& out_ids, Plan& p);
+                           const std::vector<int>& in_dtypes, const std::vector<int>& out_ids,
+                           Plan& p);
   rtenhip_status infer_shapes(int op_id, const std::vector<const Shape*>& ins,
                               std::vector<Shape>& outs);
+  rtenhip_status infer_dtypes(int op_id, const std::vector<int>& ins, std::vector<int>& outs);
   rtenhip_status exec_op(Plan& p, int op_id);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);

@@ -159,6 +159,25 @@ static bool out_matches(const rtenhip_tensor* y, const int64_t* shape, int nd) {
   return true;
 }
 
+// Gather for the graph executor: out-of-range indices are recorded in *flag
+// (device int, zeroed by the caller) instead of synchronizing, so the launch
+// can be captured in a hipGraph; the run checks the flag when it completes.
+rtenhip_status launch_gather(const rtenhip_tensor* x, const rtenhip_tensor_i32* indices, int64_t axis,
+                             rtenhip_tensor* y, int* flag, hipStream_t s) {
+  IdxDesc d;
+  int64_t ax;
+  rtenhip_status st = gather_plan(x, indices, axis, d, ax);
+  if (st) return st;
+  if (!out_matches(y, d.shape, d.ndim))
+    return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Output tensor has the wrong shape");
+  const int64_t n = numel(*y);
+  if (n == 0) return RTENHIP_OK;
+  hipLaunchKernelGGL(gather_kernel, ix_grid(n), dim3(256), 0, s, x->data, indices->data, y->data, n,
+                     d, x->shape[ax], x->strides[ax], flag);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 }  // namespace rtenhip
 
 using namespace rtenhip;

@@ -38,9 +38,11 @@ constexpr int kNumOpTypes = sizeof(kOpTypes) / sizeof(kOpTypes[0]);
 enum AttrsType : uint8_t {
   kAveragePoolAttrs = 2,
   kBatchNormalizationAttrs = 3,
+  kCastAttrs = 4,
   kConvAttrs = 7,
   kConvTransposeAttrs = 8,
   kFlattenAttrs = 9,
+  kGatherAttrs = 10,
   kGemmAttrs = 11,
   kMaxPoolAttrs = 15,
   kReshapeAttrs = 17,
@@ -148,7 +150,9 @@ struct PNode {
   Attrs attrs;
   std::vector<int> inputs, outputs;
   Shape shape;
-  std::vector<float> data;
+  std::vector<float> data;      // Float32 constants
+  std::vector<int32_t> idata;   // Int32 constants
+  int dtype = RTENHIP_DTYPE_FLOAT32;
 };
 
 struct PModel {
@@ -236,10 +240,17 @@ void read_op(const std::string& type, uint8_t attrs_type, const Table& a, Attrs&
     out.nums["allowzero"] = {(double)a.scalar<uint8_t>(0, 0)};
   } else if (type == "Gelu") {
     need(kGeluAttrs);
+  } else if (type == "Gather") {
+    need(kGatherAttrs);  // impl_read_op!(Gather, attrs_as_gather_attrs, axis)
+    out.nums["axis"] = {(double)a.scalar<int32_t>(0, 0)};
+  } else if (type == "Cast") {
+    need(kCastAttrs);  // op_registry.rs:421-428: DataType::Int32, anything else Float
+    out.nums["to"] = {a.scalar<uint8_t>(0, 0) == 0 ? (double)RTENHIP_DTYPE_INT32
+                                                   : (double)RTENHIP_DTYPE_FLOAT32};
   } else {
     static const char* const no_attrs[] = {"Add", "Sub", "Mul", "Div", "Clip", "Relu", "Erf",
                                            "Exp", "Sigmoid", "Tanh", "MatMul", "Identity",
-                                           "GlobalAveragePool"};
+                                           "GlobalAveragePool", "Where", "Unsqueeze", "Squeeze"};
     for (const char* t : no_attrs)
       if (type == t) return;
     throw LoadError{RTENHIP_UNSUPPORTED_VALUE,
@@ -337,15 +348,13 @@ PModel parse(const uint8_t* bytes, size_t len) {
             throw LoadError{RTENHIP_INVALID_VALUE, "graph error: unsupported data type for external constant"};
           if (off > len || count * 4 > len - off)
             throw LoadError{RTENHIP_INVALID_VALUE, "graph error: invalid tensor data offset"};
-          pn.data.resize(count);
           if (dtype == 1) {
+            pn.data.resize(count);
             if (count) std::memcpy(pn.data.data(), bytes + off, count * 4);
           } else {
-            for (size_t k = 0; k < count; k++) {
-              int32_t iv;
-              std::memcpy(&iv, bytes + off + 4 * k, 4);
-              pn.data[k] = (float)iv;
-            }
+            pn.dtype = RTENHIP_DTYPE_INT32;
+            pn.idata.resize(count);
+            if (count) std::memcpy(pn.idata.data(), bytes + off, count * 4);
           }
         } else {
           // Inline FloatData / IntData (model.rs:504-520).
@@ -357,11 +366,13 @@ PModel parse(const uint8_t* bytes, size_t len) {
           size_t d;
           if (!cd.vec(0, n, d, 4)) throw LoadError{RTENHIP_INVALID_VALUE, "parse error: missing required field `data`"};
           if (n != count) throw LoadError{RTENHIP_INVALID_VALUE, "graph error: constant data does not match its shape"};
-          pn.data.resize(n);
           if (ct == kFloatData) {
+            pn.data.resize(n);
             if (n) std::memcpy(pn.data.data(), fb.p + d, (size_t)n * 4);
           } else {
-            for (uint32_t k = 0; k < n; k++) pn.data[k] = (float)fb.rd<int32_t>(d + 4 * (size_t)k);
+            pn.dtype = RTENHIP_DTYPE_INT32;
+            pn.idata.resize(n);
+            for (uint32_t k = 0; k < n; k++) pn.idata[k] = fb.rd<int32_t>(d + 4 * (size_t)k);
           }
         }
       } else {
@@ -394,9 +405,10 @@ std::string describe(const PModel& pm) {
       for (size_t k = 0; k < n.shape.size(); k++) sh += (k ? "x" : "") + std::to_string(n.shape[k]);
       double sum = 0;
       for (float v : n.data) sum += v;
+      for (int32_t v : n.idata) sum += v;
       char buf[64];
       snprintf(buf, sizeof buf, " sum=%.9g", sum);
-      s += "const " + n.name + " " + sh + buf + "\n";
+      s += "const " + n.name + " " + sh + (n.dtype == RTENHIP_DTYPE_INT32 ? " i32" : "") + buf + "\n";
     } else {
       s += "op " + n.name + " " + n.op_type + " in=" + ints(n.inputs) + " out=" + ints(n.outputs);
       for (auto& kv : n.attrs.nums) {
@@ -442,8 +454,11 @@ rtenhip_graph* rtenhip_model_load_with_options(rtenhip_ctx* ctx, const uint8_t* 
     if (n.kind == NodeKind::Value) {
       id = rtenhip_graph_add_value(g, n.name.c_str());
     } else if (n.kind == NodeKind::Constant) {
-      id = rtenhip_graph_add_constant(g, n.name.c_str(), n.data.data(), n.shape.data(),
-                                      (int32_t)n.shape.size());
+      id = n.dtype == RTENHIP_DTYPE_INT32
+               ? rtenhip_graph_add_constant_i32(g, n.name.c_str(), n.idata.data(), n.shape.data(),
+                                                (int32_t)n.shape.size())
+               : rtenhip_graph_add_constant(g, n.name.c_str(), n.data.data(), n.shape.data(),
+                                            (int32_t)n.shape.size());
     } else {
       Node node;
       node.kind = NodeKind::Operator;

@@ -104,8 +104,13 @@ EXPORTED_SYMBOLS = [
     "rtenhip_model_output_ids", "rtenhip_graph_node_id", "rtenhip_graph_set_io",
     "rtenhip_graph_plan", "rtenhip_gather_output_shape", "rtenhip_gather_f32",
     "rtenhip_where_output_shape", "rtenhip_where_f32", "rtenhip_cast_f32_to_i32",
-    "rtenhip_cast_i32_to_f32",
+    "rtenhip_cast_i32_to_f32", "rtenhip_graph_add_constant_i32", "rtenhip_graph_run_typed",
+    "rtenhip_graph_plan_typed",
 ]
+
+# rtenhip_dtype (sg::DataType order, include/rten_hip.h)
+DTYPE_INT32 = 0
+DTYPE_FLOAT32 = 1
 
 
 def check(code: int):

@@ -14,7 +14,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import MAX_DIMS, OpError, Tensor, _torch, check, default_context, describe, lib
+from . import (DTYPE_FLOAT32, DTYPE_INT32, MAX_DIMS, OpError, Tensor, _torch, check, default_context,
+               describe, describe_i32, lib)
 
 
 def _attr_str(attrs: dict) -> str:
@@ -65,6 +66,14 @@ class Graph:
         return self._ret(lib().rtenhip_graph_add_value(C.c_void_p(self.ptr), name.encode()), name)
 
     def add_constant(self, name: str, data: np.ndarray) -> int:
+        """Constant tensor: int32 data stays int32 (IntData), anything else is f32."""
+        if np.asarray(data).dtype == np.int32:
+            data = np.ascontiguousarray(data, dtype=np.int32)
+            shape = (C.c_int64 * max(1, data.ndim))(*data.shape)
+            nid = lib().rtenhip_graph_add_constant_i32(C.c_void_p(self.ptr), name.encode(),
+                                                      data.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                      shape, C.c_int32(data.ndim))
+            return self._ret(nid, name)
         data = np.ascontiguousarray(data, dtype=np.float32)
         shape = (C.c_int64 * max(1, data.ndim))(*data.shape)
         nid = lib().rtenhip_graph_add_constant(C.c_void_p(self.ptr), name.encode(),
@@ -94,32 +103,59 @@ class Graph:
     def timing_report(self) -> str:
         return lib().rtenhip_graph_timing_report(C.c_void_p(self.ptr)).decode()
 
-    def output_shapes(self, inputs: Dict[int, object], outputs: Sequence[int]):
+    @staticmethod
+    def _typed(inputs: Dict[int, object]):
+        """Descriptors and element types (Input::FloatTensor / IntTensor) of
+        float32 / int32 device tensors."""
+        torch = _torch()
+        descs, dts = [], []
+        for t in inputs.values():
+            if t.dtype == torch.int32:
+                descs.append(describe_i32(t))
+                dts.append(DTYPE_INT32)
+            else:
+                descs.append(describe(t))
+                dts.append(DTYPE_FLOAT32)
+        return descs, dts
+
+    def output_info(self, inputs: Dict[int, object], outputs: Sequence[int]):
+        """Planned output (shape, dtype) pairs, dtype a torch dtype."""
+        torch = _torch()
         in_ids = list(inputs.keys())
-        descs = (Tensor * max(1, len(in_ids)))(*[describe(inputs[i]) for i in in_ids])
+        dl, tl = self._typed(inputs)
+        descs = (Tensor * max(1, len(in_ids)))(*dl)
+        idt = (C.c_int32 * max(1, len(in_ids)))(*tl)
         ia = (C.c_int32 * max(1, len(in_ids)))(*in_ids)
         oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
         shapes = (C.c_int64 * (MAX_DIMS * max(1, len(outputs))))()
         ndims = (C.c_int32 * max(1, len(outputs)))()
-        check(lib().rtenhip_graph_plan(C.c_void_p(self.ptr), ia, descs, C.c_int32(len(in_ids)), oa,
-                                       C.c_int32(len(outputs)), shapes, ndims))
-        return [tuple(shapes[i * MAX_DIMS + d] for d in range(ndims[i])) for i in range(len(outputs))]
+        odt = (C.c_int32 * max(1, len(outputs)))()
+        check(lib().rtenhip_graph_plan_typed(C.c_void_p(self.ptr), ia, descs, idt, C.c_int32(len(in_ids)),
+                                             oa, C.c_int32(len(outputs)), shapes, ndims, odt))
+        return [(tuple(shapes[i * MAX_DIMS + d] for d in range(ndims[i])),
+                 torch.int32 if odt[i] == DTYPE_INT32 else torch.float32) for i in range(len(outputs))]
+
+    def output_shapes(self, inputs: Dict[int, object], outputs: Sequence[int]):
+        return [s for s, _ in self.output_info(inputs, outputs)]
 
     def run(self, inputs: Dict[int, object], outputs: Sequence[int], out=None):
-        """Graph::run: inputs {value id: device tensor}; returns device tensors."""
+        """Graph::run: inputs {value id: float32 or int32 device tensor};
+        returns device tensors (int32 where the graph's value is int32)."""
         torch = _torch()
         self.ctx.sync_stream()
         in_ids = list(inputs.keys())
         if out is None:
-            shapes = self.output_shapes(inputs, outputs)
             dev = next(iter(inputs.values())).device if inputs else torch.device("cuda")
-            out = [torch.empty(s, dtype=torch.float32, device=dev) for s in shapes]
-        descs = (Tensor * max(1, len(in_ids)))(*[describe(inputs[i]) for i in in_ids])
-        odescs = (Tensor * max(1, len(out)))(*[describe(t) for t in out])
+            out = [torch.empty(s, dtype=dt, device=dev) for s, dt in self.output_info(inputs, outputs)]
+        dl, tl = self._typed(inputs)
+        descs = (Tensor * max(1, len(in_ids)))(*dl)
+        idt = (C.c_int32 * max(1, len(in_ids)))(*tl)
+        odescs = (Tensor * max(1, len(out)))(*[describe_i32(t) if t.dtype == torch.int32 else describe(t)
+                                                for t in out])
         ia = (C.c_int32 * max(1, len(in_ids)))(*in_ids)
         oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
-        check(lib().rtenhip_graph_run(C.c_void_p(self.ptr), ia, descs, C.c_int32(len(in_ids)), oa,
-                                      odescs, C.c_int32(len(outputs))))
+        check(lib().rtenhip_graph_run_typed(C.c_void_p(self.ptr), ia, descs, idt, C.c_int32(len(in_ids)),
+                                            oa, odescs, C.c_int32(len(outputs))))
         return out
 
 
@@ -149,7 +185,10 @@ class ModelSpec:
         return name
 
     def const(self, name: str, data: np.ndarray) -> str:
-        self.nodes.append(Node("const", name, data=np.ascontiguousarray(data, np.float32)))
+        """Constant node: int32 arrays stay int32 (IntData), others are f32."""
+        data = np.asarray(data)
+        dt = np.int32 if data.dtype == np.int32 else np.float32
+        self.nodes.append(Node("const", name, data=np.ascontiguousarray(data, dt)))
         return name
 
     def op(self, op_type: str, inputs: Sequence[Optional[str]], attrs: Optional[dict] = None,

@@ -171,7 +171,9 @@ BERT_BASE_GFLOP_PER_SEQ128 = 22.347  # SURVEY.md App. A.3 (encoder, seq 128)
 
 
 def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int = 3072,
-                 seq: int = 128, eps: float = 1e-12, seed: int = 4321) -> ModelSpec:
+                 seq: int = 128, eps: float = 1e-12, seed: int = 4321, embeddings: bool = False,
+                 vocab: int = 30522, max_pos: int = 512, type_vocab: int = 2,
+                 mask_op: str = "mul") -> ModelSpec:
     """BERT-base encoder stack in the operator mix of an ONNX export as RTen
     runs it after its own fusions (GELU and LayerNormalization fused,
     src/optimize.rs): per layer Q/K/V MatMul+Add, Reshape/Transpose to heads,
@@ -184,13 +186,49 @@ def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int 
     Gather is outside the f32 hot path) and ``attention_mask`` [B, 1, 1, S]
     (additive; zeros for the all-ones mask rten-cli uses, rten-cli main.rs).
     Weights U(+-0.05) (BERT's N(0, 0.02) init has the same scale), biases
-    U(+-0.01), LayerNorm gamma ~1, beta ~0."""
-    m = ModelSpec("bert_base" if layers == 12 else f"bert_l{layers}")
+    U(+-0.01), LayerNorm gamma ~1, beta ~0.
+
+    ``embeddings=True`` prepends the embedding and mask subgraph of the ONNX
+    export (int32 inputs ``input_ids``, ``token_type_ids``, ``attention_mask``
+    [B, S]): word / position / token-type Gathers, their sum and
+    LayerNormalization; the 0/1 mask becomes the additive one through
+    Unsqueeze x2 -> Cast(Float) -> Sub(1, .) -> Mul(-10000) (``mask_op="mul"``,
+    the classic export) or Where(mask, 0, -10000) (``mask_op="where"``)."""
+    m = ModelSpec(("bert_base" if layers == 12 else f"bert_l{layers}") + ("_emb" if embeddings else ""))
     rng = np.random.default_rng(seed)
-    x = m.value("hidden_states")
-    mask = m.value("attention_mask")
-    m.inputs = ["hidden_states", "attention_mask"]
     dh = hidden // heads
+    if embeddings:
+        ids, types, am = m.value("input_ids"), m.value("token_type_ids"), m.value("attention_mask")
+        m.inputs = ["input_ids", "token_type_ids", "attention_mask"]
+        wte = m.const("emb.word", rng.uniform(-0.05, 0.05, (vocab, hidden)).astype(np.float32))
+        wpe = m.const("emb.position", rng.uniform(-0.05, 0.05, (max_pos, hidden)).astype(np.float32))
+        wtt = m.const("emb.token_type", rng.uniform(-0.05, 0.05, (type_vocab, hidden)).astype(np.float32))
+        pos_ids = m.const("emb.position_ids", np.arange(seq, dtype=np.int32).reshape(1, seq))
+        e = m.op("Gather", [wte, ids], {"axis": 0}, name="emb.word.gather")
+        e = m.op("Add", [e, m.op("Gather", [wtt, types], {"axis": 0}, name="emb.type.gather")],
+                 name="emb.add_type")
+        e = m.op("Add", [e, m.op("Gather", [wpe, pos_ids], {"axis": 0}, name="emb.pos.gather")],
+                 name="emb.add_pos")
+        g0 = m.const("emb.ln.gamma", (1.0 + rng.uniform(-0.1, 0.1, (hidden,))).astype(np.float32))
+        b0 = m.const("emb.ln.beta", rng.uniform(-0.1, 0.1, (hidden,)).astype(np.float32))
+        x = m.op("LayerNormalization", [e, g0, b0], {"axis": -1, "epsilon": eps}, name="emb.ln")
+        ax1 = m.const("mask.axes1", np.array([1], np.int32))
+        ax2 = m.const("mask.axes2", np.array([2], np.int32))
+        mk = m.op("Unsqueeze", [am, ax1], name="mask.unsqueeze1")
+        mk = m.op("Unsqueeze", [mk, ax2], name="mask.unsqueeze2")
+        if mask_op == "where":
+            zero = m.const("mask.zero", np.array([0.0], np.float32))
+            neg = m.const("mask.neg", np.array([-10000.0], np.float32))
+            mask = m.op("Where", [mk, zero, neg], name="mask.where")
+        else:
+            mf = m.op("Cast", [mk], {"to": 1}, name="mask.cast")
+            one = m.const("mask.one", np.array([1.0], np.float32))
+            neg = m.const("mask.neg", np.array([-10000.0], np.float32))
+            mask = m.op("Mul", [m.op("Sub", [one, mf], name="mask.invert"), neg], name="mask.scale")
+    else:
+        x = m.value("hidden_states")
+        mask = m.value("attention_mask")
+        m.inputs = ["hidden_states", "attention_mask"]
 
     def lin(name, h, cin, cout):
         w = m.const(f"{name}.weight", rng.uniform(-0.05, 0.05, (cin, cout)).astype(np.float32))

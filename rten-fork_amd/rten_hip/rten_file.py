@@ -39,6 +39,7 @@ OP_TYPES = [
 ATTRS_AVERAGE_POOL, ATTRS_BATCH_NORM, ATTRS_CONV, ATTRS_CONV_TRANSPOSE, ATTRS_FLATTEN = 2, 3, 7, 8, 9
 ATTRS_GEMM, ATTRS_MAX_POOL, ATTRS_RESHAPE, ATTRS_SOFTMAX = 11, 15, 17, 20
 ATTRS_TRANSPOSE, ATTRS_LAYER_NORM, ATTRS_GELU = 21, 30, 37
+ATTRS_CAST, ATTRS_GATHER = 4, 10
 NODE_OPERATOR, NODE_CONSTANT, NODE_VALUE = 1, 2, 3
 CONST_FLOAT_DATA, CONST_INT_DATA = 1, 2
 DTYPE_INT32, DTYPE_FLOAT32 = 0, 1
@@ -197,12 +198,18 @@ def _op_attrs(op_type: str, a: dict):
         return ATTRS_RESHAPE, Table([(0, "bool", int(bool(a.get("allowzero", 0))))])
     if op_type == "Gelu":
         return ATTRS_GELU, Table([])
+    if op_type == "Gather":
+        return ATTRS_GATHER, Table([(0, "i32", int(a.get("axis", 0)))])
+    if op_type == "Cast":
+        # CastAttrs::to, sg::DataType: Int32 = 0, Float = 1
+        return ATTRS_CAST, Table([(0, "u8", int(a.get("to", 1)))])
     return 0, None
 
 
 def to_rten_bytes(spec, inline_max: int = INLINE_MAX_ELEMS) -> bytes:
-    """Serialize a ModelSpec as a .rten V2 file.  Constants read as a shape
-    (Reshape input 1) are stored as int32, like an ONNX export."""
+    """Serialize a ModelSpec as a .rten V2 file.  int32 constants, and
+    constants read as a shape (Reshape input 1), are stored as int32 like an
+    ONNX export."""
     index: Dict[str, int] = {n.name: i for i, n in enumerate(spec.nodes)}
     int_consts = set()
     for n in spec.nodes:
@@ -217,7 +224,7 @@ def to_rten_bytes(spec, inline_max: int = INLINE_MAX_ELEMS) -> bytes:
             kind = NODE_VALUE
         elif n.kind == "const":
             arr = np.asarray(n.data)
-            is_int = n.name in int_consts
+            is_int = n.name in int_consts or arr.dtype == np.int32
             arr = arr.astype("<i4" if is_int else "<f4")
             shape = _u32v(arr.shape)
             if arr.size <= inline_max:

@@ -152,6 +152,83 @@ def test_bert_two_layers_bitexact(rh, monkeypatch, persist):
             pytest.fail(f"BERT output differs: max abs {d.max():.3g}, {(d > 0).sum()} elems")
 
 
+@pytest.mark.parametrize("mask_op", ["mul", "where"])
+def test_bert_embeddings_bitexact(rh, mask_op):
+    """BERT with its embedding and mask subgraph in the device graph: int32
+    input_ids / token_type_ids / attention_mask -> word, position and type
+    Gathers, Unsqueeze, Cast or Where, Sub / Mul -> the encoder; eager, then
+    hipGraph capture and replay, bit-exact vs the oracle."""
+    import torch
+    import graph_runner
+    from rten_hip import models
+
+    spec = models.bert_encoder(layers=2, seq=32, embeddings=True, vocab=1000, mask_op=mask_op)
+    rng = np.random.default_rng(11)
+    ids = rng.integers(0, 1000, (2, 32)).astype(np.int32)
+    tt = rng.integers(0, 2, (2, 32)).astype(np.int32)
+    am = np.ones((2, 32), np.int32)
+    am[-1, 24:] = 0
+    feed = {"input_ids": ids, "token_type_ids": tt, "attention_mask": am}
+    exp = graph_runner.run(spec, feed)[spec.outputs[0]]
+    g = spec.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(feed[n]).cuda() for i, n in enumerate(spec.inputs)}
+    out = None
+    for _ in range(3):
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
+def _gather_graph():
+    from rten_hip.graph import ModelSpec
+
+    m = ModelSpec("gather")
+    ids = m.value("ids")
+    m.inputs = ["ids"]
+    table = m.const("table", np.arange(12, dtype=np.float32).reshape(4, 3))
+    y = m.op("Gather", [table, ids], {"axis": 0}, name="gather")
+    c = m.op("Cast", [ids], {"to": 1}, name="cast")
+    m.outputs = [y, c, m.op("Relu", [y], name="relu")]
+    return m
+
+
+def test_graph_gather_index_error_and_types(rh):
+    """Gather in the captured plan reports an out-of-range index with the
+    reference's error when the run completes (gather.rs:52-60), and the next
+    valid run succeeds; negative indices count from the end; Cast of an int32
+    value; int32 data into an f32-only operator is IncorrectInputType."""
+    import torch
+    from rten_hip import OpError
+    from rten_hip.graph import ModelSpec
+
+    g = _gather_graph().to_graph()
+    good = torch.tensor([[0, 3], [-1, 2]], dtype=torch.int32).cuda()
+    bad = torch.tensor([[0, 4], [1, 2]], dtype=torch.int32).cuda()
+    table = np.arange(12, dtype=np.float32).reshape(4, 3)
+    exp = table[np.array([[0, 3], [3, 2]])]
+    outs = None
+    for feed in (good, good, good, bad, good, bad, good):  # eager, capture, replays
+        if feed is bad:
+            with pytest.raises(OpError, match="Entry in `indices` is out of range") as e:
+                g.run({g.input_ids[0]: feed}, g.output_ids, out=outs)
+            assert e.value.kind == "InvalidValue"
+            continue
+        outs = g.run({g.input_ids[0]: feed}, g.output_ids, out=outs)
+        torch.cuda.synchronize()
+        assert _bits_equal(outs[0].cpu().numpy(), exp)
+        assert outs[1].dtype == torch.float32
+        assert np.array_equal(outs[1].cpu().numpy(), feed.cpu().numpy().astype(np.float32))
+    # int32 into Relu (f32 only on the device)
+    m = ModelSpec("relu_int")
+    x = m.value("x")
+    m.inputs = ["x"]
+    m.outputs = [m.op("Relu", [x], name="relu")]
+    g2 = m.to_graph()
+    with pytest.raises(OpError) as e:
+        g2.run({g2.input_ids[0]: good}, g2.output_ids)
+    assert e.value.kind == "IncorrectInputType"
+
+
 def test_bert_base_seq128_bitexact(rh):
     """BASELINE config 4's model (BERT-base encoder, 12 layers, seq 128) at
     batch 2, bit-exact vs the oracle."""

@@ -67,7 +67,7 @@ def test_describe_round_trip_tiny():
     assert "dilations=1,1" in conv
     assert "allowzero=0" in nodes[9][1]
     # int32 shape constant (Reshape input) and an inline float constant
-    assert nodes[7][1].startswith("shape 2 sum=-1")
+    assert nodes[7][1].startswith("shape 2 i32 sum=-1")
     assert nodes[2][1].startswith("b 2 sum=0")
 
 
@@ -139,12 +139,31 @@ def test_truncated_model_is_a_parse_error():
 
 
 def test_unsupported_operator_error():
-    m = ModelSpec("cast")
+    m = ModelSpec("concat")
     x = m.value("x")
     m.inputs = ["x"]
-    m.outputs = [m.op("Cast", [x], name="cast")]
-    with pytest.raises(OpError, match="operator error: operator Cast is not supported or not enabled"):
+    m.outputs = [m.op("Concat", [x, x], name="concat")]
+    with pytest.raises(OpError, match="operator error: operator Concat is not supported or not enabled"):
         rten_file.describe_model(_model_bytes(m))
+
+
+@pytest.mark.parametrize("mask_op", ["mul", "where"])
+def test_bert_embeddings_file_round_trip(mask_op):
+    """The embedding / mask subgraph (Gather, Unsqueeze, Cast, Where) and its
+    int32 constants survive the .rten round trip: CastAttrs / GatherAttrs are
+    decoded (op_registry.rs:421-428, 486), Int32 constants stay int32
+    (model.rs:504-520), inline and in the tensor segment alike."""
+    spec = models.bert_encoder(layers=1, seq=16, embeddings=True, vocab=50, mask_op=mask_op)
+    for inline_max in (0, 10 ** 9):
+        desc = rten_file.describe_model(_model_bytes(spec, inline_max=inline_max))
+        lines = desc.splitlines()
+        assert any(" const emb.position_ids 1x16 i32 sum=120" in l for l in lines)
+        assert any(" const mask.axes2 1 i32 sum=2" in l for l in lines)
+        assert any("Gather" in l and "axis=0" in l for l in lines)
+        if mask_op == "mul":
+            assert any(" Cast " in l and "to=1" in l for l in lines)
+        else:
+            assert any(" Where " in l for l in lines)
 
 
 def test_wrong_attrs_union_error(monkeypatch):
@@ -231,12 +250,35 @@ def test_load_bert_file_bitexact(gpu):
 
 @pytest.mark.gpu
 def test_load_errors_on_device(gpu):
-    m = ModelSpec("cast")
+    m = ModelSpec("concat")
     x = m.value("x")
     m.inputs = ["x"]
-    m.outputs = [m.op("Cast", [x], name="cast")]
-    with pytest.raises(OpError, match="operator error: operator Cast"):
+    m.outputs = [m.op("Concat", [x, x], name="concat")]
+    with pytest.raises(OpError, match="operator error: operator Concat"):
         rten_file.load_model(rten_file.to_rten_bytes(m))
+
+
+@pytest.mark.gpu
+def test_load_bert_embeddings_file_bitexact(gpu):
+    """A .rten BERT with the embedding Gathers and the int32 mask path runs on
+    the device from int32 inputs, bit-exact against the oracle."""
+    import graph_runner
+
+    spec = models.bert_encoder(layers=2, seq=32, embeddings=True, vocab=300)
+    g = rten_file.load_model(rten_file.to_rten_bytes(spec, inline_max=0))
+    rng = np.random.default_rng(8)
+    ids = rng.integers(0, 300, (3, 32)).astype(np.int32)
+    tt = rng.integers(0, 2, (3, 32)).astype(np.int32)
+    am = np.ones((3, 32), np.int32)
+    am[1, 20:] = 0
+    exp = graph_runner.run(spec, {"input_ids": ids, "token_type_ids": tt, "attention_mask": am})[spec.outputs[0]]
+    feed = {g.input_ids[0]: gpu.from_numpy(ids).cuda(), g.input_ids[1]: gpu.from_numpy(tt).cuda(),
+            g.input_ids[2]: gpu.from_numpy(am).cuda()}
+    out = None
+    for _ in range(3):  # eager, capture, replay
+        out = g.run(feed, g.output_ids, out=out)
+        gpu.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
 
 
 @pytest.mark.parametrize("inline_max", [0, 10 ** 9])
