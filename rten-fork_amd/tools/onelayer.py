@@ -20,6 +20,11 @@ lib.rtenhip_debug_set_dma_config.argtypes = [ctypes.c_int]
 lib.rtenhip_debug_trust_weight_cache(ctx, 1)
 lib.rtenhip_debug_set_dma_mode.argtypes = [ctypes.c_int]
 lib.rtenhip_debug_set_dma_mode(int(os.environ.get("RTENHIP_DMA_MODE", "0")))
+# persistent launch override (k blocks per CU; unset: one block per item)
+lib.rtenhip_debug_set_dma_persist.argtypes = [ctypes.c_int]
+lib.rtenhip_debug_set_dma_persist(int(os.environ.get("RTENHIP_DMA_PERSIST", "-1")))
+lib.rtenhip_debug_set_split.argtypes = [ctypes.c_int]
+lib.rtenhip_debug_set_split(int(os.environ.get("RTENHIP_DMA_SPLIT", "1")))
 if dcfg == "off":
     lib.rtenhip_debug_set_dma(ctx, 0)
 else:
