@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")"
 MODE=$1
-CFG=${2:-"X(0, 512, 128, 128, 16, 4, 2, 2, 3) X(1, 256, 128, 128, 16, 2, 2, 2, 3) X(2, 256, 64, 64, 16, 2, 2, 4, 3) X(3, 256, 64, 64, 16, 2, 2, 4, 4)"}
+CFG=${2:-"X(0, 512, 128, 128, 16, 4, 2, 2, 3, 6) X(1, 256, 128, 128, 16, 2, 2, 2, 3, 6) X(2, 256, 64, 64, 16, 2, 2, 4, 3, 6) X(3, 256, 64, 64, 16, 2, 2, 4, 4, 6)"}
 mkdir -p build/exp$MODE exp$MODE
 for f in gemm_dma gemm_dma_p0 gemm_dma_p1 gemm_dma_p2 gemm_dma_p3; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -c csrc/$f.hip \

@@ -10,7 +10,7 @@ struct DmaCfgInfo {
   int nt, bm, bn, bk, waves_m, waves_n;
 };
 static const DmaCfgInfo kDmaCfgs[] = {
-#define RTENHIP_DMA_INFO(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) {NT, BM, BN, BK, WMW, WNW},
+#define RTENHIP_DMA_INFO(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) {NT, BM, BN, BK, WMW, WNW},
     RTENHIP_DMA_CONFIGS(RTENHIP_DMA_INFO)
 #undef RTENHIP_DMA_INFO
 };
@@ -24,7 +24,7 @@ int dma_num_cfgs() { return kNumDmaCfgs; }
 
 bool dma_cfg_bvec(int cfg) {
   switch (cfg) {
-#define RTENHIP_DMA_BV(id, NT, BM, BN, BK, WMW, WNW, MINW, ST) \
+#define RTENHIP_DMA_BV(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) \
   case id:                                                  \
     return dma_bvec_ok<NT, BM, BN, BK, WMW, WNW>();
     RTENHIP_DMA_CONFIGS(RTENHIP_DMA_BV)

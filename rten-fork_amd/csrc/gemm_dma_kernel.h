@@ -93,7 +93,7 @@ __device__ __forceinline__ float f4_at(const float4& v, int j) {
 
 // One block computes a BM x BN tile with WAVES_M x WAVES_N waves, each owning
 // a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA accumulators.
-template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES,
+template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES, int HEAD_,
           bool MULTI_KB, bool BVEC>
 __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles_m, int tiles_n) {
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
@@ -236,33 +236,34 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
   };
 
-  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+  // DMA j (0 <= j < A_PER_W + B_PER_W) of this wave's share of tile kt, into
+  // stage `stage`: the A pieces first, then the B rows.
+  auto issue_j = [&](int stage, int kt, int j) __attribute__((always_inline)) {
     const uint32_t As = lds0 + (uint32_t)(stage * STAGE * 4);
     const uint32_t Bs = As + BM * BK * 4;
-    const uint32_t a_soff = a_row_base + (uint32_t)kt * (BM * BK * 4);
-#pragma unroll
-    for (int i = 0; i < A_PER_W; i++) {
-      const uint32_t dst = As + (uint32_t)((wave * A_PER_W + i) * A_CHUNK);
+    if (j < A_PER_W) {
+      const uint32_t a_soff = a_row_base + (uint32_t)kt * (BM * BK * 4);
+      const uint32_t dst = As + (uint32_t)((wave * A_PER_W + j) * A_CHUNK);
       if constexpr (A_LB == 16)
-        lds_dma16(ra, dst, va + i * A_CHUNK, a_soff);
+        lds_dma16(ra, dst, va + j * A_CHUNK, a_soff);
       else
-        lds_dma4(ra, dst, va + i * A_CHUNK, a_soff);
+        lds_dma4(ra, dst, va + j * A_CHUNK, a_soff);
+      return;
     }
+    const int i = j - A_PER_W;
     if constexpr (BVEC) {
       const uint32_t b_soff = (uint32_t)kt * (uint32_t)(BK * d.kstride * 4);
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) {
-        const int gi = wave * B_PER_W + i;  // rows 4*gi .. 4*gi+3: 1 KB of LDS
-        lds_dma16(rb, Bs + gi * 1024, vb4[i], b_soff);
-      }
+      const int gi = wave * B_PER_W + i;  // rows 4*gi .. 4*gi+3: 1 KB of LDS
+      lds_dma16(rb, Bs + gi * 1024, vb4[i], b_soff);
     } else {
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) {
-        const int gi = wave * B_PER_W + i;  // wave-uniform
-        const int kl = gi / NG, g = gi % NG;
-        lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[i]);
-      }
+      const int gi = wave * B_PER_W + i;  // wave-uniform
+      const int kl = gi / NG, g = gi % NG;
+      lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[i]);
     }
+  };
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < A_PER_W + B_PER_W; j++) issue_j(stage, kt, j);
   };
 
   f32x16 acc[MI][NI];
@@ -371,12 +372,37 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-#ifndef RTENHIP_DMA_TAIL
-#define RTENHIP_DMA_TAIL 2
-#endif
-  constexpr int TAIL = KSTEPS >= 2 * RTENHIP_DMA_TAIL ? RTENHIP_DMA_TAIL : (KSTEPS >= 4 ? 2 : 1);
-  using IMid = std::integral_constant<int, KSTEPS - TAIL>;
+  // Each K tile: HEAD MFMA steps, the DMA wait + barrier, the next tile's
+  // LDS reads, then the TAIL steps with the refill DMAs interleaved (a few
+  // after each MFMA, inside its 64-cycle shadow) instead of one burst that
+  // the wave's own MFMAs cannot cover.
+  // HEAD_ is a configuration parameter: an early barrier (2) suits the
+  // long-K layer3 / layer4 convs, a late one (6) the 56x56 ones.
+  constexpr int HEAD = KSTEPS > HEAD_ ? HEAD_ : KSTEPS / 2;
+  constexpr int TAIL = KSTEPS - HEAD;
+  using IMid = std::integral_constant<int, HEAD>;
   using IEnd = std::integral_constant<int, KSTEPS>;
+  // The tail steps of register set SET, refilling stage `rs` with tile `rkt`
+  // when `refill`.
+  auto tail_steps = [&](auto set_tag, int rs, int rkt, bool refill) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_tag)::value;
+#pragma unroll
+    for (int t = 0; t < TAIL; t++) {
+      const int s = HEAD + t;
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++)
+          if constexpr (RTENHIP_DMA_EXPERIMENT != 2)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(f4_at(av[SET][s / 4][mi], s % 4),
+                                                               bv[SET][s][ni], acc[mi][ni], 0, 0, 0);
+      if (refill && (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2)) {
+#pragma unroll
+        for (int j = t * PER_TILE / TAIL; j < (t + 1) * PER_TILE / TAIL; j++) issue_j(rs, rkt, j);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
 
   int stage = 0;  // stage holding tile kt
   auto body = [&](auto set_tag, int kt) __attribute__((always_inline)) {
@@ -385,16 +411,16 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     __builtin_amdgcn_sched_barrier(0);  // keep the scalar load ahead of the MFMAs
     mfma_steps(set_tag, I0{}, IMid{});
     pin_k();
+    const int refill_stage = stage;
+    const bool refill = kt + 1 < kt_hi && kt + STAGES < kt_hi;
     if (kt + 1 < kt_hi) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       wait_dma(min(STAGES - 2, kt_hi - kt - 2));
       if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
-      if (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2)
-        if (kt + STAGES < kt_hi) issue(stage, kt + STAGES);
       stage = stage + 1 == STAGES ? 0 : stage + 1;
       read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
     }
-    mfma_steps(set_tag, IMid{}, IEnd{});
+    tail_steps(set_tag, refill_stage, kt + STAGES, refill);
   };
   // Steady state (STAGES = 2 or 4, whose ring period divides both the
   // register-set period 2 and the KC block): a group of STAGES tiles with
@@ -412,9 +438,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
     if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
-    if constexpr (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2) issue(STG, kt + STAGES);
     read_tile(std::integral_constant<int, SET ^ 1>{}, (STG + 1) % STAGES);
-    mfma_steps(set_tag, IMid{}, IEnd{});
+    tail_steps(set_tag, STG, kt + STAGES, true);
   };
   // Tiles [kt0, kt1) with kt0 even (register set = tile parity) and
   // (kt0 - kt_lo) % STAGES == 0 (stage of tile kt0 is 0).
@@ -805,9 +830,9 @@ static void persistent_shape(Kern kern, int nt, int static_lds, int want_k, int&
   grid = k * cus;
 }
 
-template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES, bool MKB, bool BV>
+template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES, int HD, bool MKB, bool BV>
 static void launch_dma_variant(const DmaDesc& d, int tiles_m, int tiles_n, hipStream_t s) {
-  auto kern = gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, MKB, BV>;
+  auto kern = gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, MKB, BV>;
   const int items = d.n_full + d.split_tiles * d.nkb;
   int grid = items;
   size_t pad = 0;
@@ -819,51 +844,57 @@ static void launch_dma_variant(const DmaDesc& d, int tiles_m, int tiles_n, hipSt
   hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), pad, s, d, tiles_m, tiles_n);
 }
 
-template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES>
+template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES, int HD>
 static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
   if constexpr (dma_bvec_ok<NT, BM, BN, BK, WM_, WN_>()) {
     if (d.bvec) {
       if (d.K > DKC)
-        launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true, true>(d, tiles_m, tiles_n, s);
+        launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, true>(d, tiles_m, tiles_n, s);
       else
-        launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false, true>(d, tiles_m, tiles_n, s);
+        launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, false, true>(d, tiles_m, tiles_n, s);
       return;
     }
   }
   if (d.K > DKC)
-    launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, true, false>(d, tiles_m, tiles_n, s);
+    launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, false>(d, tiles_m, tiles_n, s);
   else
-    launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, false, false>(d, tiles_m, tiles_n, s);
+    launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, false, false>(d, tiles_m, tiles_n, s);
 }
 
 // DMA tile configurations:
-//   X(id, threads, BM, BN, BK, WAVES_M, WAVES_N, min waves/SIMD, stages)
+//   X(id, threads, BM, BN, BK, WAVES_M, WAVES_N, min waves/SIMD, stages, head steps)
+// (head steps: MFMA steps of a K tile before its barrier; the rest carry the
+// interleaved refill DMAs)
 // The wave tile is (BM/WAVES_M) x (BN/WAVES_N).  All configurations produce
 // bit-identical results (same KC-block summation order), so the choice is
 // purely a performance one: dma_default_cfg below, or plan-time tuning.
 #ifndef RTENHIP_DMA_CONFIGS  // (overridable for ISA inspection builds of one config)
 #define RTENHIP_DMA_CONFIGS(X)          \
-  X(0, 512, 128, 128, 16, 4, 2, 2, 3)   \
-  X(1, 256, 128, 128, 16, 2, 2, 2, 3)   \
-  X(2, 256, 64, 256, 16, 1, 4, 2, 3)    \
-  X(3, 128, 128, 64, 16, 2, 1, 2, 3)    \
-  X(4, 128, 64, 128, 16, 1, 2, 2, 3)    \
-  X(5, 64, 64, 64, 16, 1, 1, 2, 3)      \
-  X(6, 512, 256, 128, 16, 4, 2, 2, 3)   \
-  X(7, 256, 64, 64, 16, 2, 2, 4, 3)     \
-  X(8, 128, 64, 64, 16, 2, 1, 2, 3)     \
-  X(9, 256, 128, 64, 16, 4, 1, 2, 3)    \
-  X(10, 256, 64, 128, 16, 2, 2, 2, 3)   \
-  X(11, 512, 128, 128, 16, 4, 2, 2, 4)  \
-  X(12, 256, 128, 128, 16, 2, 2, 2, 4)  \
-  X(13, 256, 64, 64, 32, 2, 2, 3, 2)    \
-  X(14, 256, 64, 64, 16, 2, 2, 4, 4)    \
-  X(15, 512, 128, 64, 16, 4, 2, 4, 3)   \
-  X(16, 512, 64, 128, 16, 2, 4, 4, 3)   \
-  X(17, 128, 32, 64, 16, 1, 2, 4, 3)    \
-  X(18, 1024, 128, 128, 16, 4, 4, 4, 3) \
-  X(19, 256, 64, 64, 16, 2, 2, 5, 3)
+  X(0, 512, 128, 128, 16, 4, 2, 2, 3, 6)   \
+  X(1, 256, 128, 128, 16, 2, 2, 2, 3, 6)   \
+  X(2, 256, 64, 256, 16, 1, 4, 2, 3, 6)    \
+  X(3, 128, 128, 64, 16, 2, 1, 2, 3, 6)    \
+  X(4, 128, 64, 128, 16, 1, 2, 2, 3, 6)    \
+  X(5, 64, 64, 64, 16, 1, 1, 2, 3, 6)      \
+  X(6, 512, 256, 128, 16, 4, 2, 2, 3, 6)   \
+  X(7, 256, 64, 64, 16, 2, 2, 4, 3, 6)     \
+  X(8, 128, 64, 64, 16, 2, 1, 2, 3, 6)     \
+  X(9, 256, 128, 64, 16, 4, 1, 2, 3, 6)    \
+  X(10, 256, 64, 128, 16, 2, 2, 2, 3, 6)   \
+  X(11, 512, 128, 128, 16, 4, 2, 2, 4, 6)  \
+  X(12, 256, 128, 128, 16, 2, 2, 2, 4, 6)  \
+  X(13, 256, 64, 64, 32, 2, 2, 3, 2, 6)    \
+  X(14, 256, 64, 64, 16, 2, 2, 4, 4, 6)    \
+  X(15, 512, 128, 64, 16, 4, 2, 4, 3, 6)   \
+  X(16, 512, 64, 128, 16, 2, 4, 4, 3, 6)   \
+  X(17, 128, 32, 64, 16, 1, 2, 4, 3, 6)    \
+  X(18, 1024, 128, 128, 16, 4, 4, 4, 3, 6) \
+  X(19, 256, 64, 64, 16, 2, 2, 5, 3, 6) \
+  X(20, 256, 64, 64, 16, 2, 2, 4, 4, 2) \
+  X(21, 256, 64, 64, 16, 2, 2, 4, 3, 2) \
+  X(22, 256, 64, 64, 16, 2, 2, 4, 4, 4) \
+  X(23, 128, 64, 64, 16, 2, 1, 2, 3, 2)
 #endif
 
 // Launch configuration cfg if it belongs to part PART of the split build
@@ -872,10 +903,10 @@ constexpr int DMA_PARTS = 4;
 template <int PART>
 bool dma_launch_part(int cfg, const DmaDesc& d, hipStream_t s) {
   switch (cfg) {
-#define RTENHIP_DMA_PART_CASE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST)     \
+#define RTENHIP_DMA_PART_CASE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) \
   case id:                                                              \
     if constexpr ((id) % DMA_PARTS == PART) {                            \
-      launch_dma_cfg<NT, BM, BN, BK, WMW, WNW, MINW, ST>(d, s);          \
+      launch_dma_cfg<NT, BM, BN, BK, WMW, WNW, MINW, ST, HD>(d, s);      \
       return true;                                                      \
     } else {                                                            \
       return false;                                                     \

@@ -1367,7 +1367,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       // Candidates are timed alone: a side-stream branch still running would
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
-      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19};
+      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
@@ -1536,7 +1536,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Candidates are timed alone: a side-stream branch still running would
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
-      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19};
+      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19, 20, 21, 22, 23};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
