@@ -217,28 +217,31 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   // K-table offsets of the tile about to be issued, loaded at the start of
   // the tile body that issues it, so the scalar load's latency hides under
   // that body's first MFMAs.
+  // Two sets (by register-set parity): the steady-state body loads the next
+  // body's offsets right after its barrier, a whole K tile before they are
+  // used, so the pre-barrier lgkmcnt(0) never waits on a fresh scalar load.
   constexpr int KPRE = BVEC ? 1 : B_PER_W;
-  uint32_t kpre[KPRE];
-  auto load_k = [&](int kt) __attribute__((always_inline)) {
+  uint32_t kpre[2][KPRE];
+  auto load_k = [&](int kt, int slot) __attribute__((always_inline)) {
     if constexpr (!BVEC) {
       kt = min(kt, tiles_k - 1);
 #pragma unroll
-      for (int i = 0; i < B_PER_W; i++) kpre[i] = (uint32_t)ktab4[kt * BK + (wave * B_PER_W + i) / NG];
+      for (int i = 0; i < B_PER_W; i++) kpre[slot][i] = (uint32_t)ktab4[kt * BK + (wave * B_PER_W + i) / NG];
     }
   };
 
   // An empty asm reading the prefetched offsets, placed after the MFMAs:
   // keeps the load from being sunk into the conditional issue block.
-  auto pin_k = [&]() __attribute__((always_inline)) {
+  auto pin_k = [&](int slot) __attribute__((always_inline)) {
     if constexpr (!BVEC) {
 #pragma unroll
-      for (int i = 0; i < B_PER_W; i++) asm volatile("" ::"s"(kpre[i]));
+      for (int i = 0; i < B_PER_W; i++) asm volatile("" ::"s"(kpre[slot][i]));
     }
   };
 
   // DMA j (0 <= j < A_PER_W + B_PER_W) of this wave's share of tile kt, into
   // stage `stage`: the A pieces first, then the B rows.
-  auto issue_j = [&](int stage, int kt, int j) __attribute__((always_inline)) {
+  auto issue_j = [&](int stage, int kt, int j, int slot) __attribute__((always_inline)) {
     const uint32_t As = lds0 + (uint32_t)(stage * STAGE * 4);
     const uint32_t Bs = As + BM * BK * 4;
     if (j < A_PER_W) {
@@ -258,12 +261,12 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     } else {
       const int gi = wave * B_PER_W + i;  // wave-uniform
       const int kl = gi / NG, g = gi % NG;
-      lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[i]);
+      lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[slot][i]);
     }
   };
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < A_PER_W + B_PER_W; j++) issue_j(stage, kt, j);
+    for (int j = 0; j < A_PER_W + B_PER_W; j++) issue_j(stage, kt, j, 0);
   };
 
   f32x16 acc[MI][NI];
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
                                                                bv[SET][s][ni], acc[mi][ni], 0, 0, 0);
       if (refill && (RTENHIP_DMA_EXPERIMENT == 0 || RTENHIP_DMA_EXPERIMENT == 2)) {
 #pragma unroll
-        for (int j = t * PER_TILE / TAIL; j < (t + 1) * PER_TILE / TAIL; j++) issue_j(rs, rkt, j);
+        for (int j = t * PER_TILE / TAIL; j < (t + 1) * PER_TILE / TAIL; j++) issue_j(rs, rkt, j, SET);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -407,10 +410,10 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   int stage = 0;  // stage holding tile kt
   auto body = [&](auto set_tag, int kt) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
-    load_k(kt + STAGES);  // unconditional (clamped): no phi, so no early wait
+    load_k(kt + STAGES, SET);  // unconditional (clamped): no phi, so no early wait
     __builtin_amdgcn_sched_barrier(0);  // keep the scalar load ahead of the MFMAs
     mfma_steps(set_tag, I0{}, IMid{});
-    pin_k();
+    pin_k(SET);
     const int refill_stage = stage;
     const bool refill = kt + 1 < kt_hi && kt + STAGES < kt_hi;
     if (kt + 1 < kt_hi) {
@@ -432,12 +435,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   auto body_fast = [&](auto set_tag, auto stg_tag, int kt) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
     constexpr int STG = decltype(stg_tag)::value;
-    load_k(kt + STAGES);
-    __builtin_amdgcn_sched_barrier(0);
     mfma_steps(set_tag, I0{}, IMid{});
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * (STAGES - 2)) : "memory");
     if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
+    load_k(kt + 1 + STAGES, SET ^ 1);  // the next body's refill offsets (this body's: kpre[SET])
     read_tile(std::integral_constant<int, SET ^ 1>{}, (STG + 1) % STAGES);
     tail_steps(set_tag, STG, kt + STAGES, true);
   };
@@ -446,6 +448,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   auto run = [&](int kt0, int kt1) __attribute__((always_inline)) {
     int kt = kt0;
     if constexpr (FAST) {
+      if (kt + STAGES <= kt1 && kt + 2 * STAGES - 1 < kt_hi) load_k(kt + STAGES, 0);
       for (; kt + STAGES <= kt1 && kt + 2 * STAGES - 1 < kt_hi; kt += STAGES) {
         body_fast(I0{}, std::integral_constant<int, 0>{}, kt);
         body_fast(I1{}, std::integral_constant<int, 1>{}, kt + 1);
@@ -492,7 +495,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
 #pragma unroll
   for (int s = 0; s < STAGES; s++)
     if (kt_lo + s < kt_hi) {
-      load_k(kt_lo + s);
+      load_k(kt_lo + s, 0);
       issue(s, kt_lo + s);
     }
   wait_dma(min(STAGES, kt_hi - kt_lo) - 1);
