@@ -897,7 +897,8 @@ static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
   X(20, 256, 64, 64, 16, 2, 2, 4, 4, 2) \
   X(21, 256, 64, 64, 16, 2, 2, 4, 3, 2) \
   X(22, 256, 64, 64, 16, 2, 2, 4, 4, 4) \
-  X(23, 128, 64, 64, 16, 2, 1, 2, 3, 2)
+  X(23, 128, 64, 64, 16, 2, 1, 2, 3, 2) \
+  X(24, 256, 64, 64, 16, 2, 2, 6, 3, 6)
 #endif
 
 // Launch configuration cfg if it belongs to part PART of the split build

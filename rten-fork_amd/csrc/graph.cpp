@@ -1271,8 +1271,8 @@ rtenhip_status Graph::exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_
 }
 
 // DMA GEMM launch modes the first-run tuner times: one block per work item
-// (0) or persistent with 3 to 5 resident blocks per CU (see gemm_dma_kernel.h).
-static const int kPersistModes[4] = {0, 3, 4, 5};
+// (0) or persistent with 4 to 6 resident blocks per CU (see gemm_dma_kernel.h).
+static const int kPersistModes[4] = {0, 4, 5, 6};
 static const char* pers_tag(int k) {
   static const char* tags[] = {"", " pers1", " pers2", " pers3", " pers4", " pers5", " pers6"};
   return k >= 0 && k <= 6 ? tags[k] : " pers?";
@@ -1367,7 +1367,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       // Candidates are timed alone: a side-stream branch still running would
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
-      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23};
+      static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
@@ -1536,7 +1536,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Candidates are timed alone: a side-stream branch still running would
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
-      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19, 20, 21, 22, 23};
+      static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19, 20, 21, 22, 23, 24};
       hipEvent_t e0, e1;
       RTENHIP_HIP_CHECK(hipEventCreate(&e0));
       RTENHIP_HIP_CHECK(hipEventCreate(&e1));
