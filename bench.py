@@ -90,7 +90,7 @@ def traffic_bytes(model, batch):
     rocprofv3 PMC summary (scripts/gpu_traffic.sh -> tools/pmc_traffic.py):
     FETCH_SIZE x2 (gfx950) + WRITE_SIZE.  None when no summary exists for
     this workload."""
-    path = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
     if model != "resnet50" or batch != 64 or not os.path.exists(path):
         return None
     try:

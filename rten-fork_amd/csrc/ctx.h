@@ -82,8 +82,31 @@ struct ConvDmaArgs {
   int* counters;
   int64_t cnt_cap;
   int persist_k;  // persistent launch: resident blocks per CU (0: one block per item)
+  // The unpadded input and its geometry (direct VALU conv: padding in place).
+  const float* x_unpadded;
+  int64_t H, W, pad_t, pad_l;
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
+
+// Pointwise convs on the vector ALUs (conv_pointwise.hip): 1x1 / stride 1 /
+// unpadded / ungrouped, K <= 256, P % 4 == 0, unpadded output; mc = output
+// channels per pass (8, 16 or 32).  Weights transposed to [K][M rounded to 32].
+struct ConvPlan;
+bool conv_pw_valu_eligible(const ConvPlan& g, int64_t Hp, int64_t Wp, bool padded_out);
+int64_t pw_weight_floats(int64_t M, int64_t K);
+rtenhip_status pack_pw_weights(const float* w, int64_t M, int64_t K, float* wt, hipStream_t s);
+// variant = mc + 100 * (KX / 16): mc in {8, 16, 32} output channels per pass;
+// KX = 0 streams x per pass, KX = 16 / 32 holds a K <= KX column in VGPRs.
+bool pw_variant_ok(int variant, int64_t K);
+// Direct VALU conv (3-wide kernels, stride 1 or 2, K = C*kh*kw <= 64, OW % 4 == 0,
+// unpadded output), variant kPwDirect + mc, mc in {16, 32}.
+bool conv_direct_valu_eligible(const ConvPlan& g, bool padded_out);
+rtenhip_status conv_direct_valu(const ConvDmaArgs& a, int mc, hipStream_t s);
+constexpr int kPwDirect = 300;
+rtenhip_status conv_pw_valu(const ConvDmaArgs& a, int variant, hipStream_t s);
+// DMA-config numbers at and above this select the pointwise VALU kernel,
+// variant cfg - kPwCfgBase (graph tuner).
+constexpr int kPwCfgBase = 1000;
 bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, int64_t groups,
                        int64_t K);
 

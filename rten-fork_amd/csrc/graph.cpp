@@ -1445,11 +1445,20 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   // Input: zero-bordered by its producer, padded here, or used as is.
   const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
   auto pin = p.padded.find(n.inputs[0]);
+  // A direct VALU conv reads the unpadded input and pads in place.
+  const bool direct_cfg = ce.cfg >= kPwCfgBase + kPwDirect;
+  if (pin == p.padded.end()) {
+    a.x_unpadded = ptr_of(p, n.inputs[0]);
+    a.H = g.H;
+    a.W = g.W;
+    a.pad_t = g.pads[0];
+    a.pad_l = g.pads[1];
+  }
   if (pin != p.padded.end()) {
     a.xin = pin->second.base;
     a.Hp = pin->second.phys[2];
     a.Wp = pin->second.phys[3];
-  } else if (has_pad) {
+  } else if (has_pad && !direct_cfg) {
     a.Hp = g.H + g.pads[0] + g.pads[2];
     a.Wp = g.W + g.pads[1] + g.pads[3];
     float* xp = ctx->scratch_floats((size_t)(g.N * g.C * a.Hp * a.Wp), 1);
@@ -1518,6 +1527,21 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     e.split = true;
     return RTENHIP_OK;
   };
+  // Pointwise VALU kernel (conv_pointwise.hip) as a further tuner candidate.
+  const bool pw_ok = pin == p.padded.end() && conv_pw_valu_eligible(g, a.Hp, a.Wp, pout != p.padded.end()) &&
+                     ((uintptr_t)a.xin | (uintptr_t)a.y) % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
+  const bool direct_ok = pin == p.padded.end() && conv_direct_valu_eligible(g, pout != p.padded.end()) &&
+                         (uintptr_t)a.y % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
+  auto launch = [&]() -> rtenhip_status {
+    if (a.cfg >= kPwCfgBase + kPwDirect) return conv_direct_valu(a, a.cfg - kPwCfgBase - kPwDirect, s);
+    return a.cfg >= kPwCfgBase ? conv_pw_valu(a, a.cfg - kPwCfgBase, s) : conv_dma(ctx, a);
+  };
+  auto weight_floats = [&](int cfg) {
+    return cfg >= kPwCfgBase ? pw_weight_floats(g.O, K) : packed_conv_weight_floats(g, cfg);
+  };
+  auto pack_for = [&](int cfg, float* out) -> rtenhip_status {
+    return cfg >= kPwCfgBase ? pack_pw_weights(w, g.O, K, out, s) : pack_conv_weights(ctx, w, g, cfg, out);
+  };
   auto bind = [&](const ConvExec& e) {
     a.split = e.split;
     a.ws = e.ws;
@@ -1532,7 +1556,10 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     int chosen_persist = 0;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
-    if (autotune && cs == hipStreamCaptureStatusNone) {
+    const bool pw_forced = (pw_ok && pw_valu_mode > 0 && pw_valu_mode < kPwDirect && pw_variant_ok(pw_valu_mode, K)) ||
+                           (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32));
+    if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
+    if (autotune && cs == hipStreamCaptureStatusNone && !pw_forced) {
       // Candidates are timed alone: a side-stream branch still running would
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
@@ -1545,12 +1572,12 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Launch times of the current binding: best of n (screening) or median
       // of n (final round).
       auto time_it = [&](int n, bool median, float& out_ms) -> rtenhip_status {
-        rtenhip_status st = conv_dma(ctx, a);  // warm-up
+        rtenhip_status st = launch();  // warm-up
         if (st) return st;
         std::vector<float> ts;
         for (int r = 0; r < n; r++) {
           RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
-          st = conv_dma(ctx, a);
+          st = launch();
           if (st) return st;
           RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
           RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
@@ -1568,6 +1595,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         float* pk;
       };
       std::vector<Cand> cands;
+      float final_pad_ms = 0;  // see the direct VALU candidates
       for (int cfg : kCandidates) {
         if (cfg >= dma_num_cfgs()) continue;
         float* pk = nullptr;
@@ -1592,6 +1620,70 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           cands.push_back({ms, cfg, split, trial.persist, pk});
         }
       }
+      if (pw_ok && pw_valu_mode != 0) {
+        for (int v : {8, 16, 32, 108, 116, 208, 216}) {
+          if (!pw_variant_ok(v, K)) continue;
+          const int cfg = kPwCfgBase + v;
+          float* pk = nullptr;
+          RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
+          bufs.push_back(pk);
+          rtenhip_status st = pack_for(cfg, pk);
+          if (st) return st;
+          trial.persist = 0;
+          st = set_split(trial, cfg, false);
+          if (st) return st;
+          bind(trial);
+          a.packed_w = pk;
+          a.cfg = cfg;
+          float ms = 0;
+          st = time_it(3, false, ms);
+          if (st) return st;
+          cands.push_back({ms, cfg, 0, 0, pk});
+        }
+      }
+      if (direct_ok && pw_valu_mode != 0) {
+        // The DMA candidates' times exclude the padded copy of the input
+        // they need (made once above); the direct kernel pads in place.
+        float pad_ms = 0;
+        if (has_pad && a.xin != a.x_unpadded) {
+          std::vector<float> ts;
+          for (int r = 0; r < 4; r++) {
+            RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
+            rtenhip_status st = launch_pad_nchw(a.x_unpadded, const_cast<float*>(a.xin), g.N * g.C, (int)g.H,
+                                                (int)g.W, (int)g.pads[0], (int)g.pads[1], (int)g.pads[2],
+                                                (int)g.pads[3], s);
+            if (st) return st;
+            RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
+            RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
+            float t = 0;
+            RTENHIP_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+            ts.push_back(t);
+          }
+          std::sort(ts.begin(), ts.end());
+          pad_ms = ts[1];
+          for (Cand& c : cands)
+            if (c.cfg < kPwCfgBase) c.ms += pad_ms;
+        }
+        for (int mc : {16, 32}) {
+          const int cfg = kPwCfgBase + kPwDirect + mc;
+          float* pk = nullptr;
+          RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
+          bufs.push_back(pk);
+          rtenhip_status st = pack_for(cfg, pk);
+          if (st) return st;
+          trial.persist = 0;
+          st = set_split(trial, cfg, false);
+          if (st) return st;
+          bind(trial);
+          a.packed_w = pk;
+          a.cfg = cfg;
+          float ms = 0;
+          st = time_it(3, false, ms);
+          if (st) return st;
+          cands.push_back({ms, cfg, 0, 0, pk});
+        }
+        final_pad_ms = pad_ms;
+      }
       // Final round: the three fastest, median of seven launches each (the
       // screening minimum of many near-equal candidates favours noise).
       std::sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) { return x.ms < y.ms; });
@@ -1607,6 +1699,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         float ms = 0;
         st = time_it(7, true, ms);
         if (st) return st;
+        if (c.cfg < kPwCfgBase) ms += final_pad_ms;
         if (ms < best_ms) {
           best_ms = ms;
           chosen = c.cfg;
@@ -1621,18 +1714,18 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       if (trial.ws) (void)hipFree(trial.ws);
       if (trial.counters) (void)hipFree(trial.counters);
     }
-    RTENHIP_HIP_CHECK(hipMalloc(&ce.packed, (size_t)packed_conv_weight_floats(g, chosen) * 4));
-    rtenhip_status st = pack_conv_weights(ctx, w, g, chosen, ce.packed);
+    RTENHIP_HIP_CHECK(hipMalloc(&ce.packed, (size_t)weight_floats(chosen) * 4));
+    rtenhip_status st = pack_for(chosen, ce.packed);
     if (st) return st;
-    st = set_split(ce, chosen, chosen_split);
+    st = set_split(ce, chosen, chosen_split && chosen < kPwCfgBase);
     if (st) return st;
     ce.cfg = chosen;
-    ce.persist = persist_mode >= 0 ? persist_mode : chosen_persist;
+    ce.persist = chosen >= kPwCfgBase ? 0 : persist_mode >= 0 ? persist_mode : chosen_persist;
   }
   a.packed_w = ce.packed;
   a.cfg = ce.cfg;
   bind(ce);
-  return conv_dma(ctx, a);
+  return launch();
 }
 
 rtenhip_status Graph::find_plan(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
@@ -1909,8 +2002,10 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           const ConvPlan& cg = ce->second.g;
           const long long gm = cg.O, gn = cg.N * cg.oh * cg.ow, gk = cg.KC * cg.kh * cg.kw;
           const double fl = 2.0 * gm * (double)gn * gk;
-          snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%d%s%s %.1f TF/s", gm, gn, gk,
-                   ce->second.cfg, ce->second.split ? " split" : "", pers_tag(ce->second.persist), ms > 0 ? fl / (ms * 1e9) : 0.0);
+          const int cc = ce->second.cfg;
+          const std::string cname = cc >= kPwCfgBase ? "valu" + std::to_string(cc - kPwCfgBase) : std::to_string(cc);
+          snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%s%s%s %.1f TF/s", gm, gn, gk,
+                   cname.c_str(), ce->second.split ? " split" : "", pers_tag(ce->second.persist), ms > 0 ? fl / (ms * 1e9) : 0.0);
           os << buf;
         }
         auto me = plan->matmuls.find(plan->ops[i]);
@@ -2201,6 +2296,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
   if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->use_side_stream = s[0] != '0';
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(6, atoi(s)));
+  if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

@@ -180,6 +180,7 @@ struct Graph {
   bool use_hip_graph = true;
   bool autotune = true;  // time DMA conv configurations on a plan's first run
   int persist_mode = -1; // DMA GEMM launches: -1 tuned, 0 never persistent, k: always, k blocks/CU
+  int pw_valu_mode = -1; // pointwise convs on the VALU kernel: -1 tuned, 0 never, v > 0 forced variant (pw_variant_ok)
   std::string timing_report;
   std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
 

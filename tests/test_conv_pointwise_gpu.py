@@ -1,0 +1,170 @@
+"""Pointwise convs on the VALU kernel (csrc/conv_pointwise.hip) against the CPU
+oracle: conv_2d_pointwise (src/ops/conv.rs:24-68) = per-image
+gemm_uninit_bias with one KC block (K <= 256), then the fused Add / Relu /
+Clip in the graph.  Bar: bit-exact, for every kernel variant (channel-chunk
+width, streamed or register-resident x column) the tuner
+can pick (RTENHIP_PW_VALU forces one), including partial chunks (M not a
+multiple of it), K not a multiple of the kernel's 8-deep load group, K = 1,
+no bias, and a fused residual.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rh():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import rten_hip
+
+    rten_hip.default_context()
+    return rten_hip
+
+
+def _bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+# (N, C=K, H, W, O, bias, tail): tail in {"clip", "relu", "add_relu", "add", "none"}
+CASES = [
+    (2, 20, 12, 12, 24, True, "clip"),
+    (3, 16, 28, 28, 96, True, "relu"),
+    (2, 144, 8, 8, 24, True, "add"),
+    (2, 32, 10, 10, 40, False, "add_relu"),
+    (1, 256, 4, 4, 40, True, "none"),
+    (2, 1, 8, 8, 16, True, "none"),
+    (2, 13, 6, 6, 7, True, "clip"),
+]
+
+
+@pytest.mark.parametrize("mode", ["8", "16", "32", "108", "116", "208", "216"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[:5])) + f"-{c[6]}")
+def test_pointwise_valu_bitexact(rh, monkeypatch, mode, case):
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, C, H, W, O, has_bias, tail = case
+    if int(mode) >= 100 and C > int(mode) // 100 * 16:
+        pytest.skip("x-resident variant needs K <= KX")
+    monkeypatch.setenv("RTENHIP_PW_VALU", mode)
+    rng = np.random.default_rng(C * 131 + O)
+    m = ModelSpec("pw")
+    x = m.value("x")
+    m.inputs = ["x"]
+    ins = {"x": rng.uniform(-1, 1, (N, C, H, W)).astype(np.float32)}
+    w = m.const("w", rng.uniform(-0.5, 0.5, (O, C, 1, 1)).astype(np.float32))
+    args = [x, w]
+    if has_bias:
+        args.append(m.const("b", rng.uniform(-0.2, 0.2, (O,)).astype(np.float32)))
+    y = m.op("Conv", args, {"pads": [0, 0, 0, 0], "strides": [1, 1]})
+    if tail.startswith("add"):
+        r = m.value("r")
+        m.inputs.append("r")
+        ins["r"] = rng.uniform(-1, 1, (N, O, H, W)).astype(np.float32)
+        y = m.op("Add", [y, r])
+    if tail.endswith("relu"):
+        y = m.op("Relu", [y])
+    elif tail == "clip":
+        y = m.op("Clip", [y, m.const("lo", np.array(0, np.float32)), m.const("hi", np.array(6, np.float32))])
+    m.outputs = [y]
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
+    out = None
+    for _ in range(3):  # eager, capture, replay
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        o = out[0].cpu().numpy()
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+    g.set_timing(True)
+    g.run(dev, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    assert f"cfg=valu{mode}" in g.timing_report()
+
+
+@pytest.mark.parametrize("mode", ["16", "-1"])
+def test_mobilenet_v2_pointwise_valu(rh, monkeypatch, mode):
+    """MobileNetV2 (batch 2) with every eligible 1x1 conv forced onto the
+    VALU kernel, and with the tuner choosing per layer: oracle bits."""
+    import torch
+    import graph_runner
+    from rten_hip import models
+
+    monkeypatch.setenv("RTENHIP_PW_VALU", mode)
+    spec = models.mobilenet_v2()
+    x = np.random.default_rng(5).random((2, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {"input": x})[spec.outputs[0]]
+    g = spec.to_graph()
+    xd = torch.from_numpy(x).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        o = out[0].cpu().numpy()
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+    if mode == "16":
+        g.set_timing(True)
+        g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert g.timing_report().count("cfg=valu16") >= 20
+
+
+# Direct VALU conv (3-wide kernels): (N, C, H, W, O, kh, stride, pads, tail)
+DIRECT_CASES = [
+    (2, 3, 16, 16, 32, 3, 2, [1, 1, 1, 1], "clip"),  # MobileNetV2 stem shape, small
+    (2, 3, 17, 15, 24, 3, 2, [1, 1, 1, 1], "relu"),  # odd input, OW = 8
+    (1, 4, 12, 12, 40, 3, 1, [1, 1, 1, 1], "none"),  # stride 1, partial chunk
+    (2, 2, 9, 12, 16, 1, 1, [0, 1, 0, 1], "add"),   # 1x3 kernel, residual
+    (1, 7, 10, 14, 8, 3, 2, [0, 2, 1, 1], "clip"),  # asymmetric pads, K = 63
+]
+
+
+@pytest.mark.parametrize("mode", ["316", "332"])
+@pytest.mark.parametrize("case", DIRECT_CASES, ids=lambda c: "x".join(map(str, c[:6])) + f"s{c[6]}-{c[8]}")
+def test_direct_valu_bitexact(rh, monkeypatch, mode, case):
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, C, H, W, O, kh, st, pads, tail = case
+    monkeypatch.setenv("RTENHIP_PW_VALU", mode)
+    rng = np.random.default_rng(C * 17 + O + kh)
+    m = ModelSpec("direct")
+    x = m.value("x")
+    m.inputs = ["x"]
+    ins = {"x": rng.uniform(-1, 1, (N, C, H, W)).astype(np.float32)}
+    w = m.const("w", rng.uniform(-0.5, 0.5, (O, C, kh, 3)).astype(np.float32))
+    b = m.const("b", rng.uniform(-0.2, 0.2, (O,)).astype(np.float32))
+    y = m.op("Conv", [x, w, b], {"pads": pads, "strides": [st, st]})
+    if tail == "add":
+        oh = (H + pads[0] + pads[2] - kh) // st + 1
+        ow = (W + pads[1] + pads[3] - 3) // st + 1
+        r = m.value("r")
+        m.inputs.append("r")
+        ins["r"] = rng.uniform(-1, 1, (N, O, oh, ow)).astype(np.float32)
+        y = m.op("Add", [y, r])
+    elif tail == "relu":
+        y = m.op("Relu", [y])
+    elif tail == "clip":
+        y = m.op("Clip", [y, m.const("lo", np.array(0, np.float32)), m.const("hi", np.array(6, np.float32))])
+    m.outputs = [y]
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
+    out = None
+    for _ in range(3):  # eager, capture, replay
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        o = out[0].cpu().numpy()
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+    g.set_timing(True)
+    g.run(dev, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    assert f"cfg=valu{mode}" in g.timing_report()
