@@ -130,7 +130,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   const int n_full = d.n_full;
   // Placement experiment (separate builds only): wave 0 records where and
   // when this block ran into a debug buffer of its own (vector stores).
-  unsigned long long t_start = 0;
+  unsigned long long t_start = 0, t_kend = 0, t_sync = 0, t_bias = 0;
   if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_start = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&]() __attribute__((always_inline)) {
     if constexpr (RTENHIP_DMA_EXPERIMENT == 5) {
@@ -138,11 +138,13 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
         const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
         const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-        volatile unsigned long long* p = d.stamps + 4 * (size_t)bid;
+        volatile unsigned long long* p = d.stamps + 8 * (size_t)bid;
         p[0] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
         p[1] = t_start;
         p[2] = t_end;
-        p[3] = (unsigned long long)bid;
+        p[3] = t_kend;  // end of the (last) item's K loop
+        p[4] = t_sync;  // vectorised epilogue: after its drain + barrier
+        p[5] = t_bias;  //   after the first accumulator block is in the LDS slot
       }
     }
   };
@@ -295,7 +297,9 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   };
 
   // End of K block 0: v = alpha*acc (+ beta*C) + bias (gemm.rs:1004-1050).
-  auto first_block = [&](f32x16& v, const f32x16& a, int mi, int ni) __attribute__((always_inline)) {
+  // with_bias false: the caller adds the bias itself, next in the same order
+  // (the vectorised epilogue, after its LDS transpose).
+  auto first_block = [&](f32x16& v, const f32x16& a, int mi, int ni, bool with_bias = true) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < 16; j++) {
       const int ml = min(lrow(mi, j), m_lim);
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
       } else {
         x = d.alpha == 1.f ? a[j] : __fmul_rn(a[j], d.alpha);  // x * 1 == x exactly
       }
-      if (d.bias) x = __fadd_rn(x, bias_row(mi, j));
+      if (with_bias && d.bias) x = __fadd_rn(x, bias_row(mi, j));
       v[j] = x;
     }
   };
@@ -474,7 +478,13 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   const int rr = lane >> 3;        // row within an 8-row group
   const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
   float4 rpre[RES_PRE ? 4 : 1];
+  // With RES_PRE the bias of the lane's 4 epilogue rows is prefetched too.
+  float bpre[RES_PRE ? 4 : 1];
   if constexpr (RES_PRE) {
+    if (d.vec4 && d.bias && !d.cin) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) bpre[i] = d.bias[min(tm + wm + i * 8 + rr, M - 1)];
+    }
     if (d.vec4 && d.residual) {
       const int n = tn + wn + c4;
       const bool ncol_ok = n <= N - 1;
@@ -624,6 +634,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
   }
 
+  if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_kend = __builtin_amdgcn_s_memrealtime();
   // ---- epilogue ----
   auto apply_act = [&](float x) __attribute__((always_inline)) {
     if (d.act == RTENHIP_ACT_RELU) {
@@ -635,6 +646,14 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
     return x;
   };
+  // Relu / Clip / none as selects (no per-element branches); Gelu separately.
+  const bool act_relu = d.act == RTENHIP_ACT_RELU, act_clip = d.act == RTENHIP_ACT_CLIP;
+  const float clip_lo = d.act_lo, clip_hi = d.act_hi;
+  auto apply_act_sel = [&](float x) __attribute__((always_inline)) {
+    const float r = fmaxf(x, 0.f);
+    const float c = x < clip_lo ? clip_lo : (x > clip_hi ? clip_hi : x);
+    return act_relu ? r : (act_clip ? c : x);
+  };
   if (VEC_FITS && d.vec4) {
     // Row-contiguous outputs (P % 4 == 0, unpadded): each 32x32 accumulator
     // block is transposed through this wave's LDS slot so every lane stores
@@ -642,20 +661,36 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     // instead of 16 dword accesses.  Same per-element arithmetic as below.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land in the slots
     __syncthreads();  // every wave is done reading the K stages
+    if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_sync = __builtin_amdgcn_s_memrealtime();
     float* slot = lds + wave * 1024;
+    // Without a C input the bias is added after the transpose: a lane then
+    // needs the bias of its 4 rows only (vector loads issued together),
+    // instead of two scalar loads per accumulator element.
+    const bool bias_late = !MULTI_KB && d.bias && !d.cin;
+    const bool gelu = d.act == RTENHIP_ACT_GELU;
 #pragma unroll
     for (int mi = 0; mi < MI; mi++)
 #pragma unroll
       for (int ni = 0; ni < NI; ni++) {
+        float bl[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bias_late) {
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            bl[i] = RES_PRE ? bpre[i] : d.bias[min(tm + wm + mi * 32 + i * 8 + rr, M - 1)];
+        }
         f32x16 v;
         if constexpr (MULTI_KB) {
           v = sum[mi][ni];
+        } else if (!d.cin && d.alpha == 1.f) {
+          v = acc[mi][ni];  // first_block without C, alpha and (late) bias: the values as they are
+          if (!bias_late && d.bias) first_block(v, acc[mi][ni], mi, ni);
         } else {
-          first_block(v, acc[mi][ni], mi, ni);
+          first_block(v, acc[mi][ni], mi, ni, !bias_late);
         }
 #pragma unroll
         for (int j = 0; j < 16; j++) slot[((j & 3) + 8 * (j >> 2) + 4 * half) * 32 + l32] = v[j];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_bias = __builtin_amdgcn_s_memrealtime();
         const int n = tn + wn + ni * 32 + c4;
         const bool ncol_ok = n <= N - 1;  // N % 4 == 0: the whole segment is in range
         const int nn = ncol_ok ? n : 0;
@@ -669,6 +704,12 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
           const int m = tm + wm + mi * 32 + row;
           const bool ok = ncol_ok && m < M;
           float4 x = *(const float4*)(slot + row * 32 + c4);
+          if (bias_late) {
+            x.x = __fadd_rn(x.x, bl[i]);
+            x.y = __fadd_rn(x.y, bl[i]);
+            x.z = __fadd_rn(x.z, bl[i]);
+            x.w = __fadd_rn(x.w, bl[i]);
+          }
           if (d.colbias && ok) {
             const float4 cb = *(const float4*)(d.colbias + p);
             x.x = __fadd_rn(x.x, cb.x);
@@ -687,10 +728,17 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
             x.z = __fadd_rn(x.z, r.z);
             x.w = __fadd_rn(x.w, r.w);
           }
-          x.x = apply_act(x.x);
-          x.y = apply_act(x.y);
-          x.z = apply_act(x.z);
-          x.w = apply_act(x.w);
+          if (gelu) {
+            x.x = vm_gelu(x.x);
+            x.y = vm_gelu(x.y);
+            x.z = vm_gelu(x.z);
+            x.w = vm_gelu(x.w);
+          } else {
+            x.x = apply_act_sel(x.x);
+            x.y = apply_act_sel(x.y);
+            x.z = apply_act_sel(x.z);
+            x.w = apply_act_sel(x.w);
+          }
           if (ok) *(float4*)(d.out + obase + (int64_t)m * d.out_c) = x;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

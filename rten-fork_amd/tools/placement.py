@@ -40,13 +40,13 @@ b = torch.from_numpy(rng.random(O, dtype=np.float32)).cuda()
 y = rten_hip.conv(x, w, b, padding=(p,) * 4, strides=(s, s))
 for _ in range(3):
     rten_hip.conv(x, w, b, padding=(p,) * 4, strides=(s, s), out=y)
-stamps = torch.zeros(4 * 200000, dtype=torch.int64, device="cuda")
+stamps = torch.zeros(8 * 200000, dtype=torch.int64, device="cuda")
 lib.rtenhip_debug_set_dma_stamps(ctypes.c_void_p(stamps.data_ptr()))
 torch.cuda.synchronize()
 rten_hip.conv(x, w, b, padding=(p,) * 4, strides=(s, s), out=y)
 torch.cuda.synchronize()
 lib.rtenhip_debug_set_dma_stamps(None)
-st = stamps.cpu().numpy().reshape(-1, 4)
+st = stamps.cpu().numpy().reshape(-1, 8)
 st = st[(st[:, 1] != 0)]
 hw = st[:, 0].astype(np.uint64)
 hwid = (hw & np.uint64(0xffffffff)).astype(np.int64)
@@ -59,7 +59,7 @@ span = t1.max() - t0.min()
 key = xcc * 1000 + se * 100 + sh * 16 + cu
 per = defaultdict(list)
 for i in range(len(st)):
-    per[key[i]].append((t0[i], t1[i], st[i, 3]))
+    per[key[i]].append((t0[i], t1[i], i))
 print(f"blocks {len(st)}  CUs used {len(per)}  kernel span {span / 100:.1f} us")
 cnt = np.array([len(v) for v in per.values()])
 print(f"blocks per CU: min {cnt.min()} max {cnt.max()} mean {cnt.mean():.2f}  histogram "
@@ -85,3 +85,14 @@ print(f"block start times (us) quantiles: " +
 # the CU's wave-time), and per-CU last end
 busy = np.array([sum(e - s for s, e, _ in v) for v in per.values()]) / 100
 print(f"per-CU summed block time us: min {busy.min():.1f} median {np.median(busy):.1f} max {busy.max():.1f}")
+# phases (experiment build 5 stamps the end of the last item's K loop in slot 3)
+tk = st[:, 3]
+if (tk > 0).all():
+    kph = (tk - t0) / 100
+    eph = (t1 - tk) / 100
+    print(f"start->K-loop end us: median {np.median(kph):.2f} p10 {np.quantile(kph, 0.1):.2f} p90 {np.quantile(kph, 0.9):.2f}")
+    print(f"epilogue us:          median {np.median(eph):.2f} p10 {np.quantile(eph, 0.1):.2f} p90 {np.quantile(eph, 0.9):.2f}")
+    if (st[:, 4] > 0).all():
+        for nm, a_, b_ in (("K end -> drain+barrier", 3, 4), ("-> block 0 in slot", 4, 5), ("-> end", 5, 2)):
+            ph = (st[:, b_] - st[:, a_]) / 100
+            print(f"  {nm:24s} median {np.median(ph):.2f} p10 {np.quantile(ph, 0.1):.2f} p90 {np.quantile(ph, 0.9):.2f}")
