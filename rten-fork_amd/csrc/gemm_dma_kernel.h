@@ -672,11 +672,32 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     for (int mi = 0; mi < MI; mi++)
 #pragma unroll
       for (int ni = 0; ni < NI; ni++) {
+        // Every load of this block is issued before its stores: vmcnt
+        // retires in order, so a load issued after a store would wait for it.
+        // Addresses are clamped in range; rows / columns out of range are
+        // computed but not stored.
+        const int n = tn + wn + ni * 32 + c4;
+        const bool ncol_ok = n <= N - 1;  // N % 4 == 0: the whole segment is in range
+        const int nn = ncol_ok ? n : 0;
+        const int img = fdiv(nn, d.fdP);
+        const int p = nn - img * d.P;
+        const int64_t obase = (int64_t)img * d.out_img + p;
+        const int64_t rbase = (int64_t)img * d.res_img + p;
         float bl[4] = {0.f, 0.f, 0.f, 0.f};
         if (bias_late) {
 #pragma unroll
           for (int i = 0; i < 4; i++)
             bl[i] = RES_PRE ? bpre[i] : d.bias[min(tm + wm + mi * 32 + i * 8 + rr, M - 1)];
+        }
+        float4 cb = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (d.colbias) cb = *(const float4*)(d.colbias + p);
+        float4 rl[RES_PRE ? 1 : 4];
+        if constexpr (!RES_PRE) {
+          if (d.residual) {
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              rl[i] = *(const float4*)(d.residual + rbase + (int64_t)min(tm + wm + mi * 32 + i * 8 + rr, M - 1) * d.res_c);
+          }
         }
         f32x16 v;
         if constexpr (MULTI_KB) {
@@ -691,13 +712,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
         for (int j = 0; j < 16; j++) slot[((j & 3) + 8 * (j >> 2) + 4 * half) * 32 + l32] = v[j];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_bias = __builtin_amdgcn_s_memrealtime();
-        const int n = tn + wn + ni * 32 + c4;
-        const bool ncol_ok = n <= N - 1;  // N % 4 == 0: the whole segment is in range
-        const int nn = ncol_ok ? n : 0;
-        const int img = fdiv(nn, d.fdP);
-        const int p = nn - img * d.P;
-        const int64_t obase = (int64_t)img * d.out_img + p;
-        const int64_t rbase = (int64_t)img * d.res_img + p;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int row = i * 8 + rr;
@@ -710,19 +724,18 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
             x.z = __fadd_rn(x.z, bl[i]);
             x.w = __fadd_rn(x.w, bl[i]);
           }
-          if (d.colbias && ok) {
-            const float4 cb = *(const float4*)(d.colbias + p);
+          if (d.colbias) {
             x.x = __fadd_rn(x.x, cb.x);
             x.y = __fadd_rn(x.y, cb.y);
             x.z = __fadd_rn(x.z, cb.z);
             x.w = __fadd_rn(x.w, cb.w);
           }
-          if (d.residual && ok) {
+          if (d.residual) {
             float4 r;
             if constexpr (RES_PRE)
               r = rpre[i];
             else
-              r = *(const float4*)(d.residual + rbase + (int64_t)m * d.res_c);
+              r = rl[i];
             x.x = __fadd_rn(x.x, r.x);
             x.y = __fadd_rn(x.y, r.y);
             x.z = __fadd_rn(x.z, r.z);
@@ -746,6 +759,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     return;
   }
   const bool full_tile = m_lim >= BM - 1 && n_lim >= BN - 1;
+  const bool gelu_any = d.act == RTENHIP_ACT_GELU;
 #pragma unroll
   for (int ni = 0; ni < NI; ni++) {
     const int nl = wn + ni * 32 + l32;
@@ -757,22 +771,38 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     const int ox = p - oy * d.OW;
     const int64_t obase = (int64_t)img * d.out_img + (int64_t)oy * d.out_row + ox + d.out_off;
     const int64_t rbase = (int64_t)img * d.res_img + p;
+    // As in the vectorised path: this block's loads (bias rows, the column
+    // bias, the residual) are issued together before its stores -- vmcnt
+    // retires in order, so a load behind a store would wait for the store.
+    const bool bias_late = !MULTI_KB && d.bias && !d.cin;
+    const float cbv = d.colbias ? d.colbias[p] : 0.f;
 #pragma unroll
     for (int mi = 0; mi < MI; mi++) {
+      float bv[16], rv[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int ml = lrow(mi, j);
+        const bool ok = full_tile || (ncol_ok && ml <= m_lim);
+        bv[j] = bias_late ? d.bias[min(tm + ml, M - 1)] : 0.f;
+        rv[j] = d.residual ? d.residual[ok ? rbase + (int64_t)(tm + ml) * d.res_c : 0] : 0.f;
+      }
       f32x16 v;
       if constexpr (MULTI_KB) {
         v = sum[mi][ni];
+      } else if (!d.cin && d.alpha == 1.f) {
+        v = acc[mi][ni];
       } else {
-        first_block(v, acc[mi][ni], mi, ni);
+        first_block(v, acc[mi][ni], mi, ni, !bias_late);
       }
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const int ml = lrow(mi, j);
         const bool ok = full_tile || (ncol_ok && ml <= m_lim);
         float x = v[j];
-        if (d.colbias) x = __fadd_rn(x, d.colbias[p]);
-        if (d.residual) x = __fadd_rn(x, d.residual[ok ? rbase + (int64_t)(tm + ml) * d.res_c : 0]);
-        x = apply_act(x);
+        if (bias_late) x = __fadd_rn(x, bv[j]);
+        if (d.colbias) x = __fadd_rn(x, cbv);
+        if (d.residual) x = __fadd_rn(x, rv[j]);
+        x = gelu_any ? apply_act(x) : apply_act_sel(x);
         if (ok) d.out[obase + (int64_t)(tm + ml) * d.out_c] = x;
       }
     }
