@@ -474,7 +474,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   // on the GEMM).  Not with MULTI_KB: held across the long K loop, its 16
   // registers push the kernel into spills.
   constexpr bool VEC_FITS = NW * 1024 <= STAGES * STAGE;
-  constexpr bool RES_PRE = VEC_FITS && !MULTI_KB && MI * NI == 1 && BK == 16;
+  constexpr bool RES_PRE = VEC_FITS && !MULTI_KB && MI * NI == 1 && BK == 16 && MINW <= 4;
   const int rr = lane >> 3;        // row within an 8-row group
   const int c4 = (lane & 7) * 4;   // first of this lane's 4 columns
   float4 rpre[RES_PRE ? 4 : 1];
