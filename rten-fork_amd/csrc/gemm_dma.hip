@@ -119,8 +119,8 @@ namespace rtenhip {
 // (q * BM + r) * 4 + j holds row r, k = 8 * (q >> 1) + 2 * j + (q & 1), so
 // the lane owning row r and k parity (q & 1) reads the A operands of 4
 // consecutive 32x32x2 MFMA steps with one ds_read_b128.  One workgroup per
-// (m tile, kcw-wide k chunk; kcw = 64, or 32 for 256-row tiles so the LDS
-// stays under 64 KB): the BM rows are read as kcw*4-byte segments (float4 per
+// (m tile, kcw-wide k chunk; kcw = BK, or wider until the chunk holds 256
+// float4s): the BM rows are read as kcw*4-byte segments (float4 per
 // lane when aligned), transposed through LDS, and the chunk's kcw/BK tiles --
 // contiguous in the packed layout -- written with float4 stores.
 
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a
   const int mt = blockIdx.x, kc = blockIdx.y;
   const int k0 = kc * kcw;
   const int64_t m0 = (int64_t)mt * BM;
-  // BM rows x kcw/4 float4s: 2..8 per thread (a multiple of 256 in total),
+  // BM rows x kcw/4 float4s: 1..8 per thread (a multiple of 256 in total),
   // all loads issued before the LDS stores.
   const int lq4 = lkcw - 2;
   const int per = (BM << lq4) >> 8;
@@ -196,9 +196,12 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
   const int tiles_k = (K + t.bk - 1) / t.bk;
   const int tiles_m = (M + t.bm - 1) / t.bm;
   if ((int64_t)tiles_m * tiles_k == 0) return RTENHIP_OK;
-  const int kcw = t.bm >= 256 ? 32 : 64;
+  // Narrow k chunks (more workgroups, so reads and writes overlap across
+  // them), but at least one float4 per thread: BM * kcw / 4 >= 256.
+  int kcw = t.bk;
+  while (t.bm * kcw < 1024) kcw *= 2;
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
-  if (kcw % t.bk != 0 || !pow2(t.bm) || t.bm < 32 || t.bm > 256 || !pow2(t.bk) || t.bk % 8 != 0 ||
+  if (kcw % t.bk != 0 || kcw > 64 || !pow2(t.bm) || t.bm < 32 || t.bm > 256 || !pow2(t.bk) || t.bk % 8 != 0 ||
       tiles_m > 0x7fffffff)
     return fail(RTENHIP_UNSUPPORTED_VALUE, "unsupported A pack shape");
   // packed output chunks are 16-byte aligned (BK * BM % 4 == 0); float4 reads
