@@ -189,9 +189,27 @@ __global__ __launch_bounds__(256) void pad_nchw_kernel(const float* __restrict__
   const bool in = (unsigned)yh < (unsigned)H;
   const float* xr = x + ((int64_t)plane * H + (in ? yh : 0)) * W;
   float* yr = y + (int64_t)r * Wp;
-  for (int c = threadIdx.x & 63; c < Wp; c += 64) {
-    const int xw = c - pl;
-    yr[c] = (in && (unsigned)xw < (unsigned)W) ? xr[xw] : 0.f;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yr, 0, Wp * 4, 0x00020000);
+  // Up to 4 * 64 columns per pass with every load issued before the stores
+  // (a store-then-load loop would wait for each store: vmcnt is in order).
+  for (int c0 = 0; c0 < Wp; c0 += 256) {
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int c = c0 + j * 64 + (threadIdx.x & 63);
+      const int xw = c - pl;
+      const bool ok = in && c < Wp && (unsigned)xw < (unsigned)W;
+      v[j] = ok ? xr[xw] : 0.f;
+    }
+    // Columns past the row end get an out-of-range buffer offset: the store
+    // is dropped by the hardware, so no lane-divergent branch (and no
+    // conservative wait) around the stores.
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int c = c0 + j * 64 + (threadIdx.x & 63);
+      const uint32_t off = c < Wp ? (uint32_t)(c * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), yrs, off, 0, 0);
+    }
   }
 }
 
