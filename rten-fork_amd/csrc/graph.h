@@ -174,7 +174,7 @@ struct Graph {
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
   hipStream_t side_stream = nullptr;
-  bool use_side_stream = true;
+  bool use_side_stream = false;  // RTENHIP_SIDE_STREAM=1: downsample branches on a second stream (measured 0.5% slower on ResNet-50 b64: the concurrent kernels were tuned alone)
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
   bool use_hip_graph = true;
