@@ -329,10 +329,15 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
         *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
       }
     } else {
-      for (int pp = 0; pp < np; pp++) {
-        const float* src = x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W;
-        float* dst = tile + (pp * rows_in + (r0 - iy_lo)) * W;
-        for (int q = threadIdx.x; q < span; q += blockDim.x) dst[q] = src[q];
+      // Rows of 14 or 7 floats (MobileNetV2's last stages): one flat loop over
+      // every plane's span, so a block of 36 small planes issues its loads
+      // together instead of one plane (49 active lanes) per round trip.
+      const int total = np * span;
+#pragma unroll 4
+      for (int t = threadIdx.x; t < total; t += blockDim.x) {
+        const int pp = t / span, q = t - pp * span;
+        tile[(pp * rows_in + (r0 - iy_lo)) * W + q] =
+            x[(int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + q];
       }
     }
   }
