@@ -440,6 +440,155 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
   }
 }
 
+// 3x3 depthwise, stride S in both axes, no dilation, OW % 4 == 0: a thread
+// owns 4 adjacent output columns and TR consecutive output rows of one plane
+// (16-byte output stores and residual loads, each staged input value read
+// from LDS once per row instead of once per tap).  A block covers PB planes x
+// RS row slices x OW/4 column groups; the input rows of its TH = RS * TR
+// output rows are staged in LDS as in depthwise_lds_kernel, with a DW4_MARGIN
+// float margin so edge reads stay inside the allocation (their values are
+// never used: colok masks them).  Per output: bias, then + v * w over the taps
+// in ky, kx order, skipped exactly as in depthwise32_kernel.
+constexpr int DW4_MARGIN = 8;
+constexpr int DW4_TR = 4;
+
+template <int S>
+__global__ __launch_bounds__(256) void depthwise_lds4_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ y, int planes, int C, int H, int W, int OH, int OW, int pt, int pl,
+    int RS, int PB, int rows_in, DwBounds b, const float* __restrict__ residual, int act, float lo,
+    float hi) {
+  extern __shared__ float4 dw4_lds[];
+  float* tile = reinterpret_cast<float*>(dw4_lds) + DW4_MARGIN;
+  constexpr int NC = 3 * S + 3;  // input columns a thread's 4 outputs need (S=1: 6, S=2: 9)
+  const int CG = OW >> 2;
+  const int TH = RS * DW4_TR;
+  const int plane0 = blockIdx.y * PB;
+  const int oy0 = blockIdx.x * TH;
+  const int iy_lo = oy0 * S - pt;  // input row held in tile row 0
+  const int np = min(PB, planes - plane0);
+  const int r0 = max(iy_lo, 0), r1 = min(iy_lo + rows_in, H);
+  if (r1 > r0) {
+    // W % 4 == 0 here (OW % 4 == 0 and W >= (OW - 1) * S + 1 ... checked on the host)
+    const int n4 = ((r1 - r0) * W) >> 2, total4 = np * n4;
+#pragma unroll 4
+    for (int t = threadIdx.x; t < total4; t += blockDim.x) {
+      const int pp = t / n4, q4 = t - pp * n4;
+      const float4 v = *(const float4*)(x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + 4 * q4);
+      *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
+    }
+  }
+  __syncthreads();
+  const int per_plane = RS * CG;
+  const int pp = threadIdx.x / per_plane;
+  const int rem = threadIdx.x - pp * per_plane;
+  const int rs = rem / CG;
+  const int ox0 = (rem - rs * CG) * 4;
+  if (pp >= np) return;
+  const int plane = plane0 + pp;
+  const int c = plane % C;
+  float wr[9];
+#pragma unroll
+  for (int t = 0; t < 9; t++) wr[t] = w[c * 9 + t];
+  const float b0 = bias ? bias[c] : 0.f;
+  bool colok[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+#pragma unroll
+    for (int kx = 0; kx < 3; kx++) colok[i][kx] = ox0 + i >= b.omin[kx] && ox0 + i < b.omax[kx];
+  const int cbase = ox0 * S - pl;
+  const int oyb = oy0 + rs * DW4_TR;
+  const int nrow = min(DW4_TR, OH - oyb);
+  float win[3][NC];
+  auto load_row = [&](int slot, int iy) __attribute__((always_inline)) {
+    const bool ok = iy >= 0 && iy < H;
+    const float* row = tile + (pp * rows_in + (ok ? iy - iy_lo : 0)) * W + cbase;
+#pragma unroll
+    for (int j = 0; j < NC; j++) win[slot][j] = ok ? row[j] : 0.f;
+  };
+  int top = oyb * S - pt;
+  load_row(0, top);
+  load_row(1, top + 1);
+  load_row(2, top + 2);
+  for (int r = 0; r < nrow; r++) {
+    const int oy = oyb + r;
+    if (r > 0) {
+      top = oy * S - pt;
+      if constexpr (S == 1) {
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+          win[0][j] = win[1][j];
+          win[1][j] = win[2][j];
+        }
+        load_row(2, top + 2);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NC; j++) win[0][j] = win[2][j];
+        load_row(1, top + 1);
+        load_row(2, top + 2);
+      }
+    }
+    float acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      acc[i] = b0;
+#pragma unroll
+      for (int ky = 0; ky < 3; ky++) {
+        const int iy = top + ky;
+        if (iy < 0 || iy >= H) continue;
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++)
+          if (colok[i][kx]) acc[i] = __fadd_rn(acc[i], __fmul_rn(win[ky][i * S + kx], wr[ky * 3 + kx]));
+      }
+    }
+    const int64_t oi = (int64_t)plane * OH * OW + (int64_t)oy * OW + ox0;
+    if (residual) {
+      const float4 rv = *(const float4*)(residual + oi);
+      acc[0] = __fadd_rn(acc[0], rv.x);
+      acc[1] = __fadd_rn(acc[1], rv.y);
+      acc[2] = __fadd_rn(acc[2], rv.z);
+      acc[3] = __fadd_rn(acc[3], rv.w);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (act == RTENHIP_ACT_RELU) acc[i] = rust_max(acc[i], 0.f);
+      else if (act == RTENHIP_ACT_CLIP) acc[i] = rust_clamp(acc[i], lo, hi);
+    }
+    *(float4*)(y + oi) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  }
+}
+
+// Launch geometry of depthwise_lds4_kernel, or false when the shape is not
+// one it handles.  Row slices per plane: the largest RS (TH = 4 RS output
+// rows per block) whose staged rows fit the LDS budget, preferring a TH that
+// divides OH; planes per block fill up to 256 threads.
+struct Dw4Geom {
+  int RS, PB, rows_in;
+  size_t lds;
+};
+static bool dw4_geometry(int H, int W, int OH, int OW, int S, int pt, int pl, int pr, Dw4Geom& g) {
+  if (OW % 4 != 0 || W % 4 != 0 || OW > 256 || pl > DW4_MARGIN / 2 || pr > DW4_MARGIN / 2) return false;
+  const int CG = OW / 4;
+  const int budget = 8192;  // floats of staged input per block (32 KB)
+  auto rows_for = [&](int th) { return (th - 1) * S + 3; };
+  int best = 0;
+  for (int rs = std::max(1, std::min(256 / CG, (OH + DW4_TR - 1) / DW4_TR)); rs >= 1; rs--) {
+    if (rows_for(rs * DW4_TR) * W > budget) continue;
+    if (!best) best = rs;
+    if (OH % (rs * DW4_TR) == 0) {
+      if (2 * rs >= best) best = rs;  // an exact split unless it halves the block
+      break;
+    }
+  }
+  if (!best) return false;
+  g.RS = best;
+  g.rows_in = rows_for(best * DW4_TR);
+  g.PB = std::max(1, 256 / (best * CG));
+  while (g.PB > 1 && g.PB * g.rows_in * W > budget) g.PB--;
+  g.lds = ((size_t)g.PB * g.rows_in * W + 2 * DW4_MARGIN) * sizeof(float);
+  return true;
+}
+
 rtenhip_status launch_depthwise(const float* x, const float* w, const float* bias, float* y,
                                 int N, int C, int H, int W, int OH, int OW, int kh, int kw,
                                 int sh, int sw, int dh, int dw, int pt, int pl,
@@ -459,9 +608,36 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
       int omax = (t + sw - 1) / sw;
       b.omax[kx] = omax > OW ? OW : omax;
     }
+    const int planes = N * C;
+    // 4 output columns per thread (depthwise_lds4_kernel) where it applies:
+    // stride 1 (3.1 -> 4.1 TB/s on MobileNetV2's s1 layers).  The stride-2
+    // instance is bit-exact too but slower than depthwise_lds_kernel there
+    // (4.3 -> 3.3 TB/s on 112x112 s2: one plane and 98 threads per block), so
+    // it is not dispatched.
+    static const bool dw4_on = [] {
+      const char* e = getenv("RTENHIP_DW4");  // A/B experiments: 0 disables
+      return !(e && atoi(e) == 0);
+    }();
+    const int pr = (OW - 1) * sw + (kw - 1) * dw + 1 - W - pl;  // right padding actually read
+    const bool al16 = ((uintptr_t)x | (uintptr_t)y | (uintptr_t)residual) % 16 == 0;
+    Dw4Geom g4;
+    if (dw4_on && kh == 3 && kw == 3 && dh == 1 && dw == 1 && sh == 1 && sw == 1 && al16 &&
+        dw4_geometry(H, W, OH, OW, sh, pt, pl, pr, g4)) {
+      dim3 grid((unsigned)((OH + g4.RS * DW4_TR - 1) / (g4.RS * DW4_TR)), (unsigned)((planes + g4.PB - 1) / g4.PB));
+      if (grid.y <= 65535) {
+        const int threads = (g4.PB * g4.RS * (OW / 4) + 63) / 64 * 64;
+        if (sh == 1)
+          hipLaunchKernelGGL(depthwise_lds4_kernel<1>, grid, dim3(threads), g4.lds, s, x, w, bias, y, planes, C,
+                             H, W, OH, OW, pt, pl, g4.RS, g4.PB, g4.rows_in, b, residual, act, lo, hi);
+        else
+          hipLaunchKernelGGL(depthwise_lds4_kernel<2>, grid, dim3(threads), g4.lds, s, x, w, bias, y, planes, C,
+                             H, W, OH, OW, pt, pl, g4.RS, g4.PB, g4.rows_in, b, residual, act, lo, hi);
+        RTENHIP_LAUNCH_CHECK();
+        return RTENHIP_OK;
+      }
+    }
     // LDS tiling (depthwise_lds_kernel): PB planes x OW columns of threads,
     // TH output rows each, at most 16 KB of staged input per block.
-    const int planes = N * C;
     if (OW <= 256 && kh * kw <= 64) {
       const int PB = 256 / OW;
       auto rows_for = [&](int th) { return (th - 1) * sh + (kh - 1) * dh + 1; };

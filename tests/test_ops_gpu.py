@@ -154,6 +154,14 @@ CONV_CASES = [
     ("depthwise-s2", (2, 96, 13, 13), (96, 3, 3), (1, 1, 1, 1), (2, 2), (1, 1), 96),
     ("depthwise-pad3-s2", (1, 4, 10, 10), (4, 3, 3), (3, 3, 3, 3), (2, 2), (1, 1), 4),
     ("pointwise-O1-gemv", (2, 20, 6, 6), (1, 1, 1), (0, 0, 0, 0), (1, 1), (1, 1), 1),
+    # 4-output-column depthwise kernel (OW % 4 == 0): s1 / s2, row slices that
+    # do not divide OH, asymmetric and zero left padding.
+    ("depthwise4-s1-28", (2, 24, 28, 28), (24, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 24),
+    ("depthwise4-s1-56", (1, 8, 56, 56), (8, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 8),
+    ("depthwise4-s2-56", (2, 16, 56, 56), (16, 3, 3), (1, 1, 1, 1), (2, 2), (1, 1), 16),
+    ("depthwise4-s2-112", (1, 4, 112, 112), (4, 3, 3), (1, 1, 1, 1), (2, 2), (1, 1), 4),
+    ("depthwise4-ragged-rows", (1, 3, 46, 12), (3, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 3),
+    ("depthwise4-pad-br", (1, 6, 24, 24), (6, 3, 3), (0, 0, 2, 2), (1, 1), (1, 1), 6),
 ]
 
 
@@ -167,6 +175,18 @@ def test_conv_bitexact(rh, oracle, case):
     got = host(rh.conv(dev(x), dev(w), dev(b), padding=pads, groups=groups, strides=strides,
                        dilations=dil))
     assert_bits(got, exp, name)
+
+
+def test_depthwise4_fused_residual_clip(rh, oracle):
+    """4-column depthwise kernel with the fused residual Add and Clip epilogue."""
+    x = rnd(oracle, 35, 2, 16, 28, 28)
+    w = rnd(oracle, 36, 16, 1, 3, 3, scale=0.3)
+    b = rnd(oracle, 37, 16)
+    res = rnd(oracle, 38, 2, 16, 28, 28)
+    exp = oracle.clip(oracle.add(oracle.conv(x, w, b, pads=(1, 1, 1, 1), groups=16), res), 0.0, 0.4)
+    got = host(rh.conv(dev(x), dev(w), dev(b), padding=(1, 1, 1, 1), groups=16, residual=dev(res),
+                       act="clip", act_range=(0.0, 0.4)))
+    assert_bits(got, exp, "depthwise4 residual clip")
 
 
 def test_conv_fused_residual_relu(rh, oracle):
