@@ -308,14 +308,27 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ y, int planes, int C, int H, int W, int OH, int OW, int kh_, int kw_,
     int sh, int sw, int dh, int dw, int pt, int pl, int TH, int PB, int rows_in, DwBounds b,
-    const float* __restrict__ residual, int act, float lo, float hi) {
+    const float* __restrict__ residual, int act, float lo, float hi, int flat) {
   extern __shared__ float tile[];
   const int plane0 = blockIdx.y * PB;
   const int oy0 = blockIdx.x * TH;
-  const int iy_lo = oy0 * sh - pt;  // input row held in tile row 0
+  const int iy_lo = oy0 * sh - pt;  // first input row the block's outputs read
   const int np = min(PB, planes - plane0);
   const int r0 = max(iy_lo, 0), r1 = min(iy_lo + rows_in, H);
-  if (r1 > r0) {
+  // Tile layout: plane pp's input row iy at tile + pp * pst + (iy - ibase) * W.
+  // flat (whole planes per block, PB * H * W % 4 == 0, 16-byte aligned x):
+  // the block's planes are one contiguous range of x, copied as is with
+  // 16-byte loads -- the small planes of MobileNetV2's last stages (rows of
+  // 14 or 7 floats) need no per-row split.
+  const int pst = flat ? H * W : rows_in * W;
+  const int ibase = flat ? 0 : iy_lo;
+  if (flat) {
+    const int n = np * H * W, n4 = n >> 2;
+    const float4* src = reinterpret_cast<const float4*>(x + (int64_t)plane0 * H * W);
+#pragma unroll 4
+    for (int t = threadIdx.x; t < n4; t += blockDim.x) reinterpret_cast<float4*>(tile)[t] = src[t];
+    for (int t = 4 * n4 + (int)threadIdx.x; t < n; t += blockDim.x) tile[t] = x[(int64_t)plane0 * H * W + t];
+  } else if (r1 > r0) {
     const int span = (r1 - r0) * W;
     if ((W & 3) == 0 && ((uintptr_t)x & 15) == 0) {
       // 16-byte copies, several in flight per thread (loads are batched
@@ -377,7 +390,7 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
       float win[3][3];
       auto load_row = [&](int slot, int iy) __attribute__((always_inline)) {
         const bool ok = iy >= 0 && iy < H;
-        const float* row = tile + (pp * rows_in + (ok ? iy - iy_lo : 0)) * W + cbase;
+        const float* row = tile + pp * pst + (ok ? iy - ibase : 0) * W + cbase;
 #pragma unroll
         for (int kx = 0; kx < 3; kx++) win[slot][kx] = (ok && colok[kx]) ? row[kx] : 0.f;
       };
@@ -428,7 +441,7 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
     for (int ky = 0; ky < (KH ? KH : kh); ky++) {
       const int iy = oy * sh + ky * dh;
       if (iy < pt || iy >= H + pt) continue;
-      const float* row = tile + (pp * rows_in + (iy - pt - iy_lo)) * W + ox * sw - pl;
+      const float* row = tile + pp * pst + (iy - pt - ibase) * W + ox * sw - pl;
 #pragma unroll
       for (int kx = 0; kx < (KW ? KW : kw); kx++) {
         if (ox < b.omin[kx] || ox >= b.omax[kx]) continue;
@@ -648,18 +661,26 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
       }();
       while (TH > 1 && PB * rows_for(TH) * W > budget) TH = (TH + 1) / 2;
       const int rows_in = rows_for(TH);
-      const size_t lds = (size_t)PB * rows_in * W * sizeof(float);
+      static const bool flat_on = [] {
+        const char* e = getenv("RTENHIP_DW_FLAT");  // A/B experiments: 0 disables
+        return !(e && atoi(e) == 0);
+      }();
+      // Whole planes per block, rows not a multiple of 4 floats: stage the
+      // block's contiguous planes with 16-byte copies (see the kernel).
+      const int flat = flat_on && TH == OH && (W & 3) != 0 && ((int64_t)PB * H * W) % 4 == 0 &&
+                       ((uintptr_t)x & 15) == 0;
+      const size_t lds = (size_t)PB * (flat ? std::max(rows_in, H) : rows_in) * W * sizeof(float);
       dim3 grid((unsigned)((OH + TH - 1) / TH), (unsigned)((planes + PB - 1) / PB));
       if (lds <= 64 * 1024 && grid.y <= 65535) {
         const int threads = (PB * OW + 63) / 64 * 64;
         if (kh == 3 && kw == 3)
           hipLaunchKernelGGL((depthwise_lds_kernel<3, 3>), grid, dim3(threads), lds, s, x, w, bias,
                              y, planes, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, TH, PB,
-                             rows_in, b, residual, act, lo, hi);
+                             rows_in, b, residual, act, lo, hi, flat);
         else
           hipLaunchKernelGGL((depthwise_lds_kernel<0, 0>), grid, dim3(threads), lds, s, x, w, bias,
                              y, planes, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, TH, PB,
-                             rows_in, b, residual, act, lo, hi);
+                             rows_in, b, residual, act, lo, hi, flat);
         RTENHIP_LAUNCH_CHECK();
         return RTENHIP_OK;
       }

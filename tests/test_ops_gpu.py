@@ -162,6 +162,10 @@ CONV_CASES = [
     ("depthwise4-s2-112", (1, 4, 112, 112), (4, 3, 3), (1, 1, 1, 1), (2, 2), (1, 1), 4),
     ("depthwise4-ragged-rows", (1, 3, 46, 12), (3, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 3),
     ("depthwise4-pad-br", (1, 6, 24, 24), (6, 3, 3), (0, 0, 2, 2), (1, 1), (1, 1), 6),
+    # whole-plane staging of rows of 14 / 7 floats (16-byte copies of the
+    # block's contiguous planes), incl. a last block whose range ends mid-float4
+    ("depthwise-flat-14", (2, 32, 14, 14), (32, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 32),
+    ("depthwise-flat-7-tail", (2, 19, 7, 7), (19, 3, 3), (1, 1, 1, 1), (1, 1), (1, 1), 19),
 ]
 
 
