@@ -6,7 +6,9 @@ plan-time tuner's candidate launches; this keeps only the steady state: the
 trailing dispatches, cut into forwards by the period of the kernel-name
 sequence, and reports per kernel (template arguments dropped) the time and
 launches per forward and the average launch duration.
-usage: rocprof_per_forward.py run_kernel_trace.csv [forwards]"""
+usage: rocprof_per_forward.py run_kernel_trace.csv [forwards] [min_period]
+(min_period: dispatches per forward at least -- BERT's layers repeat inside a
+forward, so its period is given as 12 layers x 13 dispatches = 156)"""
 import csv
 import re
 import sys
@@ -21,12 +23,13 @@ def short(name):
 def main():
     path = sys.argv[1]
     want = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    min_period = int(sys.argv[3]) if len(sys.argv) > 3 else 4
     rows = [r for r in csv.DictReader(open(path)) if "rocclr" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     # smallest period p of the trailing sequence that repeats at least twice
     period = None
-    for p in range(4, len(names) // 2 + 1):
+    for p in range(min_period, len(names) // 2 + 1):
         if names[-p:] == names[-2 * p:-p]:
             period = p
             break
