@@ -197,15 +197,21 @@ def main():
         kernel_desc = "MatMul GEMM launches (gemm_mfma_kernel / gemm_dma_kernel)"
         data = "synthetic (U[-0.5,0.5) hidden states resident in HBM; seeded U(+-0.05) weights)"
     else:
-        cfg_idx = {"resnet50": 1 if B == 64 and world == 1 else 4, "mobilenet_v2": 2}[args.model]
-        workload = (f"{spec.name} f32 batch={B} per GPU, 224x224 NCHW, BN folded "
-                    f"(BASELINE.json configs[{cfg_idx}])")
+        if args.model == "mobilenet_v2":
+            cfg = "BASELINE.json configs[2]"
+        elif B == 64:
+            cfg = "BASELINE.json configs[1]" if world == 1 else "BASELINE.json configs[4]: 64 per GPU"
+        elif B == 1:
+            cfg = "BASELINE.json metric batch=1 on the GPU path; replicas only for N > 1"
+        else:
+            cfg = "not a BASELINE.json config"
+        workload = f"{spec.name} f32 batch={B} per GPU, 224x224 NCHW, BN folded ({cfg})"
         kernel_desc = ("gemm_dma_kernel (all 53 Conv launches) + FC Gemm" if args.model == "resnet50"
                        else "Conv (DMA GEMM + depthwise) + FC Gemm")
         data = "synthetic (U[0,1) images resident in HBM; seeded He-uniform weights)"
     if rank == 0:
         line = {
-            "metric": {"resnet50": "images/sec ResNet-50 f32 batch=64 per GPU",
+            "metric": {"resnet50": f"images/sec ResNet-50 f32 batch={B} per GPU",
                        "mobilenet_v2": "images/sec MobileNetV2 f32",
                        "bert": "sequences/sec BERT-base encoder f32"}[args.model],
             "value": round(value, 2),

@@ -575,6 +575,82 @@ __global__ void gemv_kernel(int64_t N, int64_t K, const float* __restrict__ a,
   out[c] = o;
 }
 
+// gemv with B in unit row stride (simd_gemv_transposed; the FC layer at batch
+// 1, B = W^T): one wavefront per output column instead of one thread.  The
+// reference's eight lane chains of a 512-deep K block are independent of the
+// other blocks' (the lanes restart at zero per block), so lane kb*8+j of a
+// pass runs chain j of block kb (8 blocks per pass, 64 FMAs each) and a wave
+// reads a column as coalesced 32-byte runs.  The __m256::sum tree is three
+// xor shuffles (each a single commutative add, as in the reference), the
+// block's remainder k's are chained by the group's first lane, and lane 0
+// folds the blocks in K order (alpha*acc + eb*out, eb = beta then 1).  Columns
+// in a chunk's partial 8-wide tile take simd_gemv_fallback on lane 0.
+__global__ __launch_bounds__(256) void gemv_t_kernel(int64_t N, int64_t K,
+                                                     const float* __restrict__ a,
+                                                     const float* __restrict__ b, int64_t b_cs,
+                                                     float* __restrict__ out, float alpha,
+                                                     float beta, const float* __restrict__ bias,
+                                                     int64_t bbs) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= N) return;  // whole wave
+  const int64_t start = c / bbs * bbs;
+  const int64_t width = min(bbs, N - start);
+  const bool tiled = c < start + width / 8 * 8;
+  const float* col = b + c * b_cs;
+  float o = beta == 0.f ? 0.f : out[c];
+  float eb = beta;
+  constexpr int64_t KB = 512;
+  const int64_t nkb = (K + KB - 1) / KB;
+  if (!tiled) {
+    if (lane == 0)
+      for (int64_t k0 = 0; k0 < K; k0 += KB) {
+        const int64_t k1 = min(K, k0 + KB);
+        float acc = 0.f;
+        for (int64_t k = k0; k < k1; k++) acc = __fmaf_rn(a[k], col[k], acc);
+        acc = __fmul_rn(acc, alpha);
+        o = eb == 0.f ? acc : __fadd_rn(acc, __fmul_rn(eb, o));
+        eb = 1.f;
+      }
+  } else {
+    const int j = lane & 7, g = lane >> 3;
+    for (int64_t kb0 = 0; kb0 < nkb; kb0 += 8) {
+      const int64_t kb = kb0 + g;
+      const int64_t k0 = kb * KB;
+      const int64_t k1 = kb < nkb ? min(K, k0 + KB) : k0;
+      const int64_t nfull = (k1 - k0) / 8 * 8;
+      float l = 0.f;
+      int64_t d = 0;
+      for (; d + 64 <= nfull; d += 64) {
+        float av[8], bv[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          av[t] = a[k0 + d + 8 * t + j];
+          bv[t] = col[k0 + d + 8 * t + j];
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) l = __fmaf_rn(av[t], bv[t], l);
+      }
+      for (; d < nfull; d += 8) l = __fmaf_rn(a[k0 + d + j], col[k0 + d + j], l);
+      l = __fadd_rn(l, __shfl_xor(l, 4));
+      l = __fadd_rn(l, __shfl_xor(l, 2));
+      float acc = __fadd_rn(l, __shfl_xor(l, 1));
+      if (j == 0)
+        for (int64_t k = k0 + nfull; k < k1; k++) acc = __fmaf_rn(a[k], col[k], acc);
+      const int nb = (int)(nkb - kb0 < 8 ? nkb - kb0 : 8);
+      for (int q = 0; q < nb; q++) {
+        const float r = __shfl(acc, q * 8);
+        o = eb == 0.f ? __fmul_rn(alpha, r) : __fadd_rn(__fmul_rn(alpha, r), __fmul_rn(eb, o));
+        eb = 1.f;
+      }
+    }
+  }
+  if (lane == 0) {
+    if (bias) o = __fadd_rn(o, bias[0]);
+    out[c] = o;
+  }
+}
+
 rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b, int64_t b_rs,
                            int64_t b_cs, float* out, float alpha, float beta, const float* bias,
                            int64_t ref_threads, hipStream_t s) {
@@ -585,6 +661,13 @@ rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b,
   int64_t t = ref_threads > 0 ? ref_threads : 1;
   int64_t bbs = (N + t - 1) / t;
   if (bbs < 128) bbs = 128;
+  if (N <= 0) return RTENHIP_OK;
+  if (b_rs == 1) {
+    hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, N, K, a, b,
+                       b_cs, out, alpha, beta, bias, bbs);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   hipLaunchKernelGGL(gemv_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, K, a, b,
                      b_rs, b_cs, out, alpha, beta, bias, bbs);
   RTENHIP_LAUNCH_CHECK();

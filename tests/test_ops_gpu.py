@@ -118,7 +118,11 @@ def test_gemm_transposed_views(rh, oracle):
 
 
 @pytest.mark.parametrize("n,k,transposed", [(1000, 2048, True), (1000, 2048, False), (37, 13, True),
-                                            (300, 700, False), (129, 9, True)])
+                                            (300, 700, False), (129, 9, True),
+                                            # wave-per-column kernel: > 8 K blocks (two passes),
+                                            # a ragged last block, depth < 8, partial tiles
+                                            (1000, 4617, True), (130, 1003, True), (77, 5, True),
+                                            (2, 512, True), (260, 4096, True)])
 def test_gemv_bitexact(rh, oracle, n, k, transposed):
     """M == 1 takes the reference's gemv path and summation order."""
     a = rnd(oracle, 9, 1, k)
@@ -131,6 +135,20 @@ def test_gemv_bitexact(rh, oracle, n, k, transposed):
     bd = dev(b.T).t() if transposed else dev(b)
     got = host(rh.gemm(dev(a), bd, bias=dev(bias)))
     assert_bits(got, exp, "gemv")
+
+
+@pytest.mark.parametrize("alpha,beta", [(0.5, 0.75), (1.0, 1.0), (-2.0, 0.0)])
+def test_gemv_transposed_alpha_beta(rh, oracle, alpha, beta):
+    """simd_gemv_transposed with alpha / beta: beta scales the prior output on
+    the first K block only, then blocks accumulate with 1.0 (gemm.rs:651-704)."""
+    n, k = 203, 1500
+    a = rnd(oracle, 12, 1, k)
+    b = rnd(oracle, 13, n, k).T
+    out0 = rnd(oracle, 14, 1, n)
+    exp = oracle.gemm(a, b, alpha=alpha, beta=beta, out=out0.copy())
+    out = dev(out0)
+    rh.gemm(dev(a), dev(b.T).t(), alpha=alpha, beta=beta, out=out)
+    assert_bits(host(out), exp, "gemv alpha/beta")
 
 
 # --------------------------------------------------------------------------
