@@ -174,15 +174,32 @@ __device__ __forceinline__ float strided_sum(const float* p, int s, int n) {
   return acc;
 }
 
+// The same fold with n known at compile time: fully unrolled, so the LDS
+// reads are issued ahead under counted waits and the chain waits on adds only
+// (the runtime-n loop drains every read at each trip).
+template <int N>
+__device__ __forceinline__ float strided_sum_n(const float* p, int s) {
+  float v[N];
+#pragma unroll
+  for (int i = 0; i < N; i++) v[i] = p[i * s];
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < N; i++) acc = __fadd_rn(acc, v[i]);
+  return acc;
+}
+
 // LayerNorm for len % 8 == 0 on 16-byte aligned rows, R rows per workgroup:
 // the rows are staged in LDS with 16-byte copies, the 8-element chunk sums and
 // the 4-element groups of squares are formed in parallel into LDS as
 // [chunk][row], and thread r runs row r's two serial folds -- one VALU
 // instruction advances R rows' chains, where layer_norm_kernel spends a whole
 // wave instruction per add of one row.  Same operations in the same order.
+// LEN > 0: instance for that row length (folds fully unrolled); 0: any.
+template <int LEN>
 __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
-    const float* __restrict__ x, float* __restrict__ y, int64_t rows, int len, int R,
+    const float* __restrict__ x, float* __restrict__ y, int64_t rows, int len_arg, int R,
     const float* __restrict__ scale, const float* __restrict__ bias, float eps) {
+  const int len = LEN > 0 ? LEN : len_arg;
   extern __shared__ float4 lds4[];
   const int q = len >> 2;              // float4s per row
   const int nchunks = len >> 3;
@@ -209,7 +226,12 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   __syncthreads();
   if ((int)threadIdx.x < nr) {
     const int r = threadIdx.x;
-    stat[r] = __fdiv_rn(strided_sum(part + r, ps, nchunks), (float)len);
+    float total;
+    if constexpr (LEN > 0)
+      total = strided_sum_n<LEN / 8>(part + r, ps);
+    else
+      total = strided_sum(part + r, ps, nchunks);
+    stat[r] = __fdiv_rn(total, (float)len);
   }
   __syncthreads();
   // iter_sum of (x - mean)^2: groups of 4, then the tail.
@@ -228,7 +250,11 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   if ((int)threadIdx.x < nr) {
     const int r = threadIdx.x;
     const float mean = stat[r];
-    float sum = strided_sum(part + r, ps, ngroups);
+    float sum;
+    if constexpr (LEN > 0)
+      sum = strided_sum_n<(LEN - 1) / 4>(part + r, ps);
+    else
+      sum = strided_sum(part + r, ps, ngroups);
     for (int i = 4 * ngroups; i < len; i++) {
       const float d = __fsub_rn(xs[r * len + i], mean);
       sum = __fadd_rn(sum, __fmul_rn(d, d));
@@ -278,8 +304,12 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
     const size_t rshm = ((size_t)R * len + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float);
     if (rshm <= 64 * 1024) {
       const int64_t rblocks = (rows + R - 1) / R;
-      hipLaunchKernelGGL(layer_norm_rows_kernel, dim3((unsigned)rblocks), dim3(256), rshm, s, x, y,
-                         rows, (int)len, R, scale, bias, eps);
+      // BERT-base / BERT-large widths get the unrolled-fold instances.
+      auto kern = len == 768    ? layer_norm_rows_kernel<768>
+                  : len == 1024 ? layer_norm_rows_kernel<1024>
+                                : layer_norm_rows_kernel<0>;
+      hipLaunchKernelGGL(kern, dim3((unsigned)rblocks), dim3(256), rshm, s, x, y, rows, (int)len, R,
+                         scale, bias, eps);
       RTENHIP_LAUNCH_CHECK();
       return RTENHIP_OK;
     }
