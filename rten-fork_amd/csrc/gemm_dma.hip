@@ -119,25 +119,28 @@ namespace rtenhip {
 // (q * BM + r) * 4 + j holds row r, k = 8 * (q >> 1) + 2 * j + (q & 1), so
 // the lane owning row r and k parity (q & 1) reads the A operands of 4
 // consecutive 32x32x2 MFMA steps with one ds_read_b128.  One workgroup per
-// (m tile, kcw-wide k chunk; kcw = BK, or wider until the chunk holds 256
-// float4s): the BM rows are read as kcw*4-byte segments (float4 per
-// lane when aligned), transposed through LDS, and the chunk's kcw/BK tiles --
-// contiguous in the packed layout -- written with float4 stores.
+// (RB-row slice of an m tile, kcw-wide k chunk): the RB rows are read as
+// kcw*4-byte segments (float4 per lane when aligned), transposed through LDS,
+// and written as RB*16-byte runs (one per tile and q) with float4 stores.
+// RB < BM lets kcw grow (longer row segments per read) at the same
+// workgroup count.
 
 __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a, int64_t lda,
                                                      int M, int K, int lbm, int lbk,
-                                                     int tiles_k, int lkcw, int vec,
+                                                     int tiles_k, int lkcw, int lrb, int vec,
                                                      float* __restrict__ out) {
-  extern __shared__ float sh[];  // [kcw][BM + 1]
-  const int BM = 1 << lbm, BK = 1 << lbk, kcw = 1 << lkcw;
-  const int ld = BM + 1;
-  const int mt = blockIdx.x, kc = blockIdx.y;
+  extern __shared__ float sh[];  // [kcw][RB + 1]
+  const int BM = 1 << lbm, BK = 1 << lbk, kcw = 1 << lkcw, RB = 1 << lrb;
+  const int ld = RB + 1;
+  const int lsub = lbm - lrb;
+  const int mt = blockIdx.x >> lsub, rs = blockIdx.x & ((1 << lsub) - 1);
+  const int kc = blockIdx.y;
   const int k0 = kc * kcw;
-  const int64_t m0 = (int64_t)mt * BM;
-  // BM rows x kcw/4 float4s: 1..8 per thread (a multiple of 256 in total),
+  const int64_t m0 = (int64_t)mt * BM + (int64_t)rs * RB;
+  // RB rows x kcw/4 float4s: 1..8 per thread (a multiple of 256 in total),
   // all loads issued before the LDS stores.
   const int lq4 = lkcw - 2;
-  const int per = (BM << lq4) >> 8;
+  const int per = (RB << lq4) >> 8;
   float4 v[8];
 #pragma unroll
   for (int j = 0; j < 8; j++) {
@@ -173,16 +176,16 @@ __global__ __launch_bounds__(256) void pack_a_kernel(const float* __restrict__ a
   __syncthreads();
   const int kt0 = k0 / BK;
   const int nkt = min(kcw / BK, tiles_k - kt0);
-  float* o = out + ((int64_t)mt * tiles_k + kt0) * (int64_t)(BK * BM);
-  const int n = nkt * BK * BM;  // floats; BM % 4 == 0
-  const int ltile = lbm + lbk;  // log2(BK * BM)
-  for (int i = threadIdx.x * 4; i < n; i += 1024) {
-    const int t = i >> ltile;
-    const int rem4 = (i & ((1 << ltile) - 1)) >> 2;
-    const int q = rem4 >> lbm, r = rem4 & (BM - 1);
+  float* o = out + ((int64_t)mt * tiles_k + kt0) * (int64_t)(BK * BM) + (int64_t)rs * RB * 4;
+  const int lq = lbk - 2;            // log2(BK / 4): q values per tile
+  const int n4 = (nkt << lq) << lrb;  // float4 runs to write
+  for (int i4 = threadIdx.x; i4 < n4; i4 += 256) {
+    const int tq = i4 >> lrb, rl = i4 & (RB - 1);
+    const int t = tq >> lq, q = tq & ((1 << lq) - 1);
     const int kb = t * BK + 8 * (q >> 1) + (q & 1);  // k of j = 0, within the chunk
-    *(float4*)(o + i) = make_float4(sh[kb * ld + r], sh[(kb + 2) * ld + r], sh[(kb + 4) * ld + r],
-                                    sh[(kb + 6) * ld + r]);
+    *(float4*)(o + (int64_t)t * (BK * BM) + ((int64_t)q * BM + rl) * 4) =
+        make_float4(sh[kb * ld + rl], sh[(kb + 2) * ld + rl], sh[(kb + 4) * ld + rl],
+                    sh[(kb + 6) * ld + rl]);
   }
 }
 
@@ -196,10 +199,19 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
   const int tiles_k = (K + t.bk - 1) / t.bk;
   const int tiles_m = (M + t.bm - 1) / t.bm;
   if ((int64_t)tiles_m * tiles_k == 0) return RTENHIP_OK;
-  // Narrow k chunks (more workgroups, so reads and writes overlap across
-  // them), but at least one float4 per thread: BM * kcw / 4 >= 256.
+  // Workgroups of RB rows x kcw columns, at least one float4 per thread
+  // (RB * kcw / 4 >= 256): RB = min(BM, 32) with kcw widened towards 64 while
+  // K allows, so each row is read as >= 128-byte segments; narrow chunks
+  // give many workgroups, so reads and writes overlap across them.
+  static const int env_rb = [] {
+    const char* e = getenv("RTENHIP_PACK_RB");  // tuning experiments
+    return e ? atoi(e) : 0;
+  }();
+  int rb = env_rb > 0 ? env_rb : std::min(t.bm, 32);
+  if (rb > t.bm || (rb & (rb - 1)) != 0 || rb < 16) rb = t.bm;
   int kcw = t.bk;
-  while (t.bm * kcw < 1024) kcw *= 2;
+  while (rb * kcw < 1024) kcw *= 2;
+  while (kcw < 64 && kcw < K && rb * kcw * 2 <= 2048) kcw *= 2;
   auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
   if (kcw % t.bk != 0 || kcw > 64 || !pow2(t.bm) || t.bm < 32 || t.bm > 256 || !pow2(t.bk) || t.bk % 8 != 0 ||
       tiles_m > 0x7fffffff)
@@ -207,10 +219,10 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
   // packed output chunks are 16-byte aligned (BK * BM % 4 == 0); float4 reads
   // need 16-byte aligned rows
   const int vec = ((uintptr_t)a % 16 == 0 && lda % 4 == 0) ? 1 : 0;
-  const size_t lds = (size_t)kcw * (t.bm + 1) * sizeof(float);
-  dim3 grid((unsigned)tiles_m, (unsigned)((K + kcw - 1) / kcw));
+  const size_t lds = (size_t)kcw * (rb + 1) * sizeof(float);
+  dim3 grid((unsigned)tiles_m * (unsigned)(t.bm / rb), (unsigned)((K + kcw - 1) / kcw));
   hipLaunchKernelGGL(pack_a_kernel, grid, dim3(256), lds, s, a, lda, M, K, __builtin_ctz(t.bm),
-                     __builtin_ctz(t.bk), tiles_k, __builtin_ctz(kcw), vec, out);
+                     __builtin_ctz(t.bk), tiles_k, __builtin_ctz(kcw), __builtin_ctz(rb), vec, out);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }
