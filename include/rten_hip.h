@@ -91,6 +91,18 @@ rtenhip_status rtenhip_memcpy_h2d(rtenhip_ctx* ctx, void* dst, const void* src, 
 rtenhip_status rtenhip_memcpy_d2h(rtenhip_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* Kernel library identification: "gfx950" build tag + version. */
 const char* rtenhip_build_info(void);
+/* Thread count RTen's CPU path runs with, resolved once per context when it is
+ * created (rten::threading::thread_pool, src/threading.rs:41-62): the physical
+ * core count, or RTEN_NUM_THREADS clamped to [1, logical cores] (a value that
+ * does not parse as usize falls back to the physical count).  It changes
+ * results only where the reference's blocking depends on it: the gemv column
+ * blocks (src/gemm.rs:676), which the M == 1 GEMM path reproduces. */
+int32_t rtenhip_num_threads(rtenhip_ctx* ctx);
+/* num_cpus 1.16 on Linux (Cargo.lock:268-269): logical = CPUs in the affinity
+ * mask capped by a cgroup CPU quota (num_cpus::get); physical = the sum of
+ * "cpu cores" over distinct "physical id"s in /proc/cpuinfo, or logical when
+ * that finds none (num_cpus::get_physical).  Host only. */
+void rtenhip_cpu_counts(int32_t* logical, int32_t* physical);
 
 /* ---- shape helpers ------------------------------------------------------ */
 /* calc_output_size_and_padding (src/ops/pooling.rs:27-89).  pad_mode 0 = Fixed

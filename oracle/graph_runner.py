@@ -74,8 +74,8 @@ def run_op(node, ins):
     if t == "Where":
         return O.where(x, ins[1], ins[2])
     if t == "Cast":
-        # CastAttrs::to: 0 = Int32, 1 = Float (schema.fbs DataType)
-        to_int = int(a.get("to", 1)) == 0
+        # CastAttrs::to: 0 = Int32 (the schema default), 1 = Float (schema.fbs DataType)
+        to_int = int(a.get("to", 0)) == 0
         if to_int:
             return x.astype(np.int32) if x.dtype == np.int32 else O.cast_f32_to_i32(x)
         return x.astype(np.float32) if x.dtype == np.float32 else O.cast_i32_to_f32(x)

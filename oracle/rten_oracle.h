@@ -45,6 +45,10 @@ const char* orc_last_error(void);
  * (src/threading.rs:41-62). */
 int orc_num_threads(void);
 void orc_set_num_threads(int n);
+/* Re-resolve the thread count from RTEN_NUM_THREADS (src/threading.rs:41-62). */
+int orc_reset_threads(void);
+/* num_cpus::get / get_physical (num_cpus 1.16, Linux). */
+void orc_cpu_counts(int* logical, int* physical);
 
 /* XorShiftRng (rten-tensor/src/rng.rs:6-35): fill `out` with next_f32(). */
 void orc_xorshift_fill(uint64_t* state, float* out, int64_t n);

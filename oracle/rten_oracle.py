@@ -75,6 +75,19 @@ def set_num_threads(n: int):
     lib().orc_set_num_threads(int(n))
 
 
+def reset_num_threads() -> int:
+    """Re-resolve the thread count from RTEN_NUM_THREADS like
+    rten::threading::thread_pool (src/threading.rs:41-62)."""
+    return lib().orc_reset_threads()
+
+
+def cpu_counts():
+    """(logical, physical) as num_cpus::get / get_physical (num_cpus 1.16)."""
+    lg, ph = C.c_int(), C.c_int()
+    lib().orc_cpu_counts(C.byref(lg), C.byref(ph))
+    return lg.value, ph.value
+
+
 def xorshift(seed: int, n: int, state=None) -> np.ndarray:
     """XorShiftRng::new(seed).next_f32() x n (rten-tensor/src/rng.rs)."""
     st = C.c_uint64(seed)

@@ -9,6 +9,13 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
+#include <map>
+#include <string>
+#include <cctype>
+#include <cstdio>
+#include <cstring>
+#include <sched.h>
+#include <unistd.h>
 
 #include "common.h"
 
@@ -29,16 +36,86 @@ int fail(int code, const char* msg) {
 static int g_threads = 0;
 static std::once_flag g_threads_once;
 
-// src/threading.rs:41-62: physical cores unless RTEN_NUM_THREADS is set.  The
-// container's CPU share is what OpenMP reports (affinity / OMP_NUM_THREADS).
+// num_cpus 1.16 (Cargo.lock:268-269) on Linux.  get(): CPUs in the affinity
+// mask, capped by a cgroup CPU quota ceil(quota / period).
+static int logical_cpus() {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set)
+                                                       : (int)std::max(1L, sysconf(_SC_NPROCESSORS_ONLN));
+  long long q = -1, p = 0;
+  char mx[32] = {0};
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    if (fscanf(f, "%31s %lld", mx, &p) == 2 && strcmp(mx, "max") != 0) q = atoll(mx);
+    fclose(f);
+  } else if (FILE* fq = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+    if (fscanf(fq, "%lld", &q) != 1) q = -1;
+    fclose(fq);
+    if (FILE* fp = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+      if (fscanf(fp, "%lld", &p) != 1) p = 0;
+      fclose(fp);
+    }
+  }
+  if (q > 0 && p > 0) n = std::min<long long>(n, (q + p - 1) / p);
+  return std::max(1, n);
+}
+
+// get_physical(): sum of "cpu cores" per distinct "physical id" in
+// /proc/cpuinfo (pairs taken as they complete), else get().
+static int physical_cpus() {
+  std::map<unsigned, int> per_socket;
+  FILE* f = fopen("/proc/cpuinfo", "r");
+  if (f) {
+    char line[512];
+    unsigned pid = 0;
+    int cores = 0, seen = 0;
+    while (fgets(line, sizeof line, f)) {
+      char* colon = strchr(line, ':');
+      if (!colon) continue;
+      *colon = 0;
+      std::string key(line), val(colon + 1);
+      while (!key.empty() && isspace((unsigned char)key.back())) key.pop_back();
+      while (!val.empty() && isspace((unsigned char)val.back())) val.pop_back();
+      while (!val.empty() && isspace((unsigned char)val.front())) val.erase(0, 1);
+      char* end = nullptr;
+      if (key == "physical id") {
+        pid = (unsigned)strtoul(val.c_str(), &end, 10);
+        if (val.empty() || *end) break;
+        seen++;
+      } else if (key == "cpu cores") {
+        cores = (int)strtol(val.c_str(), &end, 10);
+        if (val.empty() || *end) break;
+        seen++;
+      }
+      if (seen == 2) {
+        per_socket[pid] = cores;
+        seen = 0;
+      }
+    }
+    fclose(f);
+  }
+  int total = 0;
+  for (auto& kv : per_socket) total += kv.second;
+  return total > 0 ? total : logical_cpus();
+}
+
+// src/threading.rs:41-62: physical cores, or RTEN_NUM_THREADS (a usize)
+// clamped to [1, logical]; an unparsable value means physical.
+static int resolve_threads() {
+  const char* s = getenv("RTEN_NUM_THREADS");
+  if (s) {
+    const char* d = *s == '+' ? s + 1 : s;
+    bool ok = *d != 0 && strlen(d) < 19;
+    for (const char* c = d; ok && *c; c++) ok = *c >= '0' && *c <= '9';
+    if (ok) return (int)std::max(1LL, std::min<long long>(atoll(d), logical_cpus()));
+  }
+  return physical_cpus();
+}
+
 int threads() {
   std::call_once(g_threads_once, [] {
-    int n = omp_get_max_threads();
-    if (const char* s = getenv("RTEN_NUM_THREADS")) {
-      int v = atoi(s);
-      if (v > 0) n = std::min(v, omp_get_num_procs());
-    }
-    if (g_threads == 0) g_threads = std::max(1, n);
+    if (g_threads == 0) g_threads = resolve_threads();
+    omp_set_num_threads(g_threads);
   });
   return g_threads;
 }
@@ -355,6 +432,16 @@ void orc_set_num_threads(int n) {
   threads();
   g_threads = std::max(1, n);
   omp_set_num_threads(g_threads);
+}
+int orc_reset_threads(void) {
+  threads();
+  g_threads = resolve_threads();
+  omp_set_num_threads(g_threads);
+  return g_threads;
+}
+void orc_cpu_counts(int* logical, int* physical) {
+  if (logical) *logical = logical_cpus();
+  if (physical) *physical = physical_cpus();
 }
 
 void orc_xorshift_fill(uint64_t* state, float* out, int64_t n) {

@@ -15,6 +15,7 @@
 #include "common.h"
 #include "ctx.h"
 #include "gemm_dma.h"
+#include "threads.h"
 
 namespace rtenhip {
 
@@ -36,16 +37,7 @@ rtenhip_status hip_fail(hipError_t e, const char* where) {
 
 hipStream_t stream_of(rtenhip_ctx* ctx) { return reinterpret_cast<Ctx*>(ctx)->stream; }
 
-Ctx::Ctx(int dev) : device(dev) {
-  if (const char* s = getenv("RTEN_NUM_THREADS")) {
-    int v = atoi(s);
-    if (v > 0) ref_threads = v;
-  }
-  if (ref_threads <= 0) {
-    unsigned hc = std::thread::hardware_concurrency();
-    ref_threads = hc ? (int)hc : 1;
-  }
-}
+Ctx::Ctx(int dev) : device(dev), ref_threads(rten_num_threads()) {}
 
 Ctx::~Ctx() {
   for (auto& kv : ktabs) (void)hipFree(kv.second);
@@ -740,6 +732,12 @@ rtenhip_status rtenhip_memcpy_d2h(rtenhip_ctx* ctx, void* dst, const void* src, 
   RTENHIP_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, C_(ctx)->stream));
   RTENHIP_HIP_CHECK(hipStreamSynchronize(C_(ctx)->stream));
   return RTENHIP_OK;
+}
+
+int32_t rtenhip_num_threads(rtenhip_ctx* ctx) { return C_(ctx)->ref_threads; }
+void rtenhip_cpu_counts(int32_t* logical, int32_t* physical) {
+  if (logical) *logical = logical_cpus();
+  if (physical) *physical = physical_cpus();
 }
 
 const char* rtenhip_build_info(void) { return "rten-hip gfx950 (CDNA4) f32 MFMA backend v0.1"; }

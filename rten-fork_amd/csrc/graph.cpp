@@ -69,6 +69,7 @@ Plan::~Plan() {
   if (gather_flag) (void)hipFree(gather_flag);
   for (auto& kv : convs) {
     if (kv.second.packed) (void)hipFree(kv.second.packed);
+    if (kv.second.fb_packed) (void)hipFree(kv.second.fb_packed);
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
   }
@@ -418,9 +419,10 @@ rtenhip_status Graph::infer_dtypes(int op_id, const std::vector<int>& ins, std::
   outs.assign(std::max<size_t>(1, op.outputs.size()), RTENHIP_DTYPE_FLOAT32);
   const rtenhip_status incorrect = RTENHIP_INCORRECT_INPUT_TYPE;
   if (t == "Cast") {
-    // CastAttrs::to (op_registry.rs:421-428): Int32, else Float.
-    outs[0] = op.attrs.num("to", RTENHIP_DTYPE_FLOAT32) == RTENHIP_DTYPE_INT32 ? RTENHIP_DTYPE_INT32
-                                                                               : RTENHIP_DTYPE_FLOAT32;
+    // CastAttrs::to (op_registry.rs:421-428; schema.fbs default DataType::Int32):
+    // Int32, else Float.
+    outs[0] = op.attrs.num("to", RTENHIP_DTYPE_INT32) == RTENHIP_DTYPE_INT32 ? RTENHIP_DTYPE_INT32
+                                                                             : RTENHIP_DTYPE_FLOAT32;
     return RTENHIP_OK;
   }
   if (t == "Gather") {
@@ -1270,9 +1272,32 @@ rtenhip_status Graph::exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_
   return RTENHIP_OK;
 }
 
+// Tuner scratch released on every exit path (events, candidate weight
+// buffers, a trial's split workspace and counters).
+struct TuneScratch {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<float*> bufs;
+  float** ws = nullptr;
+  int** counters = nullptr;
+  ~TuneScratch() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if ((ws && *ws) || (counters && *counters) || !bufs.empty()) (void)hipDeviceSynchronize();
+    for (float* b : bufs) (void)hipFree(b);
+    if (ws && *ws) (void)hipFree(*ws);
+    if (counters && *counters) (void)hipFree(*counters);
+  }
+};
+
 // DMA GEMM launch modes the first-run tuner times: one block per work item
 // (0) or persistent with 4 to 6 resident blocks per CU (see gemm_dma_kernel.h).
+// RTENHIP_PERSIST=k (k >= 0) restricts the tuner to launch mode k (any k >= 1
+// is a valid persistent launch: the kernel caps k at its occupancy).
 static const int kPersistModes[4] = {0, 4, 5, 6};
+static std::vector<int> persist_candidates(int forced) {
+  if (forced >= 0) return {forced};
+  return std::vector<int>(kPersistModes, kPersistModes + 4);
+}
 static const char* pers_tag(int k) {
   static const char* tags[] = {"", " pers1", " pers2", " pers3", " pers4", " pers5", " pers6"};
   return k >= 0 && k <= 6 ? tags[k] : " pers?";
@@ -1368,53 +1393,52 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
       static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
-      hipEvent_t e0, e1;
-      RTENHIP_HIP_CHECK(hipEventCreate(&e0));
-      RTENHIP_HIP_CHECK(hipEventCreate(&e1));
-      float best_ms = 1e30f;
       MatMulExec trial = me;
       trial.ws = nullptr;
       trial.counters = nullptr;
       trial.ws_floats = trial.n_counters = 0;
+      TuneScratch ts;
+      ts.ws = &trial.ws;
+      ts.counters = &trial.counters;
+      RTENHIP_HIP_CHECK(hipEventCreate(&ts.e0));
+      RTENHIP_HIP_CHECK(hipEventCreate(&ts.e1));
+      float best_ms = 1e30f;
       for (int cfg : kCandidates) {
         if (cfg >= dma_num_cfgs()) continue;
         rtenhip_status st = ensure_pack(cfg);
         if (st) return st;
-        for (int mode = 0; mode < 8; mode++) {
-          const int split = mode & 1;
-          if (split && dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg).split_tiles == 0) continue;
-          // persistent launches with 2, 3 or 4 blocks per CU, or none
-          trial.persist = kPersistModes[mode >> 1];
-          if (persist_mode >= 0 && trial.persist != persist_mode) continue;
-          st = set_split(trial, cfg, split != 0);
-          if (st) return st;
-          bind(trial, cfg);
-          st = gemm_dense_dma(ctx, da);  // warm-up (the output is rewritten below)
-          if (st) return st;
-          float ms = 1e30f;
-          for (int r = 0; r < 3; r++) {
-            RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
-            st = gemm_dense_dma(ctx, da);
+        for (int pm : persist_candidates(persist_mode)) {
+          for (int split = 0; split < 2; split++) {
+            if (split && dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg).split_tiles == 0) continue;
+            trial.persist = pm;
+            st = set_split(trial, cfg, split != 0);
             if (st) return st;
-            RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
-            RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
-            float t = 0;
-            RTENHIP_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
-            ms = std::min(ms, t);
-          }
-          if (ms < best_ms) {
-            best_ms = ms;
-            chosen = cfg;
-            chosen_split = split != 0;
-            chosen_persist = trial.persist;
+            bind(trial, cfg);
+            st = gemm_dense_dma(ctx, da);  // warm-up (the output is rewritten below)
+            if (st) return st;
+            float ms = 1e30f;
+            for (int r = 0; r < 3; r++) {
+              RTENHIP_HIP_CHECK(hipEventRecord(ts.e0, s));
+              st = gemm_dense_dma(ctx, da);
+              if (st) return st;
+              RTENHIP_HIP_CHECK(hipEventRecord(ts.e1, s));
+              RTENHIP_HIP_CHECK(hipEventSynchronize(ts.e1));
+              float t = 0;
+              RTENHIP_HIP_CHECK(hipEventElapsedTime(&t, ts.e0, ts.e1));
+              ms = std::min(ms, t);
+            }
+            if (ms < best_ms) {
+              best_ms = ms;
+              chosen = cfg;
+              chosen_split = split != 0;
+              chosen_persist = trial.persist;
+            }
           }
         }
       }
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
       RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
-      if (trial.ws) (void)hipFree(trial.ws);
-      if (trial.counters) (void)hipFree(trial.counters);
+    } else if (persist_mode >= 0) {
+      chosen_persist = persist_mode;
     }
     rtenhip_status st = ensure_pack(chosen);
     if (st) return st;
@@ -1564,11 +1588,14 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
       static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19, 20, 21, 22, 23, 24};
-      hipEvent_t e0, e1;
-      RTENHIP_HIP_CHECK(hipEventCreate(&e0));
-      RTENHIP_HIP_CHECK(hipEventCreate(&e1));
-      std::vector<float*> bufs;
       ConvExec trial;  // split buffers reused across candidates
+      TuneScratch ts;
+      ts.ws = &trial.ws;
+      ts.counters = &trial.counters;
+      RTENHIP_HIP_CHECK(hipEventCreate(&ts.e0));
+      RTENHIP_HIP_CHECK(hipEventCreate(&ts.e1));
+      hipEvent_t e0 = ts.e0, e1 = ts.e1;
+      std::vector<float*>& bufs = ts.bufs;
       // Launch times of the current binding: best of n (screening) or median
       // of n (final round).
       auto time_it = [&](int n, bool median, float& out_ms) -> rtenhip_status {
@@ -1603,12 +1630,11 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         bufs.push_back(pk);
         rtenhip_status st = pack_conv_weights(ctx, w, g, cfg, pk);
         if (st) return st;
-        for (int mode = 0; mode < 8; mode++) {
+        for (int mode = 0; mode < 2 * (int)persist_candidates(persist_mode).size(); mode++) {
           const int split = mode & 1;
           if (split && dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg).split_tiles == 0)
             continue;
-          trial.persist = kPersistModes[mode >> 1];
-          if (persist_mode >= 0 && trial.persist != persist_mode) continue;
+          trial.persist = persist_candidates(persist_mode)[mode >> 1];
           st = set_split(trial, cfg, split != 0);
           if (st) return st;
           bind(trial);
@@ -1707,12 +1733,9 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           chosen_persist = c.persist;
         }
       }
-      (void)hipEventDestroy(e0);
-      (void)hipEventDestroy(e1);
       RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
-      for (float* b : bufs) (void)hipFree(b);
-      if (trial.ws) (void)hipFree(trial.ws);
-      if (trial.counters) (void)hipFree(trial.counters);
+    } else if (persist_mode >= 0) {
+      chosen_persist = persist_mode;
     }
     RTENHIP_HIP_CHECK(hipMalloc(&ce.packed, (size_t)weight_floats(chosen) * 4));
     rtenhip_status st = pack_for(chosen, ce.packed);
@@ -1721,6 +1744,40 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     if (st) return st;
     ce.cfg = chosen;
     ce.persist = chosen >= kPwCfgBase ? 0 : persist_mode >= 0 ? persist_mode : chosen_persist;
+    if (chosen >= kPwCfgBase) {
+      ce.fb_cfg = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
+      RTENHIP_HIP_CHECK(hipMalloc(&ce.fb_packed, (size_t)packed_conv_weight_floats(g, ce.fb_cfg) * 4));
+      if ((st = pack_conv_weights(ctx, w, g, ce.fb_cfg, ce.fb_packed))) return st;
+      // The fallback's padded input copy uses ctx scratch slot 1: request it
+      // now, in the eager run, so a capture never has to grow it.
+      if (has_pad && !ctx->scratch_floats((size_t)(g.N * g.C * (g.H + g.pads[0] + g.pads[2]) *
+                                                   (g.W + g.pads[1] + g.pads[3])), 1))
+        return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    }
+  }
+  if (ce.cfg >= kPwCfgBase) {
+    // The VALU kernels take 16-byte aligned x (pointwise), y and residual; the
+    // plan was tuned on the first run's pointers, and graph inputs / outputs
+    // can be rebound to misaligned views later.
+    const bool direct = ce.cfg >= kPwCfgBase + kPwDirect;
+    const uintptr_t align = (uintptr_t)a.y | (uintptr_t)a.residual | (direct ? 0 : (uintptr_t)a.xin);
+    if (align % 16 != 0) {
+      if (direct && has_pad) {
+        a.Hp = g.H + g.pads[0] + g.pads[2];
+        a.Wp = g.W + g.pads[1] + g.pads[3];
+        float* xp = ctx->scratch_floats((size_t)(g.N * g.C * a.Hp * a.Wp), 1);
+        if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+        rtenhip_status st = launch_pad_nchw(a.x_unpadded, xp, g.N * g.C, (int)g.H, (int)g.W, (int)g.pads[0],
+                                            (int)g.pads[1], (int)g.pads[2], (int)g.pads[3], s);
+        if (st) return st;
+        a.xin = xp;
+      }
+      ConvExec none;
+      bind(none);
+      a.packed_w = ce.fb_packed;
+      a.cfg = ce.fb_cfg;
+      return conv_dma(ctx, a);
+    }
   }
   a.packed_w = ce.packed;
   a.cfg = ce.cfg;
@@ -2023,14 +2080,16 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
   }
   ctx->stream = caller;
-  if (!st && plan->gather_flag) {
-    // Gather's index check (gather.rs:52-60) completes with the run: read and
-    // clear the flag the kernels set on an out-of-range index.
+  if (plan->gather_flag) {
+    // Gather's index check (gather.rs:52-60) completes with the run: read the
+    // flag the kernels set on an out-of-range index, and clear it whatever the
+    // run's status, so a failed run cannot leave it set for the next one.
     int bad = 0;
-    RTENHIP_HIP_CHECK(hipMemcpyAsync(&bad, plan->gather_flag, sizeof(int), hipMemcpyDeviceToHost, exec_stream));
-    RTENHIP_HIP_CHECK(hipMemsetAsync(plan->gather_flag, 0, sizeof(int), exec_stream));
-    RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
-    if (bad) st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+    if (!st) RTENHIP_HIP_CHECK(hipMemcpyAsync(&bad, plan->gather_flag, sizeof(int), hipMemcpyDeviceToHost, exec_stream));
+    const hipError_t e1 = hipMemsetAsync(plan->gather_flag, 0, sizeof(int), exec_stream);
+    const hipError_t e2 = hipStreamSynchronize(exec_stream);
+    if (!st && (e1 != hipSuccess || e2 != hipSuccess)) st = hip_fail(e1 != hipSuccess ? e1 : e2, "gather flag");
+    if (!st && bad) st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
   }
   RTENHIP_HIP_CHECK(hipEventRecord(ev_out, exec_stream));
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
@@ -2295,7 +2354,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
   if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->use_side_stream = s[0] != '0';
-  if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(6, atoi(s)));
+  if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   return reinterpret_cast<rtenhip_graph*>(g);
 }

@@ -96,6 +96,11 @@ struct ConvExec {
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
   int persist = 0;          // persistent launch, blocks per CU (0: one block per item); tuned
+  // A VALU configuration (cfg >= kPwCfgBase) needs 16-byte aligned operands;
+  // a later run bound to a misaligned graph input / output view takes this
+  // DMA configuration instead (weights packed for it when the VALU one is chosen).
+  int fb_cfg = -1;
+  float* fb_packed = nullptr;
   // A Gemm (FC layer) run as this conv: x [B, K] as B images of [K, 1, 1],
   // W [O, K] (transB) as O pointwise filters, C [O] as the bias.
   bool fc = false;

@@ -83,6 +83,9 @@ def lib():
             L.rtenhip_model_describe.argtypes = [C.POINTER(C.c_uint8), C.c_size_t]
             L.rtenhip_model_input_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
             L.rtenhip_model_output_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
+            L.rtenhip_num_threads.restype = C.c_int32
+            L.rtenhip_num_threads.argtypes = [C.c_void_p]
+            L.rtenhip_cpu_counts.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
             _lib = L
     return _lib
 
@@ -105,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_plan", "rtenhip_gather_output_shape", "rtenhip_gather_f32",
     "rtenhip_where_output_shape", "rtenhip_where_f32", "rtenhip_cast_f32_to_i32",
     "rtenhip_cast_i32_to_f32", "rtenhip_graph_add_constant_i32", "rtenhip_graph_run_typed",
-    "rtenhip_graph_plan_typed",
+    "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts",
 ]
 
 # rtenhip_dtype (sg::DataType order, include/rten_hip.h)
@@ -160,6 +163,11 @@ class Context:
             raise RuntimeError(lib().rtenhip_last_error_message().decode())
         self.sync_stream()
 
+    @property
+    def num_threads(self) -> int:
+        """RTen's thread-pool size this context reproduces (src/threading.rs:41-62)."""
+        return int(lib().rtenhip_num_threads(C.c_void_p(self.ptr)))
+
     def sync_stream(self, stream=None):
         torch = _torch()
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
@@ -175,6 +183,13 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def cpu_counts():
+    """(logical, physical) CPU counts as num_cpus 1.16 reports them (host only)."""
+    lg, ph = C.c_int32(), C.c_int32()
+    lib().rtenhip_cpu_counts(C.byref(lg), C.byref(ph))
+    return lg.value, ph.value
 
 
 _default_ctx: Optional[Context] = None

@@ -201,8 +201,8 @@ def _op_attrs(op_type: str, a: dict):
     if op_type == "Gather":
         return ATTRS_GATHER, Table([(0, "i32", int(a.get("axis", 0)))])
     if op_type == "Cast":
-        # CastAttrs::to, sg::DataType: Int32 = 0, Float = 1
-        return ATTRS_CAST, Table([(0, "u8", int(a.get("to", 1)))])
+        # CastAttrs::to, sg::DataType: Int32 = 0 (the schema default), Float = 1
+        return ATTRS_CAST, Table([(0, "u8", int(a.get("to", 0)))])
     return 0, None
 
 

@@ -168,3 +168,49 @@ def test_direct_valu_bitexact(rh, monkeypatch, mode, case):
     g.run(dev, g.output_ids, out=out)
     torch.cuda.synchronize()
     assert f"cfg=valu{mode}" in g.timing_report()
+
+
+def _offset_view(arr, torch):
+    """A contiguous device copy of ``arr`` starting 4 bytes past a 16-byte
+    boundary (as an ``out=`` slice or a sliced graph input would be)."""
+    base = torch.empty(arr.size + 1, dtype=torch.float32, device="cuda")
+    v = base[1:].view(arr.shape)
+    v.copy_(torch.from_numpy(arr))
+    assert v.data_ptr() % 16 == 4
+    return v
+
+
+@pytest.mark.parametrize("mode,kh,pads", [("16", 1, [0, 0, 0, 0]), ("316", 3, [1, 1, 1, 1])])
+def test_valu_conv_rebound_to_misaligned_views(rh, monkeypatch, mode, kh, pads):
+    """A plan tuned onto a VALU conv kernel (16-byte operands) and later bound
+    to 4-byte-offset input / residual / output views runs its DMA fallback
+    instead of failing, with the same bits (eager and replayed)."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    monkeypatch.setenv("RTENHIP_PW_VALU", mode)
+    rng = np.random.default_rng(404 + kh)
+    N, C, H, W, O = 2, 3 if kh == 3 else 24, 16, 16, 32
+    m = ModelSpec("misaligned")
+    x = m.value("x")
+    r = m.value("r")
+    m.inputs = ["x", "r"]
+    w = m.const("w", rng.uniform(-0.5, 0.5, (O, C, kh, kh)).astype(np.float32))
+    b = m.const("b", rng.uniform(-0.2, 0.2, (O,)).astype(np.float32))
+    y = m.op("Relu", [m.op("Add", [m.op("Conv", [x, w, b], {"pads": pads, "strides": [1, 1]}), r])])
+    m.outputs = [y]
+    ins = {"x": rng.uniform(-1, 1, (N, C, H, W)).astype(np.float32),
+           "r": rng.uniform(-1, 1, (N, O, H, W)).astype(np.float32)}
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    aligned = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
+    out = g.run(aligned, g.output_ids)  # eager: the forced VALU kernel
+    torch.cuda.synchronize()
+    assert _bits_equal(out[0].cpu().numpy(), exp)
+    off = {g.input_ids[i]: _offset_view(ins[n], torch) for i, n in enumerate(m.inputs)}
+    y_off = _offset_view(np.zeros(exp.shape, np.float32), torch)
+    for feed in (off, off, aligned, off):  # capture + replays, rebinding each time
+        res = g.run(feed, g.output_ids, out=[y_off])
+        torch.cuda.synchronize()
+        assert _bits_equal(res[0].cpu().numpy(), exp)
