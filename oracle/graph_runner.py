@@ -7,6 +7,8 @@ from __future__ import annotations
 
 import numpy as np
 
+import extra_ops as X
+import optimizer
 import rten_oracle as O
 
 
@@ -38,7 +40,30 @@ def run_op(node, ins):
     if t in ("Relu", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu"):
         return O.unary(t, x)
     if t in ("Add", "Sub", "Mul", "Div"):
+        if np.asarray(x).dtype == np.int32 or np.asarray(ins[1]).dtype == np.int32:
+            if np.asarray(x).dtype != np.asarray(ins[1]).dtype:
+                raise O.OpError(1, "Input 1 has incorrect type")
+            return X.int_binary(t, x, ins[1])
         return O.binary(t, x, ins[1])
+    if t == "Pow":
+        return X.pow_(x, ins[1])
+    if t == "Sqrt":
+        return X.sqrt(x)
+    if t == "ReduceMean":
+        axes = a.get("axes")
+        if len(ins) > 1 and ins[1] is not None:  # get_axes: the axes input wins (reduce.rs:534-543)
+            axes = [int(v) for v in np.asarray(ins[1]).reshape(-1)]
+        return X.reduce_mean(x, axes, bool(a.get("keep_dims", 0)))
+    if t == "Shape":
+        return X.shape(x)
+    if t == "ConstantOfShape":
+        return X.constant_of_shape(x, a.get("value", 0))
+    if t == "Concat":
+        return X.concat(ins, int(a.get("axis", 0)))
+    if t == "Slice":
+        return X.slice_(x, ins[1], ins[2], ins[3] if len(ins) > 3 else None, ins[4] if len(ins) > 4 else None)
+    if t == "Expand":
+        return X.expand(x, ins[1])
     if t == "MaxPool":
         return O.max_pool(x, a["kernel_size"], a.get("strides", (1, 1)), a.get("pads", (0, 0, 0, 0)))
     if t == "AveragePool":
@@ -94,13 +119,56 @@ def run_op(node, ins):
     raise NotImplementedError(t)
 
 
-def run(spec, inputs: dict, outputs=None):
-    """inputs: {value name: np.ndarray}; returns {output name: np.ndarray}."""
+_OPT_CACHE = {}
+
+
+def optimized(spec):
+    """The graph RTen runs after Model::load's optimizer (oracle/optimizer.py),
+    cached per spec object."""
+    key = id(spec)
+    hit = _OPT_CACHE.get(key)
+    if hit is None or hit[0] is not spec:
+        hit = (spec, optimizer.optimize(spec, _run_node))
+        _OPT_CACHE[key] = hit
+    return hit[1]
+
+
+def _run_node(n, ins):
+    if n.op_type == "Clip":
+        env = {}
+        names = []
+        for k, v in enumerate(ins):
+            env[f"#{k}"] = v
+            names.append(f"#{k}" if v is not None else None)
+        lo, hi = _clip_bounds(env, type("N", (), {"inputs": names, "attrs": n.attrs})())
+        return O.clip(ins[0], lo, hi)
+    return run_op(n, ins)
+
+
+def _live(spec, outs):
+    prod = {o: n for n in spec.nodes if n.kind == "op" for o in n.outputs}
+    seen, stack = set(), list(outs)
+    while stack:
+        n = prod.get(stack.pop())
+        if n is not None and n.name not in seen:
+            seen.add(n.name)
+            stack.extend(i for i in n.inputs if i is not None)
+    return seen
+
+
+def run(spec, inputs: dict, outputs=None, optimize: bool = True):
+    """inputs: {value name: np.ndarray}; returns {output name: np.ndarray}.
+    optimize: run the graph as RTen's optimizer leaves it (the default of
+    ModelOptions, src/model.rs:155-207), or as stored."""
+    if optimize:
+        spec = optimized(spec)
+    outs = outputs or spec.outputs
+    live = _live(spec, outs)
     env = {n.name: n.data for n in spec.nodes if n.kind == "const"}
     env.update({k: np.ascontiguousarray(v, np.int32 if np.asarray(v).dtype == np.int32 else np.float32)
                 for k, v in inputs.items()})
     for n in spec.nodes:
-        if n.kind != "op":
+        if n.kind != "op" or n.name not in live:
             continue
         if n.op_type == "Clip":
             lo, hi = _clip_bounds(env, n)
@@ -108,5 +176,4 @@ def run(spec, inputs: dict, outputs=None):
             continue
         ins = [env[i] if i is not None else None for i in n.inputs]
         env[n.outputs[0]] = run_op(n, ins)
-    outs = outputs or spec.outputs
     return {o: env[o] for o in outs}

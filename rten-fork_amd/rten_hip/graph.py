@@ -188,7 +188,8 @@ class ModelSpec:
         """Constant node: int32 arrays stay int32 (IntData), others are f32."""
         data = np.asarray(data)
         dt = np.int32 if data.dtype == np.int32 else np.float32
-        self.nodes.append(Node("const", name, data=np.ascontiguousarray(data, dt)))
+        # np.array (not ascontiguousarray) keeps 0-d scalars 0-d
+        self.nodes.append(Node("const", name, data=np.array(data, dt, order="C", copy=True)))
         return name
 
     def op(self, op_type: str, inputs: Sequence[Optional[str]], attrs: Optional[dict] = None,

@@ -173,7 +173,7 @@ BERT_BASE_GFLOP_PER_SEQ128 = 22.347  # SURVEY.md App. A.3 (encoder, seq 128)
 def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int = 3072,
                  seq: int = 128, eps: float = 1e-12, seed: int = 4321, embeddings: bool = False,
                  vocab: int = 30522, max_pos: int = 512, type_vocab: int = 2,
-                 mask_op: str = "mul") -> ModelSpec:
+                 mask_op: str = "mul", unfused: bool = False) -> ModelSpec:
     """BERT-base encoder stack in the operator mix of an ONNX export as RTen
     runs it after its own fusions (GELU and LayerNormalization fused,
     src/optimize.rs): per layer Q/K/V MatMul+Add, Reshape/Transpose to heads,
@@ -193,8 +193,19 @@ def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int 
     [B, S]): word / position / token-type Gathers, their sum and
     LayerNormalization; the 0/1 mask becomes the additive one through
     Unsqueeze x2 -> Cast(Float) -> Sub(1, .) -> Mul(-10000) (``mask_op="mul"``,
-    the classic export) or Where(mask, 0, -10000) (``mask_op="where"``)."""
-    m = ModelSpec(("bert_base" if layers == 12 else f"bert_l{layers}") + ("_emb" if embeddings else ""))
+    the classic export) or Where(mask, 0, -10000) (``mask_op="where"``).
+
+    ``unfused=True`` emits the graph as an ONNX export hands it to RTen,
+    before RTen's optimizer (src/optimize.rs:286-518) runs: LayerNorm as
+    ReduceMean(-1) / Sub / Pow(2) / ReduceMean(-1) / Add(eps) / Sqrt / Div /
+    Mul(gamma) / Add(beta), GELU as nn.GELU's Div(sqrt 2) / Erf / Add(1) / Mul /
+    Mul(0.5), the head split and merge reshapes through a Shape -> Gather ->
+    Unsqueeze -> Concat shape subgraph, the position ids as a Slice of a
+    [1, max_pos] buffer up to the input's sequence length, and the attention
+    scale as Sqrt of a constant (folded by constant propagation).  After the
+    optimizer it is the fused graph, weights and bits included."""
+    m = ModelSpec(("bert_base" if layers == 12 else f"bert_l{layers}") + ("_emb" if embeddings else "") +
+                  ("_onnx" if unfused else ""))
     rng = np.random.default_rng(seed)
     dh = hidden // heads
     if embeddings:
@@ -203,7 +214,18 @@ def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int 
         wte = m.const("emb.word", rng.uniform(-0.05, 0.05, (vocab, hidden)).astype(np.float32))
         wpe = m.const("emb.position", rng.uniform(-0.05, 0.05, (max_pos, hidden)).astype(np.float32))
         wtt = m.const("emb.token_type", rng.uniform(-0.05, 0.05, (type_vocab, hidden)).astype(np.float32))
-        pos_ids = m.const("emb.position_ids", np.arange(seq, dtype=np.int32).reshape(1, seq))
+        if unfused:
+            # position_ids[:, :seq_len] of the registered [1, max_pos] buffer
+            buf = m.const("emb.position_ids", np.arange(max_pos, dtype=np.int32).reshape(1, max_pos))
+            ishape = m.op("Shape", [ids], name="emb.ids.shape")
+            slen = m.op("Gather", [ishape, m.const("emb.idx1", np.array(1, np.int32))], {"axis": 0},
+                        name="emb.seq_len")
+            slen = m.op("Unsqueeze", [slen, m.const("emb.axes0", np.array([0], np.int32))],
+                        name="emb.seq_len.unsqueeze")
+            pos_ids = m.op("Slice", [buf, m.const("emb.start0", np.array([0], np.int32)), slen,
+                                     m.const("emb.axes1", np.array([1], np.int32))], name="emb.position_ids.slice")
+        else:
+            pos_ids = m.const("emb.position_ids", np.arange(seq, dtype=np.int32).reshape(1, seq))
         e = m.op("Gather", [wte, ids], {"axis": 0}, name="emb.word.gather")
         e = m.op("Add", [e, m.op("Gather", [wtt, types], {"axis": 0}, name="emb.type.gather")],
                  name="emb.add_type")
@@ -211,7 +233,7 @@ def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int 
                  name="emb.add_pos")
         g0 = m.const("emb.ln.gamma", (1.0 + rng.uniform(-0.1, 0.1, (hidden,))).astype(np.float32))
         b0 = m.const("emb.ln.beta", rng.uniform(-0.1, 0.1, (hidden,)).astype(np.float32))
-        x = m.op("LayerNormalization", [e, g0, b0], {"axis": -1, "epsilon": eps}, name="emb.ln")
+        x = _layer_norm(m, "emb.ln", e, g0, b0, eps, unfused)
         ax1 = m.const("mask.axes1", np.array([1], np.int32))
         ax2 = m.const("mask.axes2", np.array([2], np.int32))
         mk = m.op("Unsqueeze", [am, ax1], name="mask.unsqueeze1")
@@ -239,17 +261,37 @@ def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int 
     def ln(name, h):
         g = m.const(f"{name}.gamma", (1.0 + rng.uniform(-0.1, 0.1, (hidden,))).astype(np.float32))
         b = m.const(f"{name}.beta", rng.uniform(-0.1, 0.1, (hidden,)).astype(np.float32))
-        return m.op("LayerNormalization", [h, g, b], {"axis": -1, "epsilon": eps}, name=name)
+        return _layer_norm(m, name, h, g, b, eps, unfused)
 
-    shape_heads = m.const("shape.heads", np.array([0, 0, heads, dh], np.float32))
-    shape_merge = m.const("shape.merge", np.array([0, 0, hidden], np.float32))
-    scale = m.const("attn.scale", np.array([np.sqrt(dh)], np.float32))
+    if unfused:
+        # scale = Sqrt(d_head) computed in the graph (constant propagation folds it)
+        scale = m.op("Sqrt", [m.const("attn.d_head", np.array(float(dh), np.float32))], name="attn.scale")
+        c_heads = m.const("shape.heads_dh", np.array([heads, dh], np.int32))
+        c_hidden = m.const("shape.hidden", np.array([hidden], np.int32))
+        idx0 = m.const("shape.idx0", np.array(0, np.int32))
+        idx1 = m.const("shape.idx1", np.array(1, np.int32))
+        ax0 = m.const("shape.axes0", np.array([0], np.int32))
+
+        def dyn_shape(name, t, tail):
+            # torch's x.size()[:2] + tail as ONNX exports it
+            sh = m.op("Shape", [t], name=f"{name}.shape")
+            d0 = m.op("Unsqueeze", [m.op("Gather", [sh, idx0], {"axis": 0}, name=f"{name}.d0"), ax0],
+                      name=f"{name}.d0u")
+            d1 = m.op("Unsqueeze", [m.op("Gather", [sh, idx1], {"axis": 0}, name=f"{name}.d1"), ax0],
+                      name=f"{name}.d1u")
+            return m.op("Concat", [d0, d1, tail], {"axis": 0}, name=f"{name}.concat")
+    else:
+        shape_heads = m.const("shape.heads", np.array([0, 0, heads, dh], np.float32))
+        shape_merge = m.const("shape.merge", np.array([0, 0, hidden], np.float32))
+        scale = m.const("attn.scale", np.array([np.sqrt(dh)], np.float32))
     h = x
     for i in range(layers):
         p = f"layer{i}"
         q = lin(f"{p}.q", h, hidden, hidden)
         k = lin(f"{p}.k", h, hidden, hidden)
         v = lin(f"{p}.v", h, hidden, hidden)
+        if unfused:
+            shape_heads = dyn_shape(f"{p}.heads", q, c_heads)
         q = m.op("Reshape", [q, shape_heads], name=f"{p}.q.reshape")
         q = m.op("Transpose", [q], {"perm": [0, 2, 1, 3]}, name=f"{p}.q.transpose")
         k = m.op("Reshape", [k, shape_heads], name=f"{p}.k.reshape")
@@ -262,15 +304,42 @@ def bert_encoder(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int 
         s = m.op("Softmax", [s], {"axis": -1}, name=f"{p}.softmax")
         c = m.op("MatMul", [s, v], name=f"{p}.av")
         c = m.op("Transpose", [c], {"perm": [0, 2, 1, 3]}, name=f"{p}.ctx.transpose")
+        if unfused:
+            shape_merge = dyn_shape(f"{p}.merge", c, c_hidden)
         c = m.op("Reshape", [c, shape_merge], name=f"{p}.ctx.reshape")
         a = lin(f"{p}.attn_out", c, hidden, hidden)
         h1 = ln(f"{p}.ln1", m.op("Add", [a, h], name=f"{p}.res1"))
         f = lin(f"{p}.ffn1", h1, hidden, ffn)
-        f = m.op("Gelu", [f], name=f"{p}.gelu")
+        f = _gelu(m, f"{p}.gelu", f, unfused)
         f = lin(f"{p}.ffn2", f, ffn, hidden)
         h = ln(f"{p}.ln2", m.op("Add", [f, h1], name=f"{p}.res2"))
     m.outputs = [h]
     return m
+
+
+def _layer_norm(m: ModelSpec, name, x, gamma, beta, eps, unfused):
+    """LayerNormalization, or torch.onnx's decomposition of it (opset < 17)."""
+    if not unfused:
+        return m.op("LayerNormalization", [x, gamma, beta], {"axis": -1, "epsilon": eps}, name=name)
+    mean = m.op("ReduceMean", [x], {"axes": [-1], "keep_dims": 1}, name=f"{name}.mean")
+    d = m.op("Sub", [x, mean], name=f"{name}.sub")
+    var = m.op("ReduceMean", [m.op("Pow", [d, m.const(f"{name}.two", np.array(2.0, np.float32))],
+                                   name=f"{name}.pow")], {"axes": [-1], "keep_dims": 1}, name=f"{name}.var")
+    den = m.op("Sqrt", [m.op("Add", [var, m.const(f"{name}.eps", np.array(eps, np.float32))],
+                             name=f"{name}.add_eps")], name=f"{name}.sqrt")
+    y = m.op("Div", [d, den], name=f"{name}.div")
+    return m.op("Add", [m.op("Mul", [y, gamma], name=f"{name}.mul"), beta], name=name)
+
+
+def _gelu(m: ModelSpec, name, x, unfused):
+    """Gelu, or nn.GELU as ONNX exports it: x * (erf(x / sqrt 2) + 1) * 0.5."""
+    if not unfused:
+        return m.op("Gelu", [x], name=name)
+    e = m.op("Erf", [m.op("Div", [x, m.const(f"{name}.sqrt2", np.array(np.sqrt(2.0), np.float32))],
+                          name=f"{name}.div")], name=f"{name}.erf")
+    a = m.op("Add", [e, m.const(f"{name}.one", np.array(1.0, np.float32))], name=f"{name}.add")
+    return m.op("Mul", [m.op("Mul", [x, a], name=f"{name}.mul"),
+                        m.const(f"{name}.half", np.array(0.5, np.float32))], name=name)
 
 
 def bert_flops(layers: int = 12, hidden: int = 768, heads: int = 12, ffn: int = 3072,
