@@ -41,32 +41,41 @@ def parse():
     p.add_argument("--model", default="resnet50", choices=["resnet50", "mobilenet_v2", "bert"])
     p.add_argument("--seq", type=int, default=128, help="BERT sequence length")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--timing-report", action="store_true")
     return p.parse_args()
 
 
-def cpu_baseline(spec, seconds: float):
-    """Time the CPU oracle (restated RTen CPU path) on ResNet-50 batch 1."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
+def cpu_baseline(spec, seconds: float, batch: int, feed_fn):
+    """Time the CPU oracle (RTen's CPU algorithm restated in C++: BLIS 6x16
+    AVX2-FMA GEMM, KC = 256, per-image conv parallelism, VirtualIm2Col offset
+    tables with masked gathers) on the benchmark's own config and batch.
 
-    import graph_runner
+    RTen sizes its pool to the physical cores (src/threading.rs:41-62); on a
+    box whose CPU share is smaller than the machine, that would oversubscribe
+    the share, so RTEN_NUM_THREADS is set to the share (OMP_NUM_THREADS when
+    the box sets it, else the logical count) -- an RTen-supported setting --
+    and all three counts are reported."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import rten_oracle
 
-    x = np.random.default_rng(99).random((1, 3, 224, 224), dtype=np.float32)
-    graph_runner.run(spec, {"input": x})  # warm-up
+    logical, physical = rten_oracle.cpu_counts()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or logical
+    os.environ["RTEN_NUM_THREADS"] = str(min(share, logical))
+    threads = rten_oracle.reset_num_threads()
+    import graph_runner
+
+    feed = feed_fn()
+    graph_runner.run(spec, feed)  # warm-up (also builds the optimized graph)
     times = []
     t_end = time.time() + seconds
-    while time.time() < t_end or len(times) < 3:
+    while time.time() < t_end or len(times) < 2:
         t0 = time.perf_counter()
-        graph_runner.run(spec, {"input": x})
+        graph_runner.run(spec, feed)
         times.append(time.perf_counter() - t0)
     times.sort()
     med = times[len(times) // 2]
-    import platform
-
-    cpu_model = platform.processor() or "unknown"
+    cpu_model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
             if line.startswith("model name"):
@@ -74,14 +83,19 @@ def cpu_baseline(spec, seconds: float):
                 break
     except OSError:
         pass
+    unit = "sequences/s" if spec.name.startswith("bert") else "images/s"
     return {
-        "value": round(1.0 / med, 3),
-        "unit": "images/s",
-        "cores": rten_oracle.num_threads(),
+        "value": round(batch / med, 3),
+        "unit": unit,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{spec.name} batch 1, {len(times)} runs in ~{seconds:.0f}s, median "
-                  f"{med * 1e3:.1f} ms; restated RTen algorithm (C++ BLIS 6x16 AVX2-FMA, "
-                  f"KC=256), not the Rust binary; host CPU: {cpu_model}",
+        "logical_cpus": logical,
+        "physical_cores": physical,
+        "sample": f"{spec.name} batch {batch} (the benchmark config), {len(times)} runs in ~{seconds:.0f}s, "
+                  f"median {med * 1e3:.1f} ms per batch; restated RTen algorithm (C++ BLIS 6x16 "
+                  f"AVX2-FMA, KC=256, im2col offset tables + masked gathers), not the Rust binary; "
+                  f"{threads} threads (RTEN_NUM_THREADS); host: {cpu_model}, {logical} logical CPUs "
+                  f"(num_cpus::get), {physical} physical cores (num_cpus::get_physical)",
     }
 
 
@@ -122,19 +136,23 @@ def main():
     ctx = rten_hip.Context(torch.cuda.current_device())
     B = args.batch
     rng = np.random.default_rng(1234 + rank)
-    extra = {}
     if args.model == "bert":
-        spec = models.bert_encoder(seq=args.seq)
+        # rten-cli's inputs for a BERT .rten (rten-cli/src/main.rs:250-259):
+        # *_ids -> zeros, *_mask -> ones; the embedding Gathers and the mask
+        # subgraph run inside the timed step.
+        spec = models.bert_encoder(seq=args.seq, embeddings=True)
         flops_per_img = models.bert_flops(seq=args.seq)
-        x = torch.from_numpy(rng.random((B, args.seq, 768), dtype=np.float32) - 0.5).cuda()
-        mask = torch.zeros((B, 1, 1, args.seq), dtype=torch.float32).cuda()
+        feed_np = {"input_ids": np.zeros((B, args.seq), np.int32),
+                   "token_type_ids": np.zeros((B, args.seq), np.int32),
+                   "attention_mask": np.ones((B, args.seq), np.int32)}
     else:
         spec = models.resnet50() if args.model == "resnet50" else models.mobilenet_v2()
         flops_per_img = models.conv_flops(spec, 1)
-        x = torch.from_numpy(rng.random((B, 3, 224, 224), dtype=np.float32)).cuda()
+        feed_np = {"input": rng.random((B, 3, 224, 224), dtype=np.float32)}
     g = spec.to_graph(ctx)
-    if args.model == "bert":
-        extra = {g.input_ids[1]: mask}
+    dev = [torch.from_numpy(feed_np[n]).cuda() for n in spec.inputs]
+    x = dev[0]
+    extra = {g.input_ids[i]: dev[i] for i in range(1, len(dev))}
     (out,) = g.run({g.input_ids[0]: x, **extra}, g.output_ids)  # plans + tunes conv kernels
 
     from rten_hip.parallel import BatchShardRunner
@@ -190,12 +208,17 @@ def main():
     conv_ms /= n_prof
     gemm_flops = flops_per_img * B
     achieved = gemm_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    hbm_bound = args.model == "mobilenet_v2"
+    if hbm_bound:
+        io_bytes = models.conv_io_bytes(spec, B)
+        achieved_gbs = io_bytes / (conv_ms * 1e-3) / 1e9 if conv_ms > 0 else 0.0
 
     if args.model == "bert":
         workload = (f"{spec.name} encoder f32 batch={B} per GPU, seq {args.seq}, hidden 768, "
-                    f"12 heads, FFN 3072 (BASELINE.json configs[3])")
-        kernel_desc = "MatMul GEMM launches (gemm_mfma_kernel / gemm_dma_kernel)"
-        data = "synthetic (U[-0.5,0.5) hidden states resident in HBM; seeded U(+-0.05) weights)"
+                    f"12 heads, FFN 3072, embeddings + mask subgraph (BASELINE.json configs[3])")
+        kernel_desc = "MatMul GEMM launches (gemm_dma_kernel) + FusedAttention"
+        data = ("synthetic (rten-cli inputs: input_ids / token_type_ids zeros, attention_mask ones, "
+                "resident in HBM; seeded U(+-0.05) weights)")
     else:
         if args.model == "mobilenet_v2":
             cfg = "BASELINE.json configs[2]"
@@ -207,8 +230,23 @@ def main():
             cfg = "not a BASELINE.json config"
         workload = f"{spec.name} f32 batch={B} per GPU, 224x224 NCHW, BN folded ({cfg})"
         kernel_desc = ("gemm_dma_kernel (all 53 Conv launches) + FC Gemm" if args.model == "resnet50"
-                       else "Conv (DMA GEMM + depthwise) + FC Gemm")
+                       else "all Conv launches (DMA GEMM / VALU pointwise / depthwise) + FC Gemm")
         data = "synthetic (U[0,1) images resident in HBM; seeded He-uniform weights)"
+    if hbm_bound:
+        roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved_gbs / HBM_PEAK_GBPS, 4), "traffic": traffic_bytes(args.model, B),
+                    "kernel": kernel_desc, "bytes_per_step": io_bytes,
+                    "kernel_ms_per_step": round(conv_ms, 4),
+                    "mfma_tflops": round(achieved, 2)}
+    else:
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2),
+                    "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
+                    "traffic": traffic_bytes(args.model, B),
+                    "kernel": kernel_desc,
+                    "flops_per_step": gemm_flops,
+                    "kernel_ms_per_step": round(conv_ms, 4),
+                    "model_frac": round(value / world * flops_per_img / 1e12 / F32_MFMA_PEAK_TFLOPS, 4)}
     if rank == 0:
         line = {
             "metric": {"resnet50": f"images/sec ResNet-50 f32 batch={B} per GPU",
@@ -229,18 +267,10 @@ def main():
                        "model": spec.name, "global_batch": world * B,
                        "seq_len": args.seq if args.model == "bert" else None,
                        "parallelism": f"batch-shard x{world} (replicated weights, RCCL all-gather of logits)"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2),
-                         "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4),
-                         "traffic": traffic_bytes(args.model, B),
-                         "kernel": kernel_desc,
-                         "flops_per_step": gemm_flops,
-                         "kernel_ms_per_step": round(conv_ms, 4),
-                         "model_frac": round(value / world * flops_per_img / 1e12 /
-                                             F32_MFMA_PEAK_TFLOPS, 4)},
+            "roofline": roofline,
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(spec, args.cpu_seconds, B, lambda: feed_np)
         if args.timing_report:
             sys.stderr.write(report + "\n")
         print(json.dumps(line), flush=True)

@@ -202,6 +202,7 @@ typedef enum {
   RTENHIP_UNARY_TANH = 5,
   RTENHIP_UNARY_EXP = 6,
   RTENHIP_UNARY_SILU = 7,
+  RTENHIP_UNARY_SQRT = 8, /* Sqrt (unary_elementwise.rs:653): correctly rounded */
 } rtenhip_unary_op;
 rtenhip_status rtenhip_unary_f32(rtenhip_ctx* ctx, int op, const rtenhip_tensor* x, float p0,
                                  float p1, rtenhip_tensor* y);
@@ -212,9 +213,23 @@ typedef enum {
   RTENHIP_BINARY_SUB = 1,
   RTENHIP_BINARY_MUL = 2,
   RTENHIP_BINARY_DIV = 3,
+  /* Pow (binary_elementwise.rs:742-770): exponent 2 -> x*x, 3 -> x*x*x (the
+   * reference's fast paths, bit-exact); any other exponent is computed in
+   * double precision and rounded once, within 1 ULP of the libm powf the
+   * reference calls (not bit-pinned). */
+  RTENHIP_BINARY_POW = 4,
 } rtenhip_binary_op;
 rtenhip_status rtenhip_binary_f32(rtenhip_ctx* ctx, int op, const rtenhip_tensor* a,
                                   const rtenhip_tensor* b, rtenhip_tensor* y);
+
+/* ReduceMean (src/ops/reduce.rs:225-400): mean over `axes` (n_axes == 0: all
+ * axes) of a contiguous f32 tensor, in the reference's summation order: the
+ * 8-wide slice_sum for a reduction over the last axis, the 4-wide iter_sum
+ * otherwise (slice_reductions.rs:38-85), divided by the element count.  y has
+ * the reduced shape (keep_dims: reduced axes kept as 1).  Errors "Axis is
+ * invalid", "Cannot reduce empty tensor". */
+rtenhip_status rtenhip_reduce_mean_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, const int32_t* axes,
+                                       int32_t n_axes, int keep_dims, rtenhip_tensor* y);
 
 /* ---- graph executor (Graph::run, src/graph.rs:733-1073) ------------------ */
 typedef struct rtenhip_graph rtenhip_graph;
@@ -300,6 +315,14 @@ const char* rtenhip_model_describe(const uint8_t* bytes, size_t len);
 int32_t rtenhip_model_input_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
 int32_t rtenhip_model_output_ids(rtenhip_graph* g, int32_t* ids, int32_t cap);
 int32_t rtenhip_graph_node_id(rtenhip_graph* g, const char* name);
+/* The graph as it stands (after rtenhip_graph_optimize): one line per node,
+ * tab-separated -- "id\top\tname\tOperatorName\tin,ids\tout,ids" for each
+ * operator still in the graph, with RTen's Operator::name() after its fusions
+ * (optimize.rs:286-518: "Gelu", "LayerNormalization", "Silu",
+ * "FusedTranspose(MatMul)"; device fusions as "FusedAttention" or the base
+ * operator), "id\tconst\tname\tdims" (dims "AxB...", after constant
+ * propagation too) and "id\tvalue\tname".  Host only. */
+const char* rtenhip_graph_describe(rtenhip_graph* g);
 
 /* ---- Index / select / convert (BERT embedding and mask path) ---- */
 

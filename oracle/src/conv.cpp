@@ -5,6 +5,7 @@
 // Follows src/ops/conv.rs:24-280 (dispatcher, pointwise, im2col path),
 // src/ops/conv/im2col.rs:75-260 (VirtualIm2Col), src/ops/conv/depthwise.rs:24-203
 // and src/ops/pooling.rs:27-375.
+#include <immintrin.h>
 #include <omp.h>
 
 #include <algorithm>
@@ -14,32 +15,64 @@
 
 namespace orc {
 
-// VirtualIm2Col (im2col.rs:44-181): row r = (c, ky, kx), col = (oy, ox).
+// VirtualIm2Col (im2col.rs:44-260): row r = (c, ky, kx), col = (oy, ox).
+// VirtualIm2Col::new (im2col.rs:75-181): offset tables built once per conv
+// geometry -- per row the channel, y and x offsets, per column (padded to a
+// multiple of the panel width) the patch corner's y and x offsets, all
+// premultiplied by the image strides -- plus the largest valid y / x offsets.
+struct Im2ColTables {
+  std::vector<int32_t> row_chan, row_y, row_x;
+  std::vector<int32_t> col_y, col_x;
+  int32_t max_y = 0, max_x = 0;
+  Im2ColTables(int64_t C, int64_t H, int64_t W, int64_t kh, int64_t kw, int64_t sh, int64_t sw, int64_t dh,
+               int64_t dw, int64_t pt, int64_t pl, int64_t oh, int64_t ow, int64_t panel) {
+    for (int64_t c = 0; c < C; c++)
+      for (int64_t ky = 0; ky < kh; ky++)
+        for (int64_t kx = 0; kx < kw; kx++) {
+          row_chan.push_back((int32_t)(c * H * W));
+          row_y.push_back((int32_t)(W * ky * dh));
+          row_x.push_back((int32_t)(kx * dw));
+        }
+    const int64_t n_cols = oh * ow, padded = (n_cols + panel - 1) / panel * panel;
+    for (int64_t col = 0; col < padded; col++) {
+      const int64_t py = col / ow, px = col % ow;
+      col_y.push_back((int32_t)((py * sh - pt) * W));
+      col_x.push_back((int32_t)(px * sw - pl));
+    }
+    max_y = (int32_t)((H - 1) * W);
+    max_x = (int32_t)(W - 1);
+  }
+};
+
 struct Im2Col : VirtualB {
   const float* img;  // [C,H,W] contiguous
-  int64_t C, H, W, kh, kw, sh, sw, dh, dw, pt, pl, oh, ow;
-  int64_t rows() const override { return C * kh * kw; }
-  int64_t cols() const override { return oh * ow; }
+  const Im2ColTables* t;
+  int64_t n_rows, n_cols;
+  int64_t rows() const override { return n_rows; }
+  int64_t cols() const override { return n_cols; }
+  // pack_b_impl (im2col.rs:190-260) for the AVX2 kernel (NR = 16 = 2 x 8
+  // lanes): per column panel, per row, a masked gather of 8 lanes twice;
+  // offsets in the padding region read as 0.
   void pack_b(float* out, int64_t nr, int64_t k0, int64_t k1, int64_t c0,
               int64_t c1) const override {
-    int64_t c1p = c0 + (c1 - c0 + nr - 1) / nr * nr;
-    int64_t n_rows = k1 - k0;
+    const int64_t c1p = c0 + (c1 - c0 + nr - 1) / nr * nr;
+    const __m256i zero = _mm256_setzero_si256(), neg1 = _mm256_set1_epi32(-1);
+    const __m256i ymax1 = _mm256_set1_epi32(t->max_y + 1), xmax1 = _mm256_set1_epi32(t->max_x + 1);
+    float* o = out;
     for (int64_t pc = c0; pc < c1p; pc += nr) {
-      float* po = out + (pc - c0) / nr * n_rows * nr;
-      int64_t iy0[64], ix0[64];
-      for (int64_t j = 0; j < nr; j++) {
-        int64_t col = pc + j;
-        int64_t py = col / ow, px = col % ow;
-        iy0[j] = py * sh - pt;
-        ix0[j] = px * sw - pl;
-      }
       for (int64_t r = k0; r < k1; r++) {
-        int64_t c = r / (kh * kw), ky = (r / kw) % kh, kx = r % kw;
-        const float* chan = img + c * H * W;
-        float* o = po + (r - k0) * nr;
-        for (int64_t j = 0; j < nr; j++) {
-          int64_t y = iy0[j] + ky * dh, x = ix0[j] + kx * dw;
-          o[j] = (y >= 0 && y < H && x >= 0 && x < W) ? chan[y * W + x] : 0.f;
+        const __m256i rc = _mm256_set1_epi32(t->row_chan[r]), ry = _mm256_set1_epi32(t->row_y[r]),
+                      rx = _mm256_set1_epi32(t->row_x[r]);
+        for (int64_t i = 0; i < nr; i += 8) {
+          const __m256i y = _mm256_add_epi32(_mm256_loadu_si256((const __m256i*)(t->col_y.data() + pc + i)), ry);
+          const __m256i x = _mm256_add_epi32(_mm256_loadu_si256((const __m256i*)(t->col_x.data() + pc + i)), rx);
+          const __m256i off = _mm256_add_epi32(rc, _mm256_add_epi32(y, x));
+          const __m256i ok = _mm256_and_si256(
+              _mm256_and_si256(_mm256_cmpgt_epi32(y, neg1), _mm256_cmpgt_epi32(ymax1, y)),
+              _mm256_and_si256(_mm256_cmpgt_epi32(x, neg1), _mm256_cmpgt_epi32(xmax1, x)));
+          const __m256 v = _mm256_mask_i32gather_ps(_mm256_castsi256_ps(zero), img, off, _mm256_castsi256_ps(ok), 4);
+          _mm256_storeu_ps(o, v);
+          o += 8;
         }
       }
     }
@@ -165,23 +198,15 @@ static int conv2d(const float* x, const int64_t xs[4], const float* w, const int
     // Per-image parallelism (conv.rs:243-270, par_bridge).  Each image's
     // GEMM then runs on its worker; summation order is unaffected.
     bool par_images = N > 1;
+    const Im2ColTables tables(ipg, H, W, kh, kw, strides[0], strides[1], dil[0], dil[1], pads[0], pads[1], oh,
+                              ow, 16);
 #pragma omp parallel for schedule(dynamic, 1) if (par_images)
     for (int64_t n = 0; n < N; n++) {
       Im2Col im;
       im.img = x + (n * C + g * ipg) * H * W;
-      im.C = ipg;
-      im.H = H;
-      im.W = W;
-      im.kh = kh;
-      im.kw = kw;
-      im.sh = strides[0];
-      im.sw = strides[1];
-      im.dh = dil[0];
-      im.dw = dil[1];
-      im.pt = pads[0];
-      im.pl = pads[1];
-      im.oh = oh;
-      im.ow = ow;
+      im.t = &tables;
+      im.n_rows = ipg * kh * kw;
+      im.n_cols = oh * ow;
       gemm_impl(y + (n * O + g * opg) * P, P, A, nullptr, &im, 1.f, 0.f, gb, par_images);
     }
   }

@@ -144,6 +144,21 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s);
 rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s);
+// Strided view -> strided view copy of 4-byte elements (either dtype).
+rtenhip_status launch_copy_view(const float* src, const int64_t* shape, const int64_t* src_strides, int ndim,
+                                float* dst, const int64_t* dst_strides, hipStream_t s);
+rtenhip_status launch_fill(void* y, int64_t n, uint32_t bits, hipStream_t s);
+// ReduceMean (norm.hip): rows of `len` contiguous elements in slice_sum order,
+// or per output element an iter_sum over a strided sub-block (up to 8 kept
+// and 8 reduced dims).
+rtenhip_status launch_reduce_mean_rows(const float* x, float* y, int64_t rows, int64_t len, hipStream_t s);
+struct ReduceDesc {
+  int nk, nr;  // kept / reduced dims
+  int64_t kshape[RTENHIP_MAX_DIMS], kstride[RTENHIP_MAX_DIMS];
+  int64_t rshape[RTENHIP_MAX_DIMS], rstride[RTENHIP_MAX_DIMS];
+  int64_t n_out, n_red;
+};
+rtenhip_status launch_reduce_mean_iter(const float* x, float* y, const ReduceDesc& d, hipStream_t s);
 // col2im of ConvTranspose (conv.rs:329-375): col [N, O*kh*kw, H, W] -> y
 // [N, O, OH, OW], each output = bias (or 0) + its columns in (ky, kx) order.
 rtenhip_status launch_col2im(const float* col, const float* bias, float* y, int64_t N, int64_t O,

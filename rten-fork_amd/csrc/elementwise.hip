@@ -20,6 +20,7 @@ __device__ __forceinline__ float unary_apply(float v, float p0, float p1) {
   if constexpr (OP == RTENHIP_UNARY_TANH) return vm_tanh(v);
   if constexpr (OP == RTENHIP_UNARY_EXP) return vm_exp(v);
   if constexpr (OP == RTENHIP_UNARY_SILU) return __fmul_rn(v, vm_sigmoid(v));
+  if constexpr (OP == RTENHIP_UNARY_SQRT) return sqrt_rn(v);
   return v;
 }
 
@@ -69,6 +70,7 @@ rtenhip_status launch_unary(int op, const float* x, float* y, int64_t n, float p
     CASE(RTENHIP_UNARY_TANH)
     CASE(RTENHIP_UNARY_EXP)
     CASE(RTENHIP_UNARY_SILU)
+    CASE(RTENHIP_UNARY_SQRT)
 #undef CASE
     default:
       return fail(RTENHIP_UNSUPPORTED_VALUE, "Unsupported unary op");
@@ -82,6 +84,12 @@ __device__ __forceinline__ float binary_apply(float a, float b) {
   if constexpr (OP == RTENHIP_BINARY_ADD) return __fadd_rn(a, b);
   if constexpr (OP == RTENHIP_BINARY_SUB) return __fsub_rn(a, b);
   if constexpr (OP == RTENHIP_BINARY_MUL) return __fmul_rn(a, b);
+  if constexpr (OP == RTENHIP_BINARY_POW) {
+    // powf with the reference's fast paths (binary_elementwise.rs:742-751)
+    if (b == 2.f) return __fmul_rn(a, a);
+    if (b == 3.f) return __fmul_rn(__fmul_rn(a, a), a);
+    return (float)pow((double)a, (double)b);
+  }
   return __fdiv_rn(a, b);
 }
 
@@ -137,6 +145,9 @@ rtenhip_status launch_binary(int op, const float* a, const float* b, float* y, i
       break;
     case RTENHIP_BINARY_DIV:
       hipLaunchKernelGGL(binary_kernel<RTENHIP_BINARY_DIV>, g, bl, 0, s, a, b, y, n, d, mode, inner, nb);
+      break;
+    case RTENHIP_BINARY_POW:
+      hipLaunchKernelGGL(binary_kernel<RTENHIP_BINARY_POW>, g, bl, 0, s, a, b, y, n, d, mode, inner, nb);
       break;
     default:
       return fail(RTENHIP_UNSUPPORTED_VALUE, "Unsupported binary op");
@@ -254,6 +265,59 @@ rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStr
     d.strides[i] = src.strides[i];
   }
   hipLaunchKernelGGL(copy_strided_kernel, stream_grid(n, 1), dim3(256), 0, s, src.data, dst, n, d);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+// Strided view -> strided view copy of 4-byte elements (Concat's blocks,
+// Slice / Expand views into a strided destination).
+struct ViewDesc {
+  int ndim;
+  int64_t shape[RTENHIP_MAX_DIMS];
+  int64_t src[RTENHIP_MAX_DIMS];
+  int64_t dst[RTENHIP_MAX_DIMS];
+};
+__global__ void copy_view_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, ViewDesc d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    int64_t rem = i, so = 0, dof = 0;
+    for (int k = d.ndim - 1; k >= 0; k--) {
+      const int64_t idx = rem % d.shape[k];
+      rem /= d.shape[k];
+      so += idx * d.src[k];
+      dof += idx * d.dst[k];
+    }
+    y[dof] = x[so];
+  }
+}
+
+rtenhip_status launch_copy_view(const float* src, const int64_t* shape, const int64_t* src_strides, int ndim,
+                                float* dst, const int64_t* dst_strides, hipStream_t s) {
+  int64_t n = 1;
+  for (int i = 0; i < ndim; i++) n *= shape[i];
+  if (n == 0) return RTENHIP_OK;
+  if (ndim > RTENHIP_MAX_DIMS) return fail(RTENHIP_UNSUPPORTED_VALUE, "too many dims");
+  ViewDesc d{};
+  d.ndim = ndim;
+  for (int i = 0; i < ndim; i++) {
+    d.shape[i] = shape[i];
+    d.src[i] = src_strides[i];
+    d.dst[i] = dst_strides[i];
+  }
+  hipLaunchKernelGGL(copy_view_kernel, stream_grid(n, 1), dim3(256), 0, s, src, dst, n, d);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+// ConstantOfShape on the device (generate.rs:28-42): every element = v.
+__global__ void fill_kernel(uint32_t* __restrict__ y, int64_t n, uint32_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = v;
+}
+
+rtenhip_status launch_fill(void* y, int64_t n, uint32_t bits, hipStream_t s) {
+  if (n == 0) return RTENHIP_OK;
+  hipLaunchKernelGGL(fill_kernel, stream_grid(n, 1), dim3(256), 0, s, static_cast<uint32_t*>(y), n, bits);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

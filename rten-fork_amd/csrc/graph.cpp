@@ -67,6 +67,8 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 
 Plan::~Plan() {
   if (gather_flag) (void)hipFree(gather_flag);
+  for (auto& kv : host_dev)
+    if (kv.second) (void)hipFree(kv.second);
   for (auto& kv : convs) {
     if (kv.second.packed) (void)hipFree(kv.second.packed);
     if (kv.second.fb_packed) (void)hipFree(kv.second.fb_packed);
@@ -159,11 +161,30 @@ int Graph::add_node(Node n) {
 }
 
 // Constant scalar from a small host copy (Clip min/max, Reshape shape).
+// Values of a constant, or of a plan-time value of the plan being made (shape
+// inputs of Reshape / Unsqueeze / Expand ..., Clip bounds), as floats.
 static bool const_values(const Graph& g, int id, std::vector<float>& out) {
   if (id < 0 || id >= (int)g.nodes.size()) return false;
   const Node& n = g.nodes[id];
-  if (n.kind != NodeKind::Constant || n.host_small.empty()) return false;
-  out = n.host_small;
+  if (n.kind == NodeKind::Constant && !n.host_small.empty()) {
+    out = n.host_small;
+    return true;
+  }
+  HostVal tmp;
+  const HostVal* hv = g.host_value(id, tmp);
+  if (!hv) return false;
+  out.resize(hv->raw.size());
+  for (size_t k = 0; k < hv->raw.size(); k++)
+    out[k] = hv->dtype == RTENHIP_DTYPE_INT32 ? (float)(int32_t)hv->raw[k] : HostVal::u2f(hv->raw[k]);
+  return true;
+}
+// The same as integers (exact for int32 values).
+static bool int_values(const Graph& g, int id, std::vector<int64_t>& out) {
+  HostVal tmp;
+  const HostVal* hv = id >= 0 ? g.host_value(id, tmp) : nullptr;
+  if (!hv) return false;
+  out.resize(hv->raw.size());
+  for (size_t k = 0; k < hv->raw.size(); k++) out[k] = hv->i(k);
   return true;
 }
 
@@ -302,14 +323,14 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
     if (axis < 0 || axis > (int64_t)x.size()) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
     outs[0] = {prod(x, 0, axis), prod(x, axis)};
   } else if (t == "Reshape") {
-    std::vector<float> sv;
-    if (!const_values(*this, op.inputs.size() > 1 ? op.inputs[1] : -1, sv))
+    std::vector<int64_t> sv;
+    if (!int_values(*this, op.inputs.size() > 1 ? op.inputs[1] : -1, sv))
       return fail(RTENHIP_UNSUPPORTED_VALUE, "Reshape needs a constant shape");
     Shape s;
     int infer = -1;
     int64_t known = 1;
     for (size_t i = 0; i < sv.size(); i++) {
-      int64_t d = (int64_t)sv[i];
+      int64_t d = sv[i];
       if (d == 0 && op.attrs.num("allowzero", 0) == 0) d = i < x.size() ? x[i] : 0;
       if (d == -1) {
         infer = (int)i;
@@ -393,11 +414,88 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
     outs[0].clear();
     for (size_t i = 0; i < x.size(); i++)
       if (!drop[i]) outs[0].push_back(x[i]);
+  } else if (t == "Pow") {
+    if ((st = need(1))) return st;
+    const Shape& b = *in(1);
+    int64_t os[RTENHIP_MAX_DIMS];
+    int on;
+    if (!broadcast_shapes(x.data(), (int)x.size(), b.data(), (int)b.size(), os, &on))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast inputs");
+    outs[0].assign(os, os + on);
+  } else if (t == "Shape") {
+    outs[0] = {(int64_t)x.size()};
+  } else if (t == "ReduceMean") {
+    // reduce (reduce.rs:225-330): axes from input 1 when present (get_axes,
+    // reduce.rs:534-543), else the attribute; none / empty = all axes.
+    std::vector<int64_t> axes;
+    const int ai = op.inputs.size() > 1 ? op.inputs[1] : -1;
+    if (ai >= 0) {
+      if (!int_values(*this, ai, axes)) return fail(RTENHIP_UNSUPPORTED_VALUE, "ReduceMean needs constant axes");
+    } else {
+      axes = op.attrs.ints("axes", {});
+    }
+    const int64_t nd = (int64_t)x.size();
+    std::vector<bool> red(x.size(), axes.empty());
+    for (int64_t a : axes) {
+      if (a < -nd || a >= nd) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+      red[a < 0 ? a + nd : a] = true;
+    }
+    if (nd > 0 && prod(x) == 0) return fail(RTENHIP_INVALID_VALUE, "Cannot reduce empty tensor");
+    const bool keep = op.attrs.num("keep_dims", 0) != 0;
+    outs[0].clear();
+    for (size_t d = 0; d < x.size(); d++)
+      if (!red[d]) outs[0].push_back(x[d]);
+      else if (keep) outs[0].push_back(1);
+  } else if (t == "ConstantOfShape") {
+    std::vector<int64_t> sv;
+    if (!int_values(*this, op.inputs[0], sv))
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "ConstantOfShape needs a shape known at plan time");
+    if (x.size() != 1) return fail(RTENHIP_INVALID_VALUE, "Input 0 has wrong number of dims");
+    outs[0].assign(sv.begin(), sv.end());
+    for (int64_t d : outs[0])
+      if (d < 0) return fail(RTENHIP_INVALID_VALUE, "Shape values must be non-negative");
+  } else if (t == "Concat") {
+    // concatenated_shape (concat.rs:15-41)
+    int64_t axis = (int64_t)op.attrs.num("axis", 0);
+    if (axis < -(int64_t)x.size() || axis >= (int64_t)x.size()) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+    if (axis < 0) axis += (int64_t)x.size();
+    outs[0] = x;
+    for (size_t i = 1; i < ins.size(); i++) {
+      if (!ins[i]) return fail(RTENHIP_MISSING_INPUTS, "Missing required input");
+      const Shape& o = *ins[i];
+      if (o.size() != x.size())
+        return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Tensors must have the same number of dimensions");
+      for (size_t d = 0; d < x.size(); d++) {
+        if ((int64_t)d == axis) outs[0][d] += o[d];
+        else if (o[d] != x[d])
+          return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Dimensions must be the same except for concat axis");
+      }
+    }
+  } else if (t == "Slice") {
+    if ((st = need(1)) || (st = need(2))) return st;
+    int64_t base;
+    std::vector<int64_t> dims, sst;
+    if (!slice_view(*this, op, x, base, dims, sst, st)) {
+      if (st) return st;
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Slice needs starts / ends / axes / steps known at plan time");
+    }
+    outs[0].assign(dims.begin(), dims.end());
+  } else if (t == "Expand") {
+    // expand_output_shape (layout.rs:17-26)
+    std::vector<int64_t> sv;
+    if (!int_values(*this, op.inputs.size() > 1 ? op.inputs[1] : -1, sv))
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "Expand needs a shape known at plan time");
+    int64_t os[RTENHIP_MAX_DIMS];
+    int on;
+    if (sv.size() > RTENHIP_MAX_DIMS ||
+        !broadcast_shapes(x.data(), (int)x.size(), sv.data(), (int)sv.size(), os, &on))
+      return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Cannot broadcast input with target shape");
+    outs[0].assign(os, os + on);
   } else {
     // Shape-preserving ops: unary activations, BatchNormalization,
     // LayerNormalization, Softmax, Identity, Cast.
     static const std::set<std::string> same = {
-        "Relu", "Clip", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu", "BatchNormalization",
+        "Relu", "Clip", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu", "Sqrt", "BatchNormalization",
         "LayerNormalization", "Softmax", "Identity", "Cast"};
     if (!same.count(t)) {
       std::string msg = "Unsupported operator type: " + t;
@@ -439,23 +537,45 @@ rtenhip_status Graph::infer_dtypes(int op_id, const std::vector<int>& ins, std::
   // Shape ops move 4-byte elements of either type; their extra inputs (shape,
   // axes) are int32 in the reference.
   if (t == "Identity" || t == "Flatten" || t == "Transpose" || t == "Reshape" || t == "Unsqueeze" ||
-      t == "Squeeze") {
+      t == "Squeeze" || t == "Slice" || t == "Expand") {
     outs[0] = dt(0);
     return RTENHIP_OK;
   }
-  for (size_t i = 0; i < ins.size(); i++)
-    if (ins[i] == RTENHIP_DTYPE_INT32) {
-      // The reference runs integer Add/Sub/Mul/Div; the device kernels are f32.
-      if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div")
-        return fail(RTENHIP_UNSUPPORTED_VALUE, "int32 arithmetic is not supported on the device");
-      return fail(incorrect, ("Input " + std::to_string(i) + " has incorrect type").c_str());
+  if (t == "Shape") {
+    outs[0] = RTENHIP_DTYPE_INT32;
+    return RTENHIP_OK;
+  }
+  if (t == "ConstantOfShape") {
+    // Scalar::Int / Scalar::Float (op_registry.rs:444-456), Int(0) by default
+    if (dt(0) != RTENHIP_DTYPE_INT32) return fail(incorrect, "Input 0 has incorrect type");
+    outs[0] = op.attrs.str("dtype", "int32") == "int32" ? RTENHIP_DTYPE_INT32 : RTENHIP_DTYPE_FLOAT32;
+    return RTENHIP_OK;
+  }
+  if (t == "Concat") {
+    for (size_t i = 1; i < ins.size(); i++)
+      if (dt(i) != dt(0)) return fail(incorrect, ("Input " + std::to_string(i) + " has incorrect type").c_str());
+    outs[0] = dt(0);
+    return RTENHIP_OK;
+  }
+  if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div") {
+    // Integer arithmetic (the shape subgraph) is evaluated at plan time only;
+    // make_plan rejects an int32 one whose inputs are not known then.
+    if (dt(0) == RTENHIP_DTYPE_INT32 || dt(1) == RTENHIP_DTYPE_INT32) {
+      if (dt(0) != dt(1)) return fail(incorrect, "Input 1 has incorrect type");
+      outs[0] = RTENHIP_DTYPE_INT32;
     }
+    return RTENHIP_OK;
+  }
+  // ReduceMean's optional axes input is int32.
+  const size_t n_data = t == "ReduceMean" ? 1 : ins.size();
+  for (size_t i = 0; i < n_data; i++)
+    if (ins[i] == RTENHIP_DTYPE_INT32) return fail(incorrect, ("Input " + std::to_string(i) + " has incorrect type").c_str());
   return RTENHIP_OK;
 }
 
 static bool is_unary(const std::string& t) {
   return t == "Relu" || t == "Clip" || t == "Gelu" || t == "Erf" || t == "Sigmoid" ||
-         t == "Tanh" || t == "Exp" || t == "Silu";
+         t == "Tanh" || t == "Exp" || t == "Silu" || t == "Sqrt";
 }
 
 rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vector<Shape>& in_shapes,
@@ -502,6 +622,12 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   }
 
   // Shapes and element types.
+  std::set<int> host_ops;
+  planning_host = &p.host;
+  struct ResetHost {
+    Graph* g;
+    ~ResetHost() { g->planning_host = nullptr; }
+  } reset_host{this};
   std::map<int, Shape> shapes;
   for (size_t i = 0; i < in_ids.size(); i++) shapes[in_ids[i]] = in_shapes[i];
   for (size_t i = 0; i < in_ids.size(); i++) p.dtypes[in_ids[i]] = in_dtypes[i];
@@ -568,9 +694,61 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       shapes[nodes[op].outputs[k]] = outs[k];
       p.dtypes[nodes[op].outputs[k]] = out_dt[std::min(k, out_dt.size() - 1)];
     }
-    if (nodes[op].op_type == "Gather" && !p.gather_flag) {
+    // Plan-time evaluation of the shape subgraph (graph_host.cpp).
+    if (nodes[op].outputs.size() == 1 && nodes[op].fused_residual < 0 && !nodes[op].fused_act) {
+      HostVal hv;
+      rtenhip_status hst = RTENHIP_OK;
+      if (host_eval(op, ins, outs[0], out_dt[0], hv, hst)) {
+        p.host[nodes[op].outputs[0]] = std::move(hv);
+        host_ops.insert(op);
+        continue;
+      }
+      if (hst) {
+        std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
+        set_error(hst, msg);
+        return hst;
+      }
+    }
+    const std::string& ty = nodes[op].op_type;
+    if ((ty == "Add" || ty == "Sub" || ty == "Mul" || ty == "Div") && out_dt[0] == RTENHIP_DTYPE_INT32) {
+      std::string msg = "Operator \"" + nodes[op].name +
+                        "\" failed: int32 arithmetic on values not known at plan time is not supported on the device";
+      set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
+      return RTENHIP_UNSUPPORTED_VALUE;
+    }
+    if (ty == "Gather" && !p.gather_flag) {
       RTENHIP_HIP_CHECK(hipMalloc(&p.gather_flag, sizeof(int)));
       RTENHIP_HIP_CHECK(hipMemset(p.gather_flag, 0, sizeof(int)));
+    }
+  }
+  planning_host = nullptr;
+  // Operators evaluated at plan time are never launched; a plan-time value a
+  // launched operator reads (in any role) or the caller asks for is uploaded
+  // once into plan-owned memory.
+  if (!host_ops.empty()) {
+    std::vector<int> kept;
+    for (int op : p.ops)
+      if (!host_ops.count(op)) kept.push_back(op);
+    p.ops = kept;
+    std::set<int> needed(out_ids.begin(), out_ids.end());
+    for (int op : p.ops) {
+      for (int i : nodes[op].inputs) needed.insert(i);
+      needed.insert(nodes[op].fused_residual);
+    }
+    for (auto& kv : p.host) {
+      if (!needed.count(kv.first)) continue;
+      float* d = nullptr;
+      const size_t bytes = std::max<size_t>(4, kv.second.raw.size() * 4);
+      RTENHIP_HIP_CHECK(hipMalloc(&d, bytes));
+      p.host_dev[kv.first] = d;
+      if (!kv.second.raw.empty())
+        RTENHIP_HIP_CHECK(hipMemcpy(d, kv.second.raw.data(), kv.second.raw.size() * 4, hipMemcpyHostToDevice));
+    }
+    for (auto& kv : p.host) {
+      Slot sl;
+      sl.offset = SIZE_MAX - 2;  // plan-owned (host_dev), outside the arena
+      sl.shape = kv.second.shape;
+      p.slots[kv.first] = sl;
     }
   }
 
@@ -915,6 +1093,10 @@ float* Graph::ptr_of(Plan& p, int v) {
   if (n.kind == NodeKind::Constant) return n.dev;
   for (size_t i = 0; i < p.input_ids.size(); i++)
     if (p.input_ids[i] == v) return p.bound_in[i];
+  // A plan-time value that is also an output is read from its plan-owned
+  // copy (the caller's buffer receives it only at the end of the run).
+  auto hit = p.host_dev.find(v);
+  if (hit != p.host_dev.end()) return hit->second;
   for (size_t i = 0; i < p.output_ids.size(); i++)
     if (p.output_ids[i] == v) return p.bound_out[i];
   auto pit = p.padded.find(v);
@@ -1021,7 +1203,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     int op = t == "Relu" ? RTENHIP_UNARY_RELU : t == "Clip" ? RTENHIP_UNARY_CLIP
            : t == "Gelu" ? RTENHIP_UNARY_GELU : t == "Erf" ? RTENHIP_UNARY_ERF
            : t == "Sigmoid" ? RTENHIP_UNARY_SIGMOID : t == "Tanh" ? RTENHIP_UNARY_TANH
-           : t == "Exp" ? RTENHIP_UNARY_EXP : RTENHIP_UNARY_SILU;
+           : t == "Exp" ? RTENHIP_UNARY_EXP : t == "Sqrt" ? RTENHIP_UNARY_SQRT : RTENHIP_UNARY_SILU;
     float lo = -3.40282347e38f, hi = 3.40282347e38f;
     if (op == RTENHIP_UNARY_CLIP) {
       std::vector<float> v;
@@ -1031,6 +1213,75 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       hi = (float)n.attrs.num("max", hi);
     }
     return rtenhip_unary_f32(c, op, &x, lo, hi, &y);
+  }
+  if (t == "Pow") {
+    rtenhip_tensor b = T(n.inputs[1]);
+    return rtenhip_binary_f32(c, RTENHIP_BINARY_POW, &x, &b, &y);
+  }
+  if (t == "ReduceMean") {
+    std::vector<int64_t> ax64;
+    const int ai = n.inputs.size() > 1 ? n.inputs[1] : -1;
+    if (ai >= 0) {
+      planning_host = &p.host;
+      const bool ok = int_values(*this, ai, ax64);
+      planning_host = nullptr;
+      if (!ok) return fail(RTENHIP_UNSUPPORTED_VALUE, "ReduceMean needs constant axes");
+    } else {
+      ax64 = n.attrs.ints("axes", {});
+    }
+    std::vector<int32_t> ax(ax64.begin(), ax64.end());
+    return rtenhip_reduce_mean_f32(c, &x, ax.data(), (int32_t)ax.size(), (int)n.attrs.num("keep_dims", 0), &y);
+  }
+  if (t == "ConstantOfShape") {
+    const bool is_int = n.attrs.str("dtype", "int32") == "int32";
+    const double v = n.attrs.num("value", 0);
+    uint32_t bits;
+    if (is_int) {
+      bits = (uint32_t)(int32_t)v;
+    } else {
+      const float f = (float)v;
+      std::memcpy(&bits, &f, 4);
+    }
+    return launch_fill(y.data, numel(y), bits, ctx->stream);
+  }
+  if (t == "Expand") {
+    // expand_to (layout.rs:28-73): x broadcast to y's shape, stride 0 on
+    // broadcast dims.
+    rtenhip_tensor v = y;
+    v.data = x.data;
+    const int off = y.ndim - x.ndim;
+    for (int d = 0; d < y.ndim; d++) {
+      const int xd = d - off;
+      v.strides[d] = xd < 0 || x.shape[xd] == 1 ? 0 : x.strides[xd];
+    }
+    return launch_copy_strided(v, y.data, ctx->stream);
+  }
+  if (t == "Slice") {
+    int64_t base;
+    std::vector<int64_t> dims, sst;
+    rtenhip_status st = RTENHIP_OK;
+    planning_host = &p.host;
+    const bool ok = slice_view(*this, n, Shape(x.shape, x.shape + x.ndim), base, dims, sst, st);
+    planning_host = nullptr;
+    if (!ok) return st ? st : fail(RTENHIP_UNSUPPORTED_VALUE, "Slice needs starts / ends known at plan time");
+    rtenhip_tensor v = y;
+    v.data = x.data + base;
+    for (int d = 0; d < y.ndim; d++) v.strides[d] = sst[d];
+    return launch_copy_strided(v, y.data, ctx->stream);
+  }
+  if (t == "Concat") {
+    // concat_impl (concat.rs:43-67): each input into its block of y.
+    int64_t axis = (int64_t)n.attrs.num("axis", 0);
+    if (axis < 0) axis += y.ndim;
+    int64_t at = 0;
+    for (size_t i = 0; i < n.inputs.size(); i++) {
+      rtenhip_tensor xi = T(n.inputs[i]);
+      rtenhip_status st = launch_copy_view(xi.data, xi.shape, xi.strides, xi.ndim, y.data + at * y.strides[axis],
+                                           y.strides, ctx->stream);
+      if (st) return st;
+      at += xi.shape[axis];
+    }
+    return RTENHIP_OK;
   }
   if (t == "Add" || t == "Sub" || t == "Mul" || t == "Div") {
     rtenhip_tensor b = T(n.inputs[1]);
@@ -1574,6 +1825,30 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     a.cnt_cap = e.n_counters;
     a.persist_k = e.persist;
   };
+  // DMA fallback of a VALU configuration (see ConvExec::fb_cfg): pads the
+  // input into ctx scratch when the conv is padded, then the DMA GEMM.
+  auto run_fallback = [&]() -> rtenhip_status {
+    ConvDmaArgs f = a;
+    const bool direct = ce.cfg >= kPwCfgBase + kPwDirect;
+    if (direct && has_pad) {
+      f.Hp = g.H + g.pads[0] + g.pads[2];
+      f.Wp = g.W + g.pads[1] + g.pads[3];
+      float* xp = ctx->scratch_floats((size_t)(g.N * g.C * f.Hp * f.Wp), 1);
+      if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+      rtenhip_status st = launch_pad_nchw(a.x_unpadded, xp, g.N * g.C, (int)g.H, (int)g.W, (int)g.pads[0],
+                                          (int)g.pads[1], (int)g.pads[2], (int)g.pads[3], s);
+      if (st) return st;
+      f.xin = xp;
+    }
+    f.split = false;
+    f.ws = nullptr;
+    f.counters = nullptr;
+    f.ws_cap = f.cnt_cap = 0;
+    f.persist_k = 0;
+    f.packed_w = ce.fb_packed;
+    f.cfg = ce.fb_cfg;
+    return conv_dma(ctx, f);
+  };
   if (ce.cfg < 0) {
     int chosen = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
     bool chosen_split = false;
@@ -1748,11 +2023,11 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       ce.fb_cfg = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
       RTENHIP_HIP_CHECK(hipMalloc(&ce.fb_packed, (size_t)packed_conv_weight_floats(g, ce.fb_cfg) * 4));
       if ((st = pack_conv_weights(ctx, w, g, ce.fb_cfg, ce.fb_packed))) return st;
-      // The fallback's padded input copy uses ctx scratch slot 1: request it
-      // now, in the eager run, so a capture never has to grow it.
-      if (has_pad && !ctx->scratch_floats((size_t)(g.N * g.C * (g.H + g.pads[0] + g.pads[2]) *
-                                                   (g.W + g.pads[1] + g.pads[3])), 1))
-        return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+      // One launch now (this first run is eager; the VALU kernel overwrites
+      // the output below) creates the fallback's K tables and records its
+      // scratch, so a later capture never allocates.
+      ce.cfg = chosen;
+      if ((st = run_fallback())) return st;
     }
   }
   if (ce.cfg >= kPwCfgBase) {
@@ -1761,23 +2036,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     // can be rebound to misaligned views later.
     const bool direct = ce.cfg >= kPwCfgBase + kPwDirect;
     const uintptr_t align = (uintptr_t)a.y | (uintptr_t)a.residual | (direct ? 0 : (uintptr_t)a.xin);
-    if (align % 16 != 0) {
-      if (direct && has_pad) {
-        a.Hp = g.H + g.pads[0] + g.pads[2];
-        a.Wp = g.W + g.pads[1] + g.pads[3];
-        float* xp = ctx->scratch_floats((size_t)(g.N * g.C * a.Hp * a.Wp), 1);
-        if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
-        rtenhip_status st = launch_pad_nchw(a.x_unpadded, xp, g.N * g.C, (int)g.H, (int)g.W, (int)g.pads[0],
-                                            (int)g.pads[1], (int)g.pads[2], (int)g.pads[3], s);
-        if (st) return st;
-        a.xin = xp;
-      }
-      ConvExec none;
-      bind(none);
-      a.packed_w = ce.fb_packed;
-      a.cfg = ce.fb_cfg;
-      return conv_dma(ctx, a);
-    }
+    if (align % 16 != 0) return run_fallback();
   }
   a.packed_w = ce.packed;
   a.cfg = ce.cfg;
@@ -1850,7 +2109,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   std::vector<int> ov(out_ids, out_ids + n_out);
   // Check the caller's output buffers (RunError::OutputMismatch).
   for (int i = 0; i < n_out; i++) {
-    const Shape& s = plan->slots[ov[i]].shape;
+    const Shape& s = nodes[ov[i]].kind == NodeKind::Constant ? nodes[ov[i]].shape : plan->slots[ov[i]].shape;
     if (outs[i].ndim != (int)s.size() || !is_contiguous(outs[i]))
       return fail(RTENHIP_INCORRECT_OUTPUT_TYPE, "Output buffer has the wrong shape");
     for (size_t d = 0; d < s.size(); d++)
@@ -1938,6 +2197,25 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
     return RTENHIP_OK;
   };
+  // Outputs that no operator writes (a constant, e.g. after constant
+  // propagation, or a plan-time value) are copied into the caller's buffers
+  // at the end of the run.
+  auto copy_static_outputs = [&]() -> rtenhip_status {
+    for (int i = 0; i < n_out; i++) {
+      const int v = ov[i];
+      const float* src = nullptr;
+      if (nodes[v].kind == NodeKind::Constant) {
+        src = nodes[v].dev;
+      } else {
+        auto it = plan->host_dev.find(v);
+        if (it != plan->host_dev.end()) src = it->second;
+      }
+      if (src && numel(outs[i]) && src != outs[i].data)
+        RTENHIP_HIP_CHECK(hipMemcpyAsync(outs[i].data, src, (size_t)numel(outs[i]) * 4, hipMemcpyDeviceToDevice,
+                                         exec_stream));
+    }
+    return RTENHIP_OK;
+  };
   auto join_all = [&]() -> rtenhip_status {
     if (timing) return RTENHIP_OK;
     auto j = plan->joins.find(-1);
@@ -1963,6 +2241,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           if (st) break;
         }
         if (!st) st = join_all();
+        if (!st) st = copy_static_outputs();
         ctx->stream = exec_stream;
         hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
         if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&plan->exec, g, nullptr, nullptr, 0);
@@ -2004,6 +2283,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     ctx->scratch_log = nullptr;
     ctx->stream = exec_stream;
     if (!st) st = join_all();
+    if (!st) st = copy_static_outputs();
     plan->eager_runs++;
     if (timing && !st) {
       (void)hipStreamSynchronize(exec_stream);
@@ -2102,9 +2382,38 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
 // intermediate value has exactly one consumer.  Results are bit-identical:
 // the epilogue applies the same f32 add and max/clamp to the same values.
 rtenhip_status Graph::optimize() {
+  // RTen's own passes first (graph_optimize.cpp): they change the operator
+  // mix (Gelu, LayerNormalization, Silu, folded constants) that the device
+  // fusions below then see.
+  rtenhip_status rst = rten_optimize();
+  if (rst) return rst;
+  // Consumers among the operators the outputs depend on: a fused subgraph's
+  // leftover intermediates (still in the graph, as in RTen) do not count.
+  std::set<int> live;
+  {
+    std::map<int, int> prod_of;
+    for (int i = 0; i < (int)nodes.size(); i++)
+      if (nodes[i].kind == NodeKind::Operator && !nodes[i].removed)
+        for (int o : nodes[i].outputs) prod_of[o] = i;
+    std::vector<int> stack;
+    if (model_outputs.empty()) {
+      for (auto& kv : prod_of) stack.push_back(kv.first);
+    } else {
+      stack = model_outputs;
+    }
+    while (!stack.empty()) {
+      const int v = stack.back();
+      stack.pop_back();
+      auto it = prod_of.find(v);
+      if (it == prod_of.end() || live.count(it->second)) continue;
+      live.insert(it->second);
+      for (int i : nodes[it->second].inputs)
+        if (i >= 0) stack.push_back(i);
+    }
+  }
   std::map<int, std::vector<int>> consumers;
   for (int i = 0; i < (int)nodes.size(); i++)
-    if (nodes[i].kind == NodeKind::Operator && !nodes[i].removed)
+    if (nodes[i].kind == NodeKind::Operator && !nodes[i].removed && live.count(i))
       for (int v : nodes[i].inputs)
         if (v >= 0) consumers[v].push_back(i);
   std::set<int> outputs(model_outputs.begin(), model_outputs.end());
@@ -2385,6 +2694,11 @@ int32_t rtenhip_graph_add_constant(rtenhip_graph* g, const char* name, const flo
     return -1;
   }
   if (count <= 64) n.host_small.assign(host_data, host_data + count);
+  if ((int64_t)count <= kHostConstMax) {
+    n.host_raw.resize(count);
+    if (count) std::memcpy(n.host_raw.data(), host_data, count * 4);
+    n.has_host = true;
+  }
   return G_(g)->add_node(std::move(n));
 }
 
@@ -2409,6 +2723,11 @@ int32_t rtenhip_graph_add_constant_i32(rtenhip_graph* g, const char* name, const
   // floats for the magnitudes such tensors hold.
   if (count <= 64)
     for (size_t i = 0; i < count; i++) n.host_small.push_back((float)host_data[i]);
+  if (count <= ((size_t)1 << 22)) {  // int32 metadata (ids buffers, shapes) stays on the host too
+    n.host_raw.resize(count);
+    if (count) std::memcpy(n.host_raw.data(), host_data, count * 4);
+    n.has_host = true;
+  }
   return G_(g)->add_node(std::move(n));
 }
 
@@ -2519,6 +2838,37 @@ const char* rtenhip_graph_timing_report(rtenhip_graph* g) { return G_(g)->timing
 int32_t rtenhip_graph_node_id(rtenhip_graph* g, const char* name) {
   auto it = G_(g)->by_name.find(name ? name : "");
   return it == G_(g)->by_name.end() ? -1 : it->second;
+}
+
+const char* rtenhip_graph_describe(rtenhip_graph* g) {
+  static thread_local std::string out;
+  out.clear();
+  const Graph* G = G_(g);
+  auto ids = [](const std::vector<int>& v) {
+    std::string r;
+    for (size_t i = 0; i < v.size(); i++) r += (i ? "," : "") + std::to_string(v[i]);
+    return r;
+  };
+  for (int i = 0; i < (int)G->nodes.size(); i++) {
+    const Node& n = G->nodes[i];
+    out += std::to_string(i);
+    if (n.kind == NodeKind::Operator) {
+      if (n.removed) {
+        out.resize(out.size() - std::to_string(i).size());
+        continue;
+      }
+      std::string name = n.fused_name.empty() ? n.op_type : n.fused_name;
+      if (name == "MatMul" && !n.input_perm.empty()) name = "FusedTranspose(MatMul)";
+      out += "\top\t" + n.name + "\t" + name + "\t" + ids(n.inputs) + "\t" + ids(n.outputs) + "\n";
+    } else if (n.kind == NodeKind::Constant) {
+      std::string dims;
+      for (size_t d = 0; d < n.shape.size(); d++) dims += (d ? "x" : "") + std::to_string(n.shape[d]);
+      out += "\tconst\t" + n.name + "\t" + dims + "\n";
+    } else {
+      out += "\tvalue\t" + n.name + "\n";
+    }
+  }
+  return out.c_str();
 }
 
 int32_t rtenhip_model_input_ids(rtenhip_graph* g, int32_t* ids, int32_t cap) {

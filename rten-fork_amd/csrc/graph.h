@@ -52,6 +52,31 @@ bool parse_attrs(const char* s, Attrs& out);
 
 enum class NodeKind { Value, Constant, Operator };
 
+// A value whose contents are known on the host when a plan is made: an int32
+// or small f32 constant, or the output of the shape subgraph of an ONNX export
+// (Shape -> Gather -> Unsqueeze -> Concat -> Reshape, position-id Slices ...),
+// which RTen runs as tiny CPU ops on every Model::run.  A plan is specialised
+// to its input shapes, so these are evaluated once, at plan time
+// (graph_host.cpp), and never launched.
+struct HostVal {
+  int dtype = RTENHIP_DTYPE_INT32;
+  Shape shape;
+  std::vector<uint32_t> raw;  // 4-byte elements: int32 values or f32 bit patterns
+  int64_t numel() const {
+    int64_t n = 1;
+    for (int64_t d : shape) n *= d;
+    return n;
+  }
+  int64_t i(size_t k) const {  // element k as an integer
+    return dtype == RTENHIP_DTYPE_INT32 ? (int64_t)(int32_t)raw[k] : (int64_t)u2f(raw[k]);
+  }
+  static float u2f(uint32_t u) {
+    float f;
+    __builtin_memcpy(&f, &u, 4);
+    return f;
+  }
+};
+
 struct Node {
   NodeKind kind = NodeKind::Value;
   std::string name;
@@ -59,6 +84,10 @@ struct Node {
   float* dev = nullptr;
   Shape shape;
   std::vector<float> host_small;   // values of small constants (int32 ones converted, exact)
+  // Host copy of a constant's elements (all int32 constants, f32 ones up to
+  // kHostConstMax elements) for plan-time evaluation of the shape subgraph.
+  std::vector<uint32_t> host_raw;
+  bool has_host = false;
   int dtype = RTENHIP_DTYPE_FLOAT32;  // constants: element type
   bool owns_dev = true;
   // Operator
@@ -77,6 +106,9 @@ struct Node {
   // that input's view (empty = reversed axes, Transpose without perm).
   std::map<int, std::vector<int64_t>> input_perm;
   bool removed = false;      // op folded into another
+  // Operator::name() of the node after RTen's fusions (optimize.rs), when it
+  // differs from op_type: "FusedTranspose(MatMul)".
+  std::string fused_name;
   bool alias_input0 = false; // output is a view of input 0 (Flatten/Reshape)
 };
 
@@ -156,6 +188,10 @@ struct Plan {
   std::vector<Shape> input_shapes;
   std::vector<int> input_dtypes;
   std::map<int, int> dtypes;          // value id -> element type (RTENHIP_DTYPE_*)
+  // Plan-time values (see HostVal) and the device copies of those a kernel
+  // or a graph output reads (uploaded once, plan-owned).
+  std::map<int, HostVal> host;
+  std::map<int, float*> host_dev;
   // Gathers with non-constant indices record an out-of-range index here; the
   // run reads and clears it when it completes (graph-capturable: no sync
   // inside the ops).
@@ -196,6 +232,15 @@ struct Graph {
                      const int32_t* out_ids, rtenhip_tensor* outs, int n_out,
                      const int32_t* in_dt = nullptr);
   rtenhip_status optimize();
+  // RTen's own passes (src/optimize.rs:286-518, graph_optimize.cpp), run
+  // first by optimize(): constant propagation, Silu / Gelu / LayerNorm fusion.
+  rtenhip_status rten_optimize();
+  rtenhip_status propagate_constants();
+  int fuse_rten_patterns();
+  // Host value of `id` (a constant with a host copy, or a plan-time value of
+  // the plan being made / run), or nullptr.
+  const HostVal* host_value(int id, HostVal& tmp) const;
+  const std::map<int, HostVal>* planning_host = nullptr;
   rtenhip_status plan_shapes(const int32_t* in_ids, const rtenhip_tensor* ins, int n_in,
                              const int32_t* out_ids, int n_out, int64_t* shapes, int32_t* ndims,
                              const int32_t* in_dt = nullptr, int32_t* out_dt = nullptr);
@@ -210,6 +255,12 @@ struct Graph {
                               std::vector<Shape>& outs);
   rtenhip_status infer_dtypes(int op_id, const std::vector<int>& ins, std::vector<int>& outs);
   rtenhip_status exec_op(Plan& p, int op_id);
+  // Plan-time evaluation of op_id from host values (graph_host.cpp): returns
+  // true with out filled, false when an input is not known on the host or the
+  // op is not one the host evaluates; st is set on an operator error.
+  bool host_eval(int op_id, const std::vector<const Shape*>& in_shapes, const Shape& out_shape,
+                 int out_dtype, HostVal& out, rtenhip_status& st);
+  rtenhip_status exec_data_op(Plan& p, int op_id, bool& handled);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
@@ -217,5 +268,15 @@ struct Graph {
                                  const rtenhip_tensor& b, const rtenhip_tensor& y, MatMulExec& me);
   float* ptr_of(Plan& p, int value_id);
 };
+
+// Slice (slice.rs:18-65) as a strided view of an input of shape xs: base
+// element offset, output dims and per-dim source strides (negative for
+// negative steps).  False when starts / ends / axes / steps are not known on
+// the host (st stays OK) or on an operator error (st set).
+bool slice_view(const Graph& g, const Node& op, const Shape& xs, int64_t& base, std::vector<int64_t>& out_dims,
+                std::vector<int64_t>& sst, rtenhip_status& st);
+
+constexpr int64_t kHostConstMax = 4096;     // f32 constants kept on the host
+constexpr int64_t kHostEvalMax = 1 << 16;    // plan-time evaluation output cap
 
 }  // namespace rtenhip

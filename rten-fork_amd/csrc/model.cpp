@@ -39,12 +39,15 @@ enum AttrsType : uint8_t {
   kAveragePoolAttrs = 2,
   kBatchNormalizationAttrs = 3,
   kCastAttrs = 4,
+  kConcatAttrs = 5,
+  kConstantOfShapeAttrs = 6,
   kConvAttrs = 7,
   kConvTransposeAttrs = 8,
   kFlattenAttrs = 9,
   kGatherAttrs = 10,
   kGemmAttrs = 11,
   kMaxPoolAttrs = 15,
+  kReduceMeanAttrs = 16,
   kReshapeAttrs = 17,
   kSoftmaxAttrs = 20,
   kTransposeAttrs = 21,
@@ -247,10 +250,33 @@ void read_op(const std::string& type, uint8_t attrs_type, const Table& a, Attrs&
     need(kCastAttrs);  // op_registry.rs:421-428: DataType::Int32, anything else Float
     out.nums["to"] = {a.scalar<uint8_t>(0, 0) == 0 ? (double)RTENHIP_DTYPE_INT32
                                                    : (double)RTENHIP_DTYPE_FLOAT32};
+  } else if (type == "Concat") {
+    need(kConcatAttrs);  // impl_read_op!(Concat, attrs_as_concat_attrs, axis)
+    out.nums["axis"] = {(double)a.scalar<int32_t>(0, 0)};
+  } else if (type == "ReduceMean") {
+    // impl_read_op!(.., reduce_axes) (op_registry.rs:351-366): axes optional
+    need(kReduceMeanAttrs);
+    std::vector<int32_t> ax;
+    if (a.vec_of(0, ax)) out.nums["axes"] = std::vector<double>(ax.begin(), ax.end());
+    out.nums["keep_dims"] = {(double)a.scalar<uint8_t>(1, 0)};
+  } else if (type == "ConstantOfShape") {
+    // op_registry.rs:444-456: value union Scalar {IntScalar = 1, FloatScalar = 2},
+    // Scalar::Int(0) when neither.
+    need(kConstantOfShapeAttrs);
+    const uint8_t vt = a.scalar<uint8_t>(0, 0);
+    const Table v = a.table(1);
+    if (vt == 2 && v) {
+      out.strs["dtype"] = "float";
+      out.nums["value"] = {(double)v.scalar<float>(0, 0.f)};
+    } else {
+      out.strs["dtype"] = "int32";
+      out.nums["value"] = {vt == 1 && v ? (double)v.scalar<int32_t>(0, 0) : 0.0};
+    }
   } else {
     static const char* const no_attrs[] = {"Add", "Sub", "Mul", "Div", "Clip", "Relu", "Erf",
                                            "Exp", "Sigmoid", "Tanh", "MatMul", "Identity",
-                                           "GlobalAveragePool", "Where", "Unsqueeze", "Squeeze"};
+                                           "GlobalAveragePool", "Where", "Unsqueeze", "Squeeze",
+                                           "Pow", "Sqrt", "Shape", "Slice", "Expand"};
     for (const char* t : no_attrs)
       if (type == t) return;
     throw LoadError{RTENHIP_UNSUPPORTED_VALUE,

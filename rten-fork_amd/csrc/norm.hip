@@ -323,4 +323,94 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
   return RTENHIP_OK;
 }
 
+// ReduceMean over the last axis (reduce.rs:270-286: reduce_slice = slice_sum
+// / len).  One wave per row: lane j forms the sums of chunks j, j+64, ... (a
+// full chunk as ((x0+x4) + (x1+x5)) + (x2+x6)) + (x3+x7), a partial one as a
+// fold from 0, slice_reductions.rs:38-55); lane 0 then folds the chunk sums in
+// order from 0 and divides by the row length.
+__global__ __launch_bounds__(256) void reduce_mean_rows_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               int64_t rows, int64_t len) {
+  extern __shared__ float chunk_sums[];  // [4 waves][nchunks]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t nchunks = (len + 7) / 8;
+  float* cs = chunk_sums + (int64_t)wave * nchunks;
+  if (row < rows) {
+    const float* xr = x + row * len;
+    for (int64_t c = lane; c < nchunks; c += 64) {
+      const int64_t b = c * 8;
+      float sum;
+      if (b + 8 <= len) {
+        const float z0 = __fadd_rn(xr[b], xr[b + 4]), z1 = __fadd_rn(xr[b + 1], xr[b + 5]);
+        const float z2 = __fadd_rn(xr[b + 2], xr[b + 6]), z3 = __fadd_rn(xr[b + 3], xr[b + 7]);
+        sum = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
+      } else {
+        sum = 0.f;
+        for (int64_t k = b; k < len; k++) sum = __fadd_rn(sum, xr[k]);
+      }
+      cs[c] = sum;
+    }
+  }
+  __syncthreads();
+  if (row < rows && lane == 0) {
+    float total = 0.f;
+    for (int64_t c = 0; c < nchunks; c++) total = __fadd_rn(total, cs[c]);
+    y[row] = __fdiv_rn(total, (float)len);
+  }
+}
+
+rtenhip_status launch_reduce_mean_rows(const float* x, float* y, int64_t rows, int64_t len, hipStream_t s) {
+  if (rows == 0) return RTENHIP_OK;
+  const size_t shmem = 4 * (size_t)((len + 7) / 8) * sizeof(float);
+  if (shmem > 64 * 1024) return fail(RTENHIP_UNSUPPORTED_VALUE, "ReduceMean row too long");
+  hipLaunchKernelGGL(reduce_mean_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), shmem, s, x, y, rows,
+                     len);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+// ReduceMean over any other axes (reduce.rs:287-318): per output element, the
+// reduced sub-block in row-major order (lanes along one axis, or the slow
+// path's slice iteration) summed with iter_sum -- groups of four as
+// sum + ((a + b) + (c + d)) while more than four remain, then one at a time
+// (slice_reductions.rs:58-85) -- divided by the element count.
+__global__ __launch_bounds__(256) void reduce_mean_iter_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               ReduceDesc d) {
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < d.n_out;
+       o += (int64_t)gridDim.x * blockDim.x) {
+    int64_t rem = o, base = 0;
+    for (int k = d.nk - 1; k >= 0; k--) {
+      base += (rem % d.kshape[k]) * d.kstride[k];
+      rem /= d.kshape[k];
+    }
+    auto at = [&](int64_t r) {
+      int64_t off = base;
+      for (int k = d.nr - 1; k >= 0; k--) {
+        off += (r % d.rshape[k]) * d.rstride[k];
+        r /= d.rshape[k];
+      }
+      return x[off];
+    };
+    float sum = 0.f;
+    int64_t r = 0, left = d.n_red;
+    while (left > 4) {
+      left -= 4;
+      const float a = at(r), b = at(r + 1), c = at(r + 2), e = at(r + 3);
+      sum = __fadd_rn(sum, __fadd_rn(__fadd_rn(a, b), __fadd_rn(c, e)));
+      r += 4;
+    }
+    for (; r < d.n_red; r++) sum = __fadd_rn(sum, at(r));
+    y[o] = __fdiv_rn(sum, (float)d.n_red);
+  }
+}
+
+rtenhip_status launch_reduce_mean_iter(const float* x, float* y, const ReduceDesc& d, hipStream_t s) {
+  if (d.n_out == 0) return RTENHIP_OK;
+  int64_t blocks = (d.n_out + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(reduce_mean_iter_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, d);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 }  // namespace rtenhip

@@ -344,6 +344,61 @@ static int64_t resolve_axis(int64_t axis, int ndim, bool* ok) {
   return axis;
 }
 
+rtenhip_status rtenhip_reduce_mean_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, const int32_t* axes,
+                                       int32_t n_axes, int keep_dims, rtenhip_tensor* y) {
+  // reduce (src/ops/reduce.rs:225-330) with the MeanReducer (334-353).
+  Ctx* cx = C_(ctx);
+  if (!x || !y) return fail(RTENHIP_MISSING_INPUTS, "Missing inputs");
+  const int nd = x->ndim;
+  std::vector<int> res;
+  if (n_axes <= 0 || !axes) {
+    for (int d = 0; d < nd; d++) res.push_back(d);
+  } else {
+    for (int i = 0; i < n_axes; i++) {
+      bool ok;
+      const int64_t a = resolve_axis(axes[i], nd, &ok);
+      if (!ok) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+      res.push_back((int)a);
+    }
+  }
+  std::sort(res.begin(), res.end());
+  const int64_t n = numel(*x);
+  if (nd > 0 && n == 0) return fail(RTENHIP_INVALID_VALUE, "Cannot reduce empty tensor");
+  std::vector<bool> red(nd, false);
+  for (int a : res) red[a] = true;
+  int64_t os[RTENHIP_MAX_DIMS];
+  int on = 0;
+  for (int d = 0; d < nd; d++)
+    if (!red[d]) os[on++] = x->shape[d];
+    else if (keep_dims) os[on++] = 1;
+  rtenhip_status st = check_out_shape(y, os, on);
+  if (st) return st;
+  if (!is_contiguous(*y)) return fail(RTENHIP_UNSUPPORTED_VALUE, "output must be contiguous");
+  // reduced_inner_dims: the sorted axes equal to ndim-1, ndim-2, ... (only a
+  // single last axis in practice), with contiguous data -> reduce_slice.
+  bool inner = nd > 0;
+  for (size_t i = 0; i < res.size(); i++) inner = inner && res[i] == nd - 1 - (int)i;
+  if (inner && is_contiguous(*x)) {
+    const int64_t len = (int)res.size() == nd ? n : x->strides[nd - 1 - (int)res.size()];
+    return launch_reduce_mean_rows(x->data, y->data, n / len, len, cx->stream);
+  }
+  ReduceDesc d{};
+  d.n_out = 1;
+  d.n_red = 1;
+  for (int k = 0; k < nd; k++) {
+    if (red[k]) {
+      d.rshape[d.nr] = x->shape[k];
+      d.rstride[d.nr++] = x->strides[k];
+      d.n_red *= x->shape[k];
+    } else {
+      d.kshape[d.nk] = x->shape[k];
+      d.kstride[d.nk++] = x->strides[k];
+      d.n_out *= x->shape[k];
+    }
+  }
+  return launch_reduce_mean_iter(x->data, y->data, d, cx->stream);
+}
+
 rtenhip_status rtenhip_layer_norm_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
                                       const rtenhip_tensor* scale, const rtenhip_tensor* bias,
                                       int64_t axis, float epsilon, rtenhip_tensor* y) {

@@ -54,6 +54,14 @@ def lib():
     global _lib
     with _lib_lock:
         if _lib is None:
+            # torch first: it brings its own HIP runtime, and librten_hip.so must
+            # bind to that one.  Loading this library first would map the
+            # system libamdhip64 and leave torch and the library on different
+            # runtimes (hipSetDevice then fails in the library).
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
             if not os.path.exists(LIB_PATH):
                 raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C {_PKG}` "
                                    "(or __graft_entry__.build())")
@@ -83,6 +91,8 @@ def lib():
             L.rtenhip_model_describe.argtypes = [C.POINTER(C.c_uint8), C.c_size_t]
             L.rtenhip_model_input_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
             L.rtenhip_model_output_ids.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
+            L.rtenhip_graph_describe.restype = C.c_char_p
+            L.rtenhip_graph_describe.argtypes = [C.c_void_p]
             L.rtenhip_num_threads.restype = C.c_int32
             L.rtenhip_num_threads.argtypes = [C.c_void_p]
             L.rtenhip_cpu_counts.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -108,7 +118,8 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_plan", "rtenhip_gather_output_shape", "rtenhip_gather_f32",
     "rtenhip_where_output_shape", "rtenhip_where_f32", "rtenhip_cast_f32_to_i32",
     "rtenhip_cast_i32_to_f32", "rtenhip_graph_add_constant_i32", "rtenhip_graph_run_typed",
-    "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts",
+    "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts", "rtenhip_reduce_mean_f32",
+    "rtenhip_graph_describe",
 ]
 
 # rtenhip_dtype (sg::DataType order, include/rten_hip.h)
@@ -491,7 +502,7 @@ def softmax(x, axis=-1, out=None, ctx=None):
     return y
 
 
-UNARY = {"Relu": 0, "Clip": 1, "Gelu": 2, "Erf": 3, "Sigmoid": 4, "Tanh": 5, "Exp": 6, "Silu": 7}
+UNARY = {"Relu": 0, "Clip": 1, "Gelu": 2, "Erf": 3, "Sigmoid": 4, "Tanh": 5, "Exp": 6, "Silu": 7, "Sqrt": 8}
 
 
 def unary(op: str, x, p0: float = 0.0, p1: float = 0.0, out=None, ctx=None):
@@ -538,7 +549,7 @@ def silu(x, **kw):
     return unary("Silu", x, **kw)
 
 
-BINARY = {"Add": 0, "Sub": 1, "Mul": 2, "Div": 3}
+BINARY = {"Add": 0, "Sub": 1, "Mul": 2, "Div": 3, "Pow": 4}
 
 
 def binary(op: str, a, b, out=None, ctx=None):
@@ -554,6 +565,29 @@ def binary(op: str, a, b, out=None, ctx=None):
     check(lib().rtenhip_binary_f32(C.c_void_p(ctx.ptr), C.c_int(BINARY[op]), C.byref(ad),
                                    C.byref(bd), C.byref(yd)))
     return y
+
+
+def reduce_mean(x, axes=None, keep_dims=False, ctx=None):
+    """ReduceMean (src/ops/reduce.rs:334-400): axes None / [] = all axes."""
+    ctx = ctx or default_context()
+    nd = x.dim()
+    ax = list(axes or [])
+    res = sorted((a + nd if a < 0 else a) for a in ax) if ax else list(range(nd))
+    shape = [1 if d in res else s for d, s in enumerate(x.shape) if keep_dims or d not in res]
+    y = _empty(tuple(shape), x)
+    xd, yd = describe(x), describe(y)
+    arr = (C.c_int32 * max(1, len(ax)))(*ax)
+    check(lib().rtenhip_reduce_mean_f32(C.c_void_p(ctx.ptr), C.byref(xd), arr, C.c_int32(len(ax)),
+                                        C.c_int(int(keep_dims)), C.byref(yd)))
+    return y
+
+
+def pow(a, b, **kw):  # noqa: A001  (the operator's name)
+    return binary("Pow", a, b, **kw)
+
+
+def sqrt(x, **kw):
+    return unary("Sqrt", x, **kw)
 
 
 def add(a, b, **kw):

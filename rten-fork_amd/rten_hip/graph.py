@@ -68,13 +68,13 @@ class Graph:
     def add_constant(self, name: str, data: np.ndarray) -> int:
         """Constant tensor: int32 data stays int32 (IntData), anything else is f32."""
         if np.asarray(data).dtype == np.int32:
-            data = np.ascontiguousarray(data, dtype=np.int32)
+            data = np.array(data, dtype=np.int32, order="C")  # keeps 0-d scalars 0-d
             shape = (C.c_int64 * max(1, data.ndim))(*data.shape)
             nid = lib().rtenhip_graph_add_constant_i32(C.c_void_p(self.ptr), name.encode(),
                                                       data.ctypes.data_as(C.POINTER(C.c_int32)),
                                                       shape, C.c_int32(data.ndim))
             return self._ret(nid, name)
-        data = np.ascontiguousarray(data, dtype=np.float32)
+        data = np.array(data, dtype=np.float32, order="C")
         shape = (C.c_int64 * max(1, data.ndim))(*data.shape)
         nid = lib().rtenhip_graph_add_constant(C.c_void_p(self.ptr), name.encode(),
                                               data.ctypes.data_as(C.POINTER(C.c_float)), shape,
@@ -84,15 +84,44 @@ class Graph:
     def add_op(self, name: str, op_type: str, inputs: Sequence[Optional[int]],
                outputs: Sequence[int], attrs: Optional[dict] = None) -> int:
         ins = [(-1 if i is None else int(i)) for i in inputs]
+        attrs = dict(attrs or {})
+        if op_type == "ConstantOfShape" and "dtype" not in attrs:
+            # Scalar::Int / Scalar::Float from the Python type of the value
+            attrs["dtype"] = "float" if isinstance(attrs.get("value", 0), float) else "int32"
         ia = (C.c_int32 * max(1, len(ins)))(*ins)
         oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
         nid = lib().rtenhip_graph_add_op(C.c_void_p(self.ptr), name.encode(), op_type.encode(),
-                                         _attr_str(attrs or {}).encode(), ia, C.c_int32(len(ins)),
+                                         _attr_str(attrs).encode(), ia, C.c_int32(len(ins)),
                                          oa, C.c_int32(len(outputs)))
         return self._ret(nid, name)
 
     def optimize(self):
         check(lib().rtenhip_graph_optimize(C.c_void_p(self.ptr)))
+
+    def describe(self):
+        """The graph after optimization, one dict per node (rtenhip_graph_describe):
+        kind "op" (with ``op`` = Operator::name(), e.g. "FusedTranspose(MatMul)",
+        ``inputs`` / ``outputs`` node ids), "const" or "value"."""
+        text = lib().rtenhip_graph_describe(C.c_void_p(self.ptr)).decode()
+        nodes = []
+        for line in text.splitlines():
+            f = line.split("\t")
+            d = {"id": int(f[0]), "kind": f[1], "name": f[2]}
+            if f[1] == "op":
+                d["op"] = f[3]
+                d["inputs"] = [int(x) for x in f[4].split(",") if x]
+                d["outputs"] = [int(x) for x in f[5].split(",") if x]
+            elif f[1] == "const":
+                d["shape"] = tuple(int(x) for x in f[3].split("x") if x)
+            nodes.append(d)
+        return nodes
+
+    def producer(self, value_id: int):
+        """The live operator producing ``value_id`` (None for a constant or an input)."""
+        for d in self.describe():
+            if d["kind"] == "op" and value_id in d["outputs"]:
+                return d
+        return None
 
     def node_id(self, name: str) -> int:
         return self.names[name]

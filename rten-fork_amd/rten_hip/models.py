@@ -167,6 +167,49 @@ def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
     return total
 
 
+def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
+    """Algorithmic HBM bytes of every Conv (and the classifier Gemm) in
+    ``spec`` at input [batch, 3, hw, hw], as the fused graph moves them: each
+    conv reads its input and weights (+ bias) once and writes its output once;
+    a residual Add fused into the conv's epilogue reads its other operand once;
+    Relu / Clip ride in the epilogue (no traffic).  The HBM-roofline figure for
+    bandwidth-bound models (MobileNetV2)."""
+    shapes = {spec.inputs[0]: (batch, 3, hw, hw)}
+    consts = {n.name: n.data.shape for n in spec.nodes if n.kind == "const"}
+    total = 0.0
+    for n in spec.nodes:
+        if n.kind != "op":
+            continue
+        xs = shapes.get(n.inputs[0]) if n.inputs and n.inputs[0] in shapes else None
+        if n.op_type == "Conv":
+            o, ci, kh, kw = consts[n.inputs[1]]
+            N, C, H, W = xs
+            p, s = n.attrs["pads"], n.attrs["strides"]
+            oh = (H + p[0] + p[2] - kh) // s[0] + 1
+            ow = (W + p[1] + p[3] - kw) // s[1] + 1
+            total += 4.0 * (N * C * H * W + N * o * oh * ow + o * ci * kh * kw + o)
+            shapes[n.outputs[0]] = (N, o, oh, ow)
+        elif n.op_type == "Add":
+            total += 4.0 * float(np.prod(xs))  # the residual operand
+            shapes[n.outputs[0]] = xs
+        elif n.op_type == "MaxPool":
+            N, C, H, W = xs
+            k, s, p = n.attrs["kernel_size"], n.attrs["strides"], n.attrs["pads"]
+            shapes[n.outputs[0]] = (N, C, (H + p[0] + p[2] - k[0]) // s[0] + 1,
+                                    (W + p[1] + p[3] - k[1]) // s[1] + 1)
+        elif n.op_type == "GlobalAveragePool":
+            shapes[n.outputs[0]] = (xs[0], xs[1], 1, 1)
+        elif n.op_type == "Flatten":
+            shapes[n.outputs[0]] = (xs[0], int(np.prod(xs[1:])))
+        elif n.op_type == "Gemm":
+            o, k = consts[n.inputs[1]]
+            total += 4.0 * (xs[0] * k + o * k + o + xs[0] * o)
+            shapes[n.outputs[0]] = (xs[0], o)
+        else:
+            shapes[n.outputs[0]] = xs
+    return total
+
+
 BERT_BASE_GFLOP_PER_SEQ128 = 22.347  # SURVEY.md App. A.3 (encoder, seq 128)
 
 

@@ -40,6 +40,8 @@ ATTRS_AVERAGE_POOL, ATTRS_BATCH_NORM, ATTRS_CONV, ATTRS_CONV_TRANSPOSE, ATTRS_FL
 ATTRS_GEMM, ATTRS_MAX_POOL, ATTRS_RESHAPE, ATTRS_SOFTMAX = 11, 15, 17, 20
 ATTRS_TRANSPOSE, ATTRS_LAYER_NORM, ATTRS_GELU = 21, 30, 37
 ATTRS_CAST, ATTRS_GATHER = 4, 10
+ATTRS_CONCAT, ATTRS_CONSTANT_OF_SHAPE, ATTRS_REDUCE_MEAN = 5, 6, 16
+SCALAR_INT, SCALAR_FLOAT = 1, 2  # union Scalar (schema.fbs:236-239)
 NODE_OPERATOR, NODE_CONSTANT, NODE_VALUE = 1, 2, 3
 CONST_FLOAT_DATA, CONST_INT_DATA = 1, 2
 DTYPE_INT32, DTYPE_FLOAT32 = 0, 1
@@ -203,6 +205,19 @@ def _op_attrs(op_type: str, a: dict):
     if op_type == "Cast":
         # CastAttrs::to, sg::DataType: Int32 = 0 (the schema default), Float = 1
         return ATTRS_CAST, Table([(0, "u8", int(a.get("to", 0)))])
+    if op_type == "Concat":
+        return ATTRS_CONCAT, Table([(0, "i32", int(a.get("axis", 0)))])
+    if op_type == "ReduceMean":
+        f = [(1, "bool", int(bool(a.get("keep_dims", 0))))]
+        if a.get("axes") is not None:
+            f.append((0, "ref", Vector("i32", [int(x) for x in a["axes"]])))
+        return ATTRS_REDUCE_MEAN, Table(f)
+    if op_type == "ConstantOfShape":
+        v = a.get("value", 0)
+        is_float = a.get("dtype") == "float" or isinstance(v, float)
+        scalar = Table([(0, "f32", float(v))]) if is_float else Table([(0, "i32", int(v))])
+        return ATTRS_CONSTANT_OF_SHAPE, Table([(0, "u8", SCALAR_FLOAT if is_float else SCALAR_INT),
+                                               (1, "ref", scalar)])
     return 0, None
 
 

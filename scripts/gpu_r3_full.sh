@@ -1,14 +1,20 @@
 #!/bin/bash
-# Round 3: full-size parity tests for the BASELINE configs, then bench lines.
+# Round 3: new tests first, then the whole GPU suite, the full-size BASELINE
+# configs and the bench lines.  Each step has its own time limit; the script
+# stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export RTEN_NUM_THREADS=8
-timeout -k 10 300 python -u -m pytest tests/test_threads.py tests/test_conv_pointwise_gpu.py -k "thread or misaligned" -x -v \
-  --timeout 120 --timeout-method thread > gpurun_out/r3_quick.log 2>&1 || { echo "quick tests failed"; tail -30 gpurun_out/r3_quick.log; exit 1; }
+PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
+timeout -k 10 400 $PYT tests/test_optimizer_gpu.py tests/test_threads.py tests/test_conv_pointwise_gpu.py -k "not test_pointwise_valu_bitexact and not test_direct_valu" \
+  > gpurun_out/r3_quick.log 2>&1 || { echo "quick tests failed"; tail -40 gpurun_out/r3_quick.log; exit 1; }
 tail -3 gpurun_out/r3_quick.log
-timeout -k 10 900 python -u -m pytest tests/test_full_size_gpu.py -x -v --timeout 600 --timeout-method thread \
-  > gpurun_out/r3_full.log 2>&1 || { echo "full-size tests failed"; tail -30 gpurun_out/r3_full.log; exit 1; }
+timeout -k 10 900 $PYT tests -m gpu --deselect tests/test_full_size_gpu.py > gpurun_out/r3_suite.log 2>&1 \
+  || { echo "gpu suite failed"; tail -40 gpurun_out/r3_suite.log; exit 1; }
+tail -3 gpurun_out/r3_suite.log
+timeout -k 10 900 $PYT tests/test_full_size_gpu.py > gpurun_out/r3_full.log 2>&1 \
+  || { echo "full-size tests failed"; tail -30 gpurun_out/r3_full.log; exit 1; }
 tail -5 gpurun_out/r3_full.log
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r3_bench.json 2> gpurun_out/r3_bench.err || exit 1
 cat gpurun_out/r3_bench.json

@@ -71,9 +71,14 @@ def test_describe_round_trip_tiny():
     assert nodes[2][1].startswith("b 2 sum=0")
 
 
-@pytest.mark.parametrize("name", ["resnet50", "mobilenet_v2", "bert_encoder"])
+@pytest.mark.parametrize("name", ["resnet50", "mobilenet_v2", "bert_encoder", "bert_onnx"])
 def test_describe_round_trip_models(name):
-    spec = getattr(models, name)() if name != "bert_encoder" else models.bert_encoder(layers=2, seq=32)
+    if name == "bert_encoder":
+        spec = models.bert_encoder(layers=2, seq=32)
+    elif name == "bert_onnx":  # ONNX primitives and the shape subgraph, before RTen's optimizer
+        spec = models.bert_encoder(layers=2, seq=32, embeddings=True, vocab=64, unfused=True)
+    else:
+        spec = getattr(models, name)()
     desc = rten_file.describe_model(_model_bytes(spec))
     _, _, nodes = _parse(desc)
     assert len(nodes) == len(spec.nodes)
@@ -91,6 +96,29 @@ def test_describe_round_trip_models(name):
             assert shape == "x".join(str(d) for d in np.asarray(n.data).shape)
         else:
             assert kind == "value"
+
+
+def test_export_op_attrs_round_trip():
+    """Attributes of the ops an ONNX export adds (op_registry.rs: ReduceMean's
+    reduce_axes, Concat's axis, ConstantOfShape's Scalar union) survive the
+    writer and the loader."""
+    m = ModelSpec("export_ops")
+    x = m.value("x")
+    m.inputs = ["x"]
+    r = m.op("ReduceMean", [x], {"axes": [-1, 1], "keep_dims": 1}, name="rm")
+    r0 = m.op("ReduceMean", [x], {"keep_dims": 0}, name="rm_all")
+    c = m.op("Concat", [r, r], {"axis": -2}, name="cat")
+    shp = m.const("shp", np.array([2, 3], np.int32))
+    k1 = m.op("ConstantOfShape", [shp], {"value": 7}, name="cos_i")
+    k2 = m.op("ConstantOfShape", [shp], {"value": 0.25}, name="cos_f")
+    m.outputs = [c, k1, k2, r0]
+    _, _, nodes = _parse(rten_file.describe_model(_model_bytes(m)))
+    ops = {rest.split(" ")[0]: rest for kind, rest in nodes.values() if kind == "op"}
+    assert "axes=-1,1" in ops["rm"] and "keep_dims=1" in ops["rm"]
+    assert "axes=" not in ops["rm_all"] and "keep_dims=0" in ops["rm_all"]
+    assert "axis=-2" in ops["cat"]
+    assert "value=7" in ops["cos_i"] and "dtype=int32" in ops["cos_i"]
+    assert "value=0.25" in ops["cos_f"] and "dtype=float" in ops["cos_f"]
 
 
 def test_inline_and_external_constants_agree():
@@ -139,11 +167,11 @@ def test_truncated_model_is_a_parse_error():
 
 
 def test_unsupported_operator_error():
-    m = ModelSpec("concat")
+    m = ModelSpec("topk")
     x = m.value("x")
     m.inputs = ["x"]
-    m.outputs = [m.op("Concat", [x, x], name="concat")]
-    with pytest.raises(OpError, match="operator error: operator Concat is not supported or not enabled"):
+    m.outputs = [m.op("TopK", [x, x], name="topk")]
+    with pytest.raises(OpError, match="operator error: operator TopK is not supported or not enabled"):
         rten_file.describe_model(_model_bytes(m))
 
 
@@ -250,11 +278,11 @@ def test_load_bert_file_bitexact(gpu):
 
 @pytest.mark.gpu
 def test_load_errors_on_device(gpu):
-    m = ModelSpec("concat")
+    m = ModelSpec("topk")
     x = m.value("x")
     m.inputs = ["x"]
-    m.outputs = [m.op("Concat", [x, x], name="concat")]
-    with pytest.raises(OpError, match="operator error: operator Concat"):
+    m.outputs = [m.op("TopK", [x, x], name="topk")]
+    with pytest.raises(OpError, match="operator error: operator TopK"):
         rten_file.load_model(rten_file.to_rten_bytes(m))
 
 
