@@ -47,6 +47,46 @@ CONST_FLOAT_DATA, CONST_INT_DATA = 1, 2
 DTYPE_INT32, DTYPE_FLOAT32 = 0, 1
 AUTOPAD_SAME, AUTOPAD_NOTSET = 0, 1
 
+# Field slots (vtable index) of every table the writer emits, by field name
+# (schema.fbs; pinned against the reference's generated code by
+# tests/test_schema_pin.py and tests/golden/schema_slots.json).
+SLOTS = {
+    "Model": {"schema_version": 0, "graph": 1, "metadata": 2},
+    "Graph": {"nodes": 0, "inputs": 1, "outputs": 2, "captures": 3},
+    "Node": {"name": 0, "data_type": 1, "data": 2},
+    "OperatorNode": {"type_": 0, "attrs_type": 1, "attrs": 2, "inputs": 3, "outputs": 4},
+    "ValueNode": {"shape": 0},
+    "ConstantNode": {"shape": 0, "data_type": 1, "data": 2, "dtype": 3, "data_offset": 4},
+    "FloatData": {"data": 0},
+    "IntData": {"data": 0},
+    "ConvAttrs": {"auto_pad": 0, "pads": 1, "groups": 2, "strides": 3, "dilations": 4},
+    "ConvTransposeAttrs": {"strides": 0, "auto_pad": 1, "pads": 2},
+    "MaxPoolAttrs": {"kernel_size": 0, "auto_pad": 1, "pads": 2, "strides": 3},
+    "AveragePoolAttrs": {"kernel_size": 0, "auto_pad": 1, "pads": 2, "strides": 3, "count_include_pad": 4},
+    "BatchNormalizationAttrs": {"epsilon": 0},
+    "GemmAttrs": {"alpha": 0, "beta": 1, "transpose_a": 2, "transpose_b": 3},
+    "FlattenAttrs": {"axis": 0},
+    "SoftmaxAttrs": {"axis": 0},
+    "LayerNormalizationAttrs": {"axis": 0, "epsilon": 1},
+    "TransposeAttrs": {"perm": 0},
+    "ReshapeAttrs": {"allow_zero": 0},
+    "GatherAttrs": {"axis": 0},
+    "CastAttrs": {"to": 0},
+    "ConcatAttrs": {"axis": 0},
+    "ReduceMeanAttrs": {"axes": 0, "keep_dims": 1},
+    "ConstantOfShapeAttrs": {"value_type": 0, "value": 1},
+    "IntScalar": {"value": 0},
+    "FloatScalar": {"value": 0},
+    "GeluAttrs": {},
+}
+
+
+def _T(table: str, *fields) -> "Table":
+    """Table of schema type ``table`` from (field name, kind, value) triples."""
+    slots = SLOTS[table]
+    return Table([(slots[name], kind, value) for name, kind, value in fields])
+
+
 HEADER_LEN = 32
 TENSOR_ALIGN = 64
 INLINE_MAX_ELEMS = 16
@@ -158,66 +198,66 @@ def _u32v(v):
 
 def _op_attrs(op_type: str, a: dict):
     """(union type, attrs table) as rten-convert writes them."""
-    def padding(fields_at):
-        auto, pads = fields_at
+    def padding():
         if str(a.get("auto_pad", "notset")).lower() in ("same", "same_upper"):
-            return [(auto, "u8", AUTOPAD_SAME)]
-        return [(auto, "u8", AUTOPAD_NOTSET), (pads, "ref", _u32v(a.get("pads", [0, 0, 0, 0])))]
+            return [("auto_pad", "u8", AUTOPAD_SAME)]
+        return [("auto_pad", "u8", AUTOPAD_NOTSET), ("pads", "ref", _u32v(a.get("pads", [0, 0, 0, 0])))]
 
     if op_type == "Conv":
-        return ATTRS_CONV, Table(padding((0, 1)) + [
-            (2, "u32", int(a.get("groups", 1))),
-            (3, "ref", _u32v(a.get("strides", [1, 1]))),
-            (4, "ref", _u32v(a.get("dilations", [1, 1])))])
+        return ATTRS_CONV, _T("ConvAttrs", *padding(),
+                              ("groups", "u32", int(a.get("groups", 1))),
+                              ("strides", "ref", _u32v(a.get("strides", [1, 1]))),
+                              ("dilations", "ref", _u32v(a.get("dilations", [1, 1]))))
     if op_type == "ConvTranspose":
-        return ATTRS_CONV_TRANSPOSE, Table([(0, "ref", _u32v(a.get("strides", [1, 1])))] +
-                                           [(f[0] + 1, f[1], f[2]) for f in padding((0, 1))])
+        return ATTRS_CONV_TRANSPOSE, _T("ConvTransposeAttrs", ("strides", "ref", _u32v(a.get("strides", [1, 1]))),
+                                        *padding())
     if op_type in ("MaxPool", "AveragePool"):
-        f = [(0, "ref", _u32v(a["kernel_size"]))] + padding((1, 2)) + [
-            (3, "ref", _u32v(a.get("strides", [1, 1])))]
+        f = [("kernel_size", "ref", _u32v(a["kernel_size"]))] + padding() + [
+            ("strides", "ref", _u32v(a.get("strides", [1, 1])))]
         if op_type == "AveragePool":
-            f.append((4, "bool", int(bool(a.get("count_include_pad", 0)))))
-            return ATTRS_AVERAGE_POOL, Table(f)
-        return ATTRS_MAX_POOL, Table(f)
+            f.append(("count_include_pad", "bool", int(bool(a.get("count_include_pad", 0)))))
+            return ATTRS_AVERAGE_POOL, _T("AveragePoolAttrs", *f)
+        return ATTRS_MAX_POOL, _T("MaxPoolAttrs", *f)
     if op_type == "BatchNormalization":
-        return ATTRS_BATCH_NORM, Table([(0, "f32", float(a.get("epsilon", 1e-5)))])
+        return ATTRS_BATCH_NORM, _T("BatchNormalizationAttrs", ("epsilon", "f32", float(a.get("epsilon", 1e-5))))
     if op_type == "Gemm":
-        return ATTRS_GEMM, Table([(0, "f32", float(a.get("alpha", 1.0))),
-                                  (1, "f32", float(a.get("beta", 1.0))),
-                                  (2, "bool", int(bool(a.get("transA", 0)))),
-                                  (3, "bool", int(bool(a.get("transB", 0))))])
+        return ATTRS_GEMM, _T("GemmAttrs", ("alpha", "f32", float(a.get("alpha", 1.0))),
+                              ("beta", "f32", float(a.get("beta", 1.0))),
+                              ("transpose_a", "bool", int(bool(a.get("transA", 0)))),
+                              ("transpose_b", "bool", int(bool(a.get("transB", 0)))))
     if op_type == "Flatten":
-        return ATTRS_FLATTEN, Table([(0, "i32", int(a.get("axis", 1)))])
+        return ATTRS_FLATTEN, _T("FlattenAttrs", ("axis", "i32", int(a.get("axis", 1))))
     if op_type == "Softmax":
-        return ATTRS_SOFTMAX, Table([(0, "i32", int(a.get("axis", -1)))])
+        return ATTRS_SOFTMAX, _T("SoftmaxAttrs", ("axis", "i32", int(a.get("axis", -1))))
     if op_type == "LayerNormalization":
-        return ATTRS_LAYER_NORM, Table([(0, "i32", int(a.get("axis", -1))),
-                                        (1, "f32", float(a.get("epsilon", 1e-5)))])
+        return ATTRS_LAYER_NORM, _T("LayerNormalizationAttrs", ("axis", "i32", int(a.get("axis", -1))),
+                                    ("epsilon", "f32", float(a.get("epsilon", 1e-5))))
     if op_type == "Transpose":
         perm = a.get("perm")
-        return ATTRS_TRANSPOSE, Table([(0, "ref", _u32v(perm) if perm is not None else None)])
+        return ATTRS_TRANSPOSE, _T("TransposeAttrs", ("perm", "ref", _u32v(perm) if perm is not None else None))
     if op_type == "Reshape":
-        return ATTRS_RESHAPE, Table([(0, "bool", int(bool(a.get("allowzero", 0))))])
+        return ATTRS_RESHAPE, _T("ReshapeAttrs", ("allow_zero", "bool", int(bool(a.get("allowzero", 0)))))
     if op_type == "Gelu":
-        return ATTRS_GELU, Table([])
+        return ATTRS_GELU, _T("GeluAttrs")
     if op_type == "Gather":
-        return ATTRS_GATHER, Table([(0, "i32", int(a.get("axis", 0)))])
+        return ATTRS_GATHER, _T("GatherAttrs", ("axis", "i32", int(a.get("axis", 0))))
     if op_type == "Cast":
         # CastAttrs::to, sg::DataType: Int32 = 0 (the schema default), Float = 1
-        return ATTRS_CAST, Table([(0, "u8", int(a.get("to", 0)))])
+        return ATTRS_CAST, _T("CastAttrs", ("to", "u8", int(a.get("to", 0))))
     if op_type == "Concat":
-        return ATTRS_CONCAT, Table([(0, "i32", int(a.get("axis", 0)))])
+        return ATTRS_CONCAT, _T("ConcatAttrs", ("axis", "i32", int(a.get("axis", 0))))
     if op_type == "ReduceMean":
-        f = [(1, "bool", int(bool(a.get("keep_dims", 0))))]
+        f = [("keep_dims", "bool", int(bool(a.get("keep_dims", 0))))]
         if a.get("axes") is not None:
-            f.append((0, "ref", Vector("i32", [int(x) for x in a["axes"]])))
-        return ATTRS_REDUCE_MEAN, Table(f)
+            f.append(("axes", "ref", Vector("i32", [int(x) for x in a["axes"]])))
+        return ATTRS_REDUCE_MEAN, _T("ReduceMeanAttrs", *f)
     if op_type == "ConstantOfShape":
         v = a.get("value", 0)
         is_float = a.get("dtype") == "float" or isinstance(v, float)
-        scalar = Table([(0, "f32", float(v))]) if is_float else Table([(0, "i32", int(v))])
-        return ATTRS_CONSTANT_OF_SHAPE, Table([(0, "u8", SCALAR_FLOAT if is_float else SCALAR_INT),
-                                               (1, "ref", scalar)])
+        scalar = _T("FloatScalar", ("value", "f32", float(v))) if is_float else _T("IntScalar", ("value", "i32", int(v)))
+        return ATTRS_CONSTANT_OF_SHAPE, _T("ConstantOfShapeAttrs",
+                                           ("value_type", "u8", SCALAR_FLOAT if is_float else SCALAR_INT),
+                                           ("value", "ref", scalar))
     return 0, None
 
 
@@ -235,7 +275,7 @@ def to_rten_bytes(spec, inline_max: int = INLINE_MAX_ELEMS) -> bytes:
     nodes = []
     for n in spec.nodes:
         if n.kind == "value":
-            data = Table([(0, "ref", None)])
+            data = _T("ValueNode", ("shape", "ref", None))
             kind = NODE_VALUE
         elif n.kind == "const":
             arr = np.asarray(n.data)
@@ -243,31 +283,32 @@ def to_rten_bytes(spec, inline_max: int = INLINE_MAX_ELEMS) -> bytes:
             arr = arr.astype("<i4" if is_int else "<f4")
             shape = _u32v(arr.shape)
             if arr.size <= inline_max:
-                payload = Table([(0, "ref", Vector("i32" if is_int else "f32", arr.reshape(-1).tolist()))])
-                data = Table([(0, "ref", shape), (1, "u8", CONST_INT_DATA if is_int else CONST_FLOAT_DATA),
-                              (2, "ref", payload)])
+                payload = _T("IntData" if is_int else "FloatData",
+                             ("data", "ref", Vector("i32" if is_int else "f32", arr.reshape(-1).tolist())))
+                data = _T("ConstantNode", ("shape", "ref", shape),
+                          ("data_type", "u8", CONST_INT_DATA if is_int else CONST_FLOAT_DATA), ("data", "ref", payload))
             else:
                 pad = (-tensor_off) % TENSOR_ALIGN
                 tensor_off += pad
                 tensors.append((tensor_off, arr))
-                data = Table([(0, "ref", shape), (3, "u16", DTYPE_INT32 if is_int else DTYPE_FLOAT32),
-                              (4, "u64", tensor_off)])
+                data = _T("ConstantNode", ("shape", "ref", shape),
+                          ("dtype", "u16", DTYPE_INT32 if is_int else DTYPE_FLOAT32), ("data_offset", "u64", tensor_off))
                 tensor_off += arr.size * 4
             kind = NODE_CONSTANT
         else:
             at, attrs = _op_attrs(n.op_type, n.attrs)
-            fields = [(0, "u8", OP_TYPES.index(n.op_type)),
-                      (3, "ref", Vector("i32", [-1 if i is None else index[i] for i in n.inputs])),
-                      (4, "ref", Vector("i32", [index[o] for o in n.outputs]))]
+            fields = [("type_", "u8", OP_TYPES.index(n.op_type)),
+                      ("inputs", "ref", Vector("i32", [-1 if i is None else index[i] for i in n.inputs])),
+                      ("outputs", "ref", Vector("i32", [index[o] for o in n.outputs]))]
             if attrs is not None:
-                fields += [(1, "u8", at), (2, "ref", attrs)]
-            data = Table(fields)
+                fields += [("attrs_type", "u8", at), ("attrs", "ref", attrs)]
+            data = _T("OperatorNode", *fields)
             kind = NODE_OPERATOR
-        nodes.append(Table([(0, "ref", String(n.name)), (1, "u8", kind), (2, "ref", data)]))
-    graph = Table([(0, "ref", Vector("ref", nodes)),
-                   (1, "ref", _u32v([index[i] for i in spec.inputs])),
-                   (2, "ref", _u32v([index[o] for o in spec.outputs]))])
-    model = Table([(0, "i32", 1), (1, "ref", graph)])
+        nodes.append(_T("Node", ("name", "ref", String(n.name)), ("data_type", "u8", kind), ("data", "ref", data)))
+    graph = _T("Graph", ("nodes", "ref", Vector("ref", nodes)),
+               ("inputs", "ref", _u32v([index[i] for i in spec.inputs])),
+               ("outputs", "ref", _u32v([index[o] for o in spec.outputs])))
+    model = _T("Model", ("schema_version", "i32", 1), ("graph", "ref", graph))
     fb = _Builder().finish(model)
     tensor_data_offset = (HEADER_LEN + len(fb) + TENSOR_ALIGN - 1) // TENSOR_ALIGN * TENSOR_ALIGN
     out = bytearray(b"RTEN" + struct.pack("<IQQQ", 2, HEADER_LEN, len(fb), tensor_data_offset))
