@@ -84,6 +84,7 @@ Plan::~Plan() {
   if (mm_pack) (void)hipFree(mm_pack);
   for (auto& kv : conv_unfused)
     if (kv.second.first) (void)hipFree(kv.second.first);
+
   for (auto& kv : side_events) {
     if (kv.second.first) (void)hipEventDestroy(kv.second.first);
     if (kv.second.second) (void)hipEventDestroy(kv.second.second);
@@ -758,13 +759,59 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     for (int i : nodes[op].inputs)
       if (i >= 0) uses[i]++;
     if (nodes[op].fused_residual >= 0) uses[nodes[op].fused_residual]++;
+    auto ef = p.expand_fused.find(op);
+    if (ef != p.expand_fused.end()) uses[ef->second]++;
   }
   std::set<int> outset(out_ids.begin(), out_ids.end());
 
   // Convs that run on the DMA GEMM.
+  // Expand -> depthwise pairs (Node::fe_op) whose shapes the fused kernel
+  // takes: the expand op leaves the plan, the depthwise op runs both.
+  {
+    std::set<int> in_plan(p.ops.begin(), p.ops.end());
+    std::set<int> outset0(out_ids.begin(), out_ids.end());
+    auto uses_of_value = [&](const std::vector<int>& ops, int v) {  // reads of v by ops
+      int cnt = 0;
+      for (int op : ops) {
+        for (int i : nodes[op].inputs) cnt += i == v;
+        cnt += nodes[op].fused_residual == v;
+      }
+      return cnt;
+    };
+    std::vector<int> drop;
+    for (int op : p.ops) {
+      const Node& n = nodes[op];
+      if (n.op_type != "Conv" || n.fe_op < 0 || !in_plan.count(n.fe_op)) continue;
+      const Node& e = nodes[n.fe_op];
+      if (e.outputs.size() != 1 || n.inputs[0] != e.outputs[0] || outset0.count(e.outputs[0]) ||
+          uses_of_value(p.ops, e.outputs[0]) != 1)
+        continue;
+      const Shape* xs = shape_of(e.inputs[0]);
+      const Shape& ys = shapes[n.outputs[0]];
+      if (!xs || xs->size() != 4 || p.dtypes[e.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
+      ConvAttrs ca = conv_attrs(n, false);
+      int64_t ohw[2], fp[4];
+      const bool ok = ca.mode == 0 && ca.dil == std::vector<int64_t>{1, 1} && ca.strides.size() == 2 &&
+                      ca.strides[0] == ca.strides[1] &&
+                      output_size_and_padding((*xs)[2], (*xs)[3], 3, 3, ca.strides[0], ca.strides[1], 0,
+                                              ca.pads.data(), 1, 1, ohw, fp) == RTENHIP_OK &&
+                      ys[2] == ohw[0] && ys[3] == ohw[1] &&
+                      expand_dw_eligible((int)(*xs)[1], (int)(*xs)[3], (int)ca.strides[0], (int)fp[0], (int)fp[1],
+                                         (int)fp[2], (int)fp[3]);
+      if (!ok) continue;
+      p.expand_fused[op] = e.inputs[0];
+      drop.push_back(n.fe_op);
+    }
+    if (!drop.empty()) {
+      std::vector<int> kept;
+      for (int op : p.ops)
+        if (std::find(drop.begin(), drop.end(), op) == drop.end()) kept.push_back(op);
+      p.ops = kept;
+    }
+  }
   for (int op : p.ops) {
     const Node& n = nodes[op];
-    if (n.op_type != "Conv" || n.inputs.size() < 2) continue;
+    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op)) continue;
     const Shape* xs = shape_of(n.inputs[0]);
     const Shape* ws = shape_of(n.inputs[1]);
     if (!xs || !ws || nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
@@ -1065,6 +1112,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       for (int i : n.inputs)
         if (i >= 0) drop_use(i);
       if (n.fused_residual >= 0) drop_use(n.fused_residual);
+      auto ef = p.expand_fused.find(op);
+      if (ef != p.expand_fused.end()) drop_use(ef->second);
     }
     auto dd = deferred_drops.find(op);
     if (dd != deferred_drops.end()) {
@@ -1166,6 +1215,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       return rtenhip_cast_f32_to_i32(c, &x, reinterpret_cast<rtenhip_tensor_i32*>(&y));
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
   }
+  if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv") {
     auto cit = p.convs.find(op_id);
     if (cit != p.convs.end() && ctx->use_dma) return exec_conv_dma(p, op_id, cit->second);
@@ -1350,6 +1400,30 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   std::string msg = "Unsupported operator type: " + t;
   set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
   return RTENHIP_UNSUPPORTED_VALUE;
+}
+
+// Expand (1x1) -> depthwise (3x3) pair (Node::fe_op) the plan runs as one
+// mbconv.hip launch, reading the expand's input.
+rtenhip_status Graph::exec_expand_dw(Plan& p, int op_id) {
+  const Node& n = nodes[op_id];
+  const Node& e = nodes[n.fe_op];
+  const int xv = p.expand_fused[op_id];
+  const Shape* xsp = plan_shape(*this, p, xv);
+  const Shape* ysp = plan_shape(*this, p, n.outputs[0]);
+  if (!xsp || !ysp) return fail(RTENHIP_HIP_ERROR, "expand+depthwise: missing shapes");
+  const Shape& xs = *xsp;
+  const Shape& ys = *ysp;
+  const float* be = e.inputs.size() > 2 && e.inputs[2] >= 0 ? ptr_of(p, e.inputs[2]) : nullptr;
+  const float* bd = n.inputs.size() > 2 && n.inputs[2] >= 0 ? ptr_of(p, n.inputs[2]) : nullptr;
+  ConvAttrs ca = conv_attrs(n, false);
+  int64_t ohw[2], fp[4];
+  rtenhip_status st = output_size_and_padding(xs[2], xs[3], 3, 3, ca.strides[0], ca.strides[1], 0, ca.pads.data(), 1,
+                                              1, ohw, fp);
+  if (st) return st;
+  return launch_expand_dw(ptr_of(p, xv), ptr_of(p, e.inputs[1]), be, ptr_of(p, n.inputs[1]), bd,
+                          ptr_of(p, n.outputs[0]), (int)xs[0], (int)xs[1], (int)ys[1], (int)xs[2], (int)xs[3],
+                          (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0], (int)fp[1], e.fused_act, e.act_lo,
+                          e.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -2299,6 +2373,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if ((n.op_type == "Conv" || n.op_type == "MatMul") &&
             (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0))
           key = n.op_type + "(fused)";
+        if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -2490,6 +2565,39 @@ rtenhip_status Graph::optimize() {
       conv.outputs[0] = a.outputs[0];
       fused++;
     }
+  }
+  // MobileNetV2 inverted residual: Conv 1x1 expand (+ its fused activation)
+  // whose only consumer is a depthwise 3x3 Conv -> one node that runs both
+  // (mbconv.hip); the depthwise conv now reads the expand's input.
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& e = nodes[i];
+    if (e.kind != NodeKind::Operator || e.removed || e.op_type != "Conv" || e.fused_residual >= 0 ||
+        e.outputs.size() != 1 || e.inputs.size() < 2 || !e.input_perm.empty())
+      continue;
+    const int wv = e.inputs[1];
+    if (wv < 0 || nodes[wv].kind != NodeKind::Constant || nodes[wv].shape.size() != 4 || nodes[wv].shape[2] != 1 ||
+        nodes[wv].shape[3] != 1)
+      continue;
+    const int bv = e.inputs.size() > 2 ? e.inputs[2] : -1;
+    if (bv >= 0 && nodes[bv].kind != NodeKind::Constant) continue;
+    ConvAttrs ea = conv_attrs(e, false);
+    if (ea.mode != 0 || ea.groups != 1 || ea.pads != std::vector<int64_t>{0, 0, 0, 0} ||
+        ea.strides != std::vector<int64_t>{1, 1} || ea.dil != std::vector<int64_t>{1, 1})
+      continue;
+    const int d_op = sole(e.outputs[0]);
+    if (d_op < 0) continue;
+    Node& dn = nodes[d_op];
+    if (dn.removed || dn.op_type != "Conv" || dn.fused_residual >= 0 || dn.fe_op >= 0 || dn.inputs.size() < 2 ||
+        dn.inputs[0] != e.outputs[0] || !dn.input_perm.empty())
+      continue;
+    const int dw = dn.inputs[1];
+    const int64_t hidden = nodes[wv].shape[0];
+    if (dw < 0 || nodes[dw].kind != NodeKind::Constant || nodes[dw].shape != Shape{hidden, 1, 3, 3} ||
+        (int64_t)dn.attrs.num("groups", 1) != hidden || (dn.inputs.size() > 2 && dn.inputs[2] >= 0 &&
+                                                         nodes[dn.inputs[2]].kind != NodeKind::Constant))
+      continue;
+    dn.fe_op = i;
+    fused++;
   }
   // FusedTranspose (optimize.rs:329-378): a MatMul reads a Transpose's input
   // as a permuted view instead of the materialised copy.  The Transpose stays

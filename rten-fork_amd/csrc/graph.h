@@ -99,6 +99,11 @@ struct Node {
   int fused_residual = -1;   // value id added after the bias
   int fused_act = 0;         // RTENHIP_ACT_*
   float act_lo = 0.f, act_hi = 0.f;
+  // MobileNetV2's expand -> depthwise pair (Graph::optimize): the 1x1 expand
+  // Conv whose only consumer is this depthwise Conv.  A plan whose shapes the
+  // fused kernel takes (mbconv.hip) drops that op and runs both here, reading
+  // the expand's input; otherwise both run as they are.
+  int fe_op = -1;
   // MatMul epilogue: constant [N] added per column after the K fold
   // (MatMul -> Add(bias)), before the residual and the activation.
   int fused_colbias = -1;
@@ -170,6 +175,9 @@ struct Plan {
   // output's shape): the conv runs into this plan-owned buffer, then the Add
   // and the activation run as the unfused graph would.  op id -> (buffer, shape).
   std::map<int, std::pair<float*, Shape>> conv_unfused;
+  // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
+  // the expand's input value, which the depthwise op then reads.
+  std::map<int, int> expand_fused;
   float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
   int64_t mm_pack_floats = 0;
   // What mm_pack holds during a run: the A value it was packed from (value
@@ -262,6 +270,7 @@ struct Graph {
                  int out_dtype, HostVal& out, rtenhip_status& st);
   rtenhip_status exec_data_op(Plan& p, int op_id, bool& handled);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
+  rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   rtenhip_status exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& a,

@@ -214,3 +214,59 @@ def test_valu_conv_rebound_to_misaligned_views(rh, monkeypatch, mode, kh, pads):
         res = g.run(feed, g.output_ids, out=[y_off])
         torch.cuda.synchronize()
         assert _bits_equal(res[0].cpu().numpy(), exp)
+
+
+# Expand (1x1) -> depthwise (3x3) pairs run as one kernel (csrc/mbconv.hip):
+# (N, C_in, H, W, hidden, stride, expand act, dw act, biases)
+EXPAND_DW = [
+    (2, 16, 112, 112, 96, 2, "clip", "clip", True),   # MobileNetV2 features.2
+    (2, 24, 56, 56, 144, 1, "clip", "clip", True),    # features.3
+    (3, 24, 56, 56, 144, 2, "clip", "clip", True),    # features.4
+    (2, 32, 28, 28, 192, 1, "relu", "none", False),   # features.5/6 shape, other acts, no biases
+    (2, 32, 28, 28, 192, 2, "none", "relu", True),    # features.7 shape
+    (1, 16, 9, 20, 40, 1, "clip", "clip", True),      # odd H, partial band
+    (2, 24, 14, 14, 64, 1, "clip", "clip", True),     # W % 4 != 0: not taken, both convs run apart
+]
+
+
+@pytest.mark.parametrize("case", EXPAND_DW, ids=lambda c: "x".join(map(str, c[:6])) + f"-{c[6]}-{c[7]}")
+def test_expand_depthwise_fused_bitexact(rh, case):
+    """The fused expand -> depthwise kernel gives the two operators' bits
+    (conv_2d_pointwise then conv_2d_depthwise_block, with the graph's Clip /
+    Relu after each), eager and replayed; shapes it does not take run unfused."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, C, H, W, M, s, act_e, act_d, biases = case
+    rng = np.random.default_rng(C * 7 + M + s)
+    m = ModelSpec("mbconv")
+    x = m.value("x")
+    m.inputs = ["x"]
+    lo, hi = m.const("lo", np.array(0.0, np.float32)), m.const("hi", np.array(6.0, np.float32))
+
+    def act(v, a):
+        if a == "clip":
+            return m.op("Clip", [v, lo, hi])
+        return m.op("Relu", [v]) if a == "relu" else v
+
+    we = m.const("we", rng.uniform(-0.5, 0.5, (M, C, 1, 1)).astype(np.float32))
+    args = [x, we] + ([m.const("be", rng.uniform(-0.2, 0.2, (M,)).astype(np.float32))] if biases else [])
+    e = act(m.op("Conv", args, {"pads": [0, 0, 0, 0], "strides": [1, 1]}, name="expand"), act_e)
+    wd = m.const("wd", rng.uniform(-0.5, 0.5, (M, 1, 3, 3)).astype(np.float32))
+    args = [e, wd] + ([m.const("bd", rng.uniform(-0.2, 0.2, (M,)).astype(np.float32))] if biases else [])
+    m.outputs = [act(m.op("Conv", args, {"pads": [1, 1, 1, 1], "strides": [s, s], "groups": M}, name="dw"), act_d)]
+    ins = {"x": rng.uniform(-1, 2, (N, C, H, W)).astype(np.float32)}
+    exp = graph_runner.run(m, ins)[m.outputs[0]]
+    g = m.to_graph()
+    xd = torch.from_numpy(ins["x"]).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
+    g.set_timing(True)
+    g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    fused = "Conv(expand+dw)" in g.timing_report()
+    assert fused == (W % 4 == 0), g.timing_report()
