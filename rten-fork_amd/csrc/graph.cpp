@@ -796,8 +796,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
                       output_size_and_padding((*xs)[2], (*xs)[3], 3, 3, ca.strides[0], ca.strides[1], 0,
                                               ca.pads.data(), 1, 1, ohw, fp) == RTENHIP_OK &&
                       ys[2] == ohw[0] && ys[3] == ohw[1] &&
-                      expand_dw_eligible((int)(*xs)[1], (int)(*xs)[3], (int)ca.strides[0], (int)fp[0], (int)fp[1],
-                                         (int)fp[2], (int)fp[3]);
+                      expand_dw_eligible((int)(*xs)[1], (int)(*xs)[2], (int)(*xs)[3], (int)ca.strides[0], (int)fp[0],
+                                         (int)fp[1], (int)fp[2], (int)fp[3]);
       if (!ok) continue;
       p.expand_fused[op] = e.inputs[0];
       drop.push_back(n.fe_op);

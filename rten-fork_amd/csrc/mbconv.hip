@@ -128,14 +128,112 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   }
 }
 
-// Whether the fused kernel takes this pair: C_in in {16, 24, 32} (the x band
-// in VGPRs), 3x3 depthwise with stride 1 or 2, no dilation, pads <= 1, W a
-// multiple of 4 with a band of rows that fits one pass of 256 threads.
-bool expand_dw_eligible(int cin, int W, int S, int pt, int pl, int pb, int pr) {
-  if (cin != 16 && cin != 24 && cin != 32) return false;
+// Small planes (MobileNetV2's 14x14 and 7x7 stages, C_in 64..160): a block
+// owns one image and a chunk of channels; the image's whole x plane set
+// (C_in x H*W) is staged in LDS once.  Each wave works on one channel
+// sub-group (planes of at most 64 pixels: four sub-groups, a lane per pixel;
+// larger planes: one sub-group, a thread per pixel), MC channels at a time:
+// each x value read from LDS feeds MC fma chains, and the sub-group's weight
+// rows are wave-uniform (scalar loads).  The G = sub-groups x MC expand
+// planes of a pass go to LDS, then the pass's depthwise outputs.  Same
+// arithmetic as expand_dw_kernel.
+template <int S, int MC>
+__global__ __launch_bounds__(256) void expand_dw_flat_kernel(ExpandDwDesc d, int cin) {
+  extern __shared__ float4 edf_lds4[];
+  const int P = d.H * d.W, OP = d.OH * d.OW;
+  const bool small = P <= 64;
+  const int subs = small ? 4 : 1;
+  const int G = subs * MC;  // channels per pass
+  float* xs = reinterpret_cast<float*>(edf_lds4);   // [cin][P]
+  float* es = xs + cin * P;                          // [G][P + margins]
+  const int estride = P + 2 * kEdMargin;
+  const int n = blockIdx.y;
+  const int c_begin = blockIdx.z * d.cpb;
+  const int c_end = min(d.hidden, c_begin + d.cpb);
+  const int t = threadIdx.x;
+  {
+    const float* xp = d.x + (int64_t)n * cin * P;
+    const int total = cin * P;
+    if ((total & 3) == 0 && ((uintptr_t)xp & 15) == 0) {
+      for (int i = t; i < total / 4; i += 256) reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xp)[i];
+    } else {
+      for (int i = t; i < total; i += 256) xs[i] = xp[i];
+    }
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int px = small ? (t & 63) : t;
+  const int sub = small ? wave : 0;
+  const bool e_on = px < P;
+  for (int c0 = c_begin; c0 < c_end; c0 += G) {
+    const int cs = __builtin_amdgcn_readfirstlane(c0 + sub * MC);  // this wave's first channel
+    if (e_on) {
+      float acc[MC];
+#pragma unroll
+      for (int o = 0; o < MC; o++) acc[o] = 0.f;
+      // Channels past c_end read weight row c_end - 1 (their values are unused).
+      const float* __restrict__ wrow[MC];
+#pragma unroll
+      for (int o = 0; o < MC; o++) wrow[o] = d.we + (int64_t)min(cs + o, c_end - 1) * cin;
+#pragma unroll 4
+      for (int k = 0; k < cin; k++) {
+        const float xv = xs[k * P + px];
+#pragma unroll
+        for (int o = 0; o < MC; o++) acc[o] = __fmaf_rn(wrow[o][k], xv, acc[o]);
+      }
+#pragma unroll
+      for (int o = 0; o < MC; o++) {
+        float v = acc[o];
+        if (d.be) v = __fadd_rn(v, d.be[min(cs + o, c_end - 1)]);
+        es[(sub * MC + o) * estride + kEdMargin + px] = ed_act(v, d.act_e, d.lo_e, d.hi_e);
+      }
+    }
+    __syncthreads();
+    const int ng = min(G, c_end - c0);
+    for (int o = t; o < ng * OP; o += 256) {
+      const int g = o / OP, q = o - g * OP;
+      const int oy = q / d.OW, ox = q - oy * d.OW;
+      const int c = c0 + g;
+      const float* eb = es + g * estride + kEdMargin;
+      const float* __restrict__ wk = d.wd + (int64_t)c * 9;
+      float acc = d.bd ? d.bd[c] : 0.f;
+#pragma unroll
+      for (int ky = 0; ky < 3; ky++) {
+        const int r = oy * S + ky - d.pt;
+        if (r < 0 || r >= d.H) continue;
+        const float* row = eb + r * d.W + ox * S - d.pl;
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++) {
+          if (ox < d.omin[kx] || ox >= d.omax[kx]) continue;
+          acc = __fadd_rn(acc, __fmul_rn(row[kx], wk[ky * 3 + kx]));
+        }
+      }
+      d.y[(((int64_t)n * d.hidden + c) * d.OH + oy) * d.OW + ox] = ed_act(acc, d.act_d, d.lo_d, d.hi_d);
+    }
+    // The next pass overwrites the expand planes.
+    __syncthreads();
+  }
+}
+
+static int flat_mc(int P) { return P <= 64 ? 8 : 16; }
+static int flat_g(int P) { return (P <= 64 ? 4 : 1) * flat_mc(P); }
+
+static bool flat_ok(int cin, int H, int W) {
+  const int P = H * W;
+  if (P > 256 || P < 1) return false;
+  const size_t lds = ((size_t)cin * P + (size_t)flat_g(P) * (P + 2 * kEdMargin)) * sizeof(float);
+  return lds <= 100 * 1024;
+}
+
+// Whether a fused kernel takes this pair: 3x3 depthwise, stride 1 or 2, no
+// dilation, pads <= 1, and either C_in in {16, 24, 32} with W a multiple of 4
+// (banded kernel, the x band in VGPRs) or a plane of at most 256 pixels whose
+// channels fit LDS (flat kernel).
+bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, int pr) {
   if (S != 1 && S != 2) return false;
-  if (W % 4 != 0 || W / 4 > 256 / 3 || pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
-  return (256 / (W / 4)) >= 3;  // at least one output row per band
+  if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
+  const bool banded = (cin == 16 || cin == 24 || cin == 32) && W % 4 == 0 && W / 4 <= 256 / 3;
+  return banded || flat_ok(cin, H, W);
 }
 
 rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be, const float* wd, const float* bd,
@@ -168,6 +266,31 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
     const int t = W + pl - kx > 0 ? W + pl - kx : 0;
     const int omax = (t + S - 1) / S;
     d.omax[kx] = omax > OW ? OW : omax;
+  }
+  const bool banded = (cin == 16 || cin == 24 || cin == 32) && W % 4 == 0 && W / 4 <= 256 / 3;
+  if (!banded) {
+    if (!flat_ok(cin, H, W)) return fail(RTENHIP_UNSUPPORTED_VALUE, "expand+depthwise: plane too large");
+    const int P = H * W, G = flat_g(P);
+    int chunks = 1;
+    while ((int64_t)N * chunks < 512 && hidden / (chunks * 2) >= G) chunks *= 2;
+    d.cpb = (hidden + chunks - 1) / chunks;
+    d.cpb = (d.cpb + G - 1) / G * G;
+    chunks = (hidden + d.cpb - 1) / d.cpb;
+    const size_t lds = ((size_t)cin * P + (size_t)G * (P + 2 * kEdMargin)) * sizeof(float);
+    dim3 grid(1u, (unsigned)N, (unsigned)chunks);
+    if (flat_mc(P) == 8) {
+      if (S == 1)
+        hipLaunchKernelGGL((expand_dw_flat_kernel<1, 8>), grid, dim3(256), lds, s, d, cin);
+      else
+        hipLaunchKernelGGL((expand_dw_flat_kernel<2, 8>), grid, dim3(256), lds, s, d, cin);
+    } else {
+      if (S == 1)
+        hipLaunchKernelGGL((expand_dw_flat_kernel<1, 16>), grid, dim3(256), lds, s, d, cin);
+      else
+        hipLaunchKernelGGL((expand_dw_flat_kernel<2, 16>), grid, dim3(256), lds, s, d, cin);
+    }
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
   }
   // Band: the most output rows whose input rows fit one pass of 256 threads.
   const int W4 = W / 4;

@@ -167,15 +167,39 @@ def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
     return total
 
 
+def _expand_dw_fused(cin: int, h: int, w: int) -> bool:
+    """Whether csrc/mbconv.hip runs an expand -> depthwise pair of these
+    shapes as one kernel (expand_dw_eligible: banded or whole-plane)."""
+    banded = cin in (16, 24, 32) and w % 4 == 0
+    p = h * w
+    g = (4 * 8) if p <= 64 else 16
+    flat = p <= 256 and (cin * p + g * (p + 8)) * 4 <= 100 * 1024
+    return banded or flat
+
+
 def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
     """Algorithmic HBM bytes of every Conv (and the classifier Gemm) in
     ``spec`` at input [batch, 3, hw, hw], as the fused graph moves them: each
     conv reads its input and weights (+ bias) once and writes its output once;
     a residual Add fused into the conv's epilogue reads its other operand once;
-    Relu / Clip ride in the epilogue (no traffic).  The HBM-roofline figure for
-    bandwidth-bound models (MobileNetV2)."""
+    Relu / Clip ride in the epilogue (no traffic); an expand -> depthwise pair
+    run as one kernel (mbconv.hip) neither writes nor reads the expand output.
+    The HBM-roofline figure for bandwidth-bound models (MobileNetV2,
+    SURVEY.md §8d)."""
     shapes = {spec.inputs[0]: (batch, 3, hw, hw)}
     consts = {n.name: n.data.shape for n in spec.nodes if n.kind == "const"}
+    producer = {o: n for n in spec.nodes if n.kind == "op" for o in n.outputs}
+
+    def source_conv(v):
+        """The 1x1 Conv behind value v (through a Clip / Relu), or None."""
+        n = producer.get(v)
+        if n is not None and n.op_type in ("Clip", "Relu"):
+            n = producer.get(n.inputs[0])
+        if n is None or n.op_type != "Conv" or consts[n.inputs[1]][2:] != (1, 1):
+            return None
+        return n
+
+    fused_e, fused_d = set(), set()
     total = 0.0
     for n in spec.nodes:
         if n.kind != "op":
@@ -187,7 +211,14 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
             p, s = n.attrs["pads"], n.attrs["strides"]
             oh = (H + p[0] + p[2] - kh) // s[0] + 1
             ow = (W + p[1] + p[3] - kw) // s[1] + 1
-            total += 4.0 * (N * C * H * W + N * o * oh * ow + o * ci * kh * kw + o)
+            rd, wr = N * C * H * W, N * o * oh * ow
+            e = source_conv(n.inputs[0])
+            if n.attrs.get("groups", 1) == C and (kh, kw) == (3, 3) and e is not None:
+                ex = shapes[e.inputs[0]]
+                if _expand_dw_fused(ex[1], ex[2], ex[3]):
+                    rd = 0  # the expand output never reaches HBM
+                    total -= 4.0 * N * C * H * W  # nor is written by the expand
+            total += 4.0 * (rd + wr + o * ci * kh * kw + o)
             shapes[n.outputs[0]] = (N, o, oh, ow)
         elif n.op_type == "Add":
             total += 4.0 * float(np.prod(xs))  # the residual operand

@@ -225,7 +225,11 @@ EXPAND_DW = [
     (2, 32, 28, 28, 192, 1, "relu", "none", False),   # features.5/6 shape, other acts, no biases
     (2, 32, 28, 28, 192, 2, "none", "relu", True),    # features.7 shape
     (1, 16, 9, 20, 40, 1, "clip", "clip", True),      # odd H, partial band
-    (2, 24, 14, 14, 64, 1, "clip", "clip", True),     # W % 4 != 0: not taken, both convs run apart
+    (2, 64, 14, 14, 384, 1, "clip", "clip", True),    # features.8-11 (whole-plane kernel)
+    (2, 96, 14, 14, 576, 2, "clip", "clip", True),    # features.14, stride 2
+    (3, 160, 7, 7, 960, 1, "clip", "clip", True),     # features.15-17 (four planes per block)
+    (2, 24, 14, 14, 40, 1, "relu", "none", False),    # whole-plane kernel, partial channel pass
+    (1, 48, 20, 20, 64, 1, "clip", "clip", True),     # neither kernel: both convs run apart
 ]
 
 
@@ -269,4 +273,4 @@ def test_expand_depthwise_fused_bitexact(rh, case):
     g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
     torch.cuda.synchronize()
     fused = "Conv(expand+dw)" in g.timing_report()
-    assert fused == (W % 4 == 0), g.timing_report()
+    assert fused == ((C in (16, 24, 32) and W % 4 == 0) or H * W <= 256), g.timing_report()
