@@ -127,71 +127,110 @@ bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, 
   return x_elems < (int64_t(1) << 29) && K >= 1 && O / groups >= 1;
 }
 
+// DmaDesc of group g of a conv (everything but the split / persistence
+// fields).  lat: the latency GEMM's addressing (lat-packed A, and for 1x1
+// kernels koff(k) = k * Hp * Wp without a table).
+static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaTile& tile, const int* tab,
+                           DmaDesc& d) {
+  const int64_t opg = a.O / a.groups, ipg = a.C / a.groups;
+  const int64_t K = ipg * a.kh * a.kw, P = a.oh * a.ow;
+  const int64_t per_group = lat ? lat_packed_floats((int)opg, (int)K) : packed_a_floats((int)opg, (int)K, tile);
+  const int64_t x_total = a.N * a.C * a.Hp * a.Wp;
+  d = DmaDesc{};
+  d.M = (int)opg;
+  d.N = (int)(a.N * P);
+  d.K = (int)K;
+  d.tile = tile;
+  d.apk = a.packed_w + g * per_group;
+  d.x = a.xin + g * ipg * a.Hp * a.Wp;
+  d.x_bytes = (uint32_t)((x_total - g * ipg * a.Hp * a.Wp) * 4);
+  d.x_img = a.C * a.Hp * a.Wp;
+  d.ystride = a.sh * a.Wp;
+  d.xstride = a.sw;
+  d.OW = (int)a.ow;
+  d.P = (int)P;
+  d.fdOW = make_fastdiv((uint32_t)a.ow);
+  d.fdP = make_fastdiv((uint32_t)P);
+  d.ktab4 = tab;
+  d.out_img = a.y_img;
+  d.out_c = P;  // channel stride of an unpadded output plane
+  d.out_row = a.ow;
+  d.out_off = 0;
+  if (a.y_row) {
+    // padded output planes: (oh + 2*pad) x y_row, interior at y_off
+    d.out_c = a.y_img / a.O;
+    d.out_row = a.y_row;
+    d.out_off = a.y_off;
+  }
+  d.out = a.y + g * opg * d.out_c;
+  d.residual = a.residual ? a.residual + g * opg * P : nullptr;
+  d.res_img = a.O * P;
+  d.res_c = P;
+  d.bias = a.bias ? a.bias + g * opg : nullptr;
+  d.alpha = 1.f;
+  d.beta = 0.f;
+  d.vec4 = (P % 4 == 0 && d.out_c == P && d.out_row == a.ow && d.out_off == 0 && d.out_img % 4 == 0 &&
+            d.res_img % 4 == 0 && g * opg * P % 4 == 0 && ((uintptr_t)a.y % 16) == 0 &&
+            (!a.residual || ((uintptr_t)a.residual % 16) == 0))
+               ? 1
+               : 0;
+  d.act = a.act;
+  d.act_lo = a.lo;
+  d.act_hi = a.hi;
+  if (lat && a.kh == 1 && a.kw == 1) d.kstride = (int)(a.Hp * a.Wp);
+}
+
+rtenhip_status lat_conv_desc(Ctx* c, const ConvDmaArgs& a, DmaDesc& d) {
+  if (a.groups != 1) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency conv descriptor: grouped conv");
+  const int* tab = nullptr;
+  if (!(a.kh == 1 && a.kw == 1)) {
+    tab = c->dtab((int)a.C, (int)a.Hp, (int)a.Wp, (int)a.kh, (int)a.kw, (int)a.dh, (int)a.dw);
+    if (!tab) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
+  }
+  fill_conv_desc(a, 0, true, DmaTile{16, 256, 1}, tab, d);
+  return RTENHIP_OK;
+}
+
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
   const int64_t opg = a.O / a.groups, ipg = a.C / a.groups;
   const int64_t K = ipg * a.kh * a.kw, P = a.oh * a.ow;
+  const bool lat = is_lat_cfg(a.cfg);
   const int cfg = a.cfg >= 0 ? a.cfg : dma_default_cfg((int)opg, (int)(a.N * P), (int)K);
-  const DmaTile tile = dma_cfg_tile(cfg);
-  const int* tab = c->dtab((int)ipg, (int)a.Hp, (int)a.Wp, (int)a.kh, (int)a.kw, (int)a.dh,
-                           (int)a.dw);
-  if (!tab) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
-  const int64_t per_group = packed_a_floats((int)opg, (int)K, tile);
-  const int64_t x_total = a.N * a.C * a.Hp * a.Wp;
+  const DmaTile tile = lat ? DmaTile{16, 256, 1} : dma_cfg_tile(cfg);
+  // 1x1 kernels: koff(k) = k * Hp * Wp for any stride (no table needed by the
+  // latency GEMM).
+  const bool one_by_one = a.kh == 1 && a.kw == 1;
+  const int* tab = nullptr;
+  if (!(lat && one_by_one)) {
+    tab = c->dtab((int)ipg, (int)a.Hp, (int)a.Wp, (int)a.kh, (int)a.kw, (int)a.dh, (int)a.dw);
+    if (!tab) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
+  }
   for (int64_t g = 0; g < a.groups; g++) {
-    DmaDesc d{};
-    d.M = (int)opg;
-    d.N = (int)(a.N * P);
-    d.K = (int)K;
-    d.tile = tile;
-    d.apk = a.packed_w + g * per_group;
-    d.x = a.xin + g * ipg * a.Hp * a.Wp;
-    d.x_bytes = (uint32_t)((x_total - g * ipg * a.Hp * a.Wp) * 4);
-    d.x_img = a.C * a.Hp * a.Wp;
-    d.ystride = a.sh * a.Wp;
-    d.xstride = a.sw;
-    d.OW = (int)a.ow;
-    d.P = (int)P;
-    d.fdOW = make_fastdiv((uint32_t)a.ow);
-    d.fdP = make_fastdiv((uint32_t)P);
-    d.ktab4 = tab;
-    d.out_img = a.y_img;
-    d.out_c = P;  // channel stride of an unpadded output plane
-    d.out_row = a.ow;
-    d.out_off = 0;
-    if (a.y_row) {
-      // padded output planes: (oh + 2*pad) x y_row, interior at y_off
-      d.out_c = a.y_img / a.O;
-      d.out_row = a.y_row;
-      d.out_off = a.y_off;
+    DmaDesc d;
+    fill_conv_desc(a, g, lat, tile, tab, d);
+    if (lat) {
+      const DmaSplit sp = lat_split_plan(d.M, d.N, d.K, cfg - kLatCfgBase);
+      if (sp.split_tiles > 0) {
+        if (!a.split || !a.ws || !a.counters || sp.ws_floats > a.ws_cap || sp.counters > a.cnt_cap)
+          return fail(RTENHIP_INVALID_VALUE, "latency conv: K-block workspace missing or too small");
+        d.ws = a.ws;
+        d.counters = a.counters;
+      }
+      rtenhip_status st = launch_gemm_lat(d, cfg - kLatCfgBase, c->stream);
+      if (st) return st;
+      continue;
     }
-    d.out = a.y + g * opg * d.out_c;
-    d.residual = a.residual ? a.residual + g * opg * P : nullptr;
-    d.res_img = a.O * P;
-    d.res_c = P;
-    d.bias = a.bias ? a.bias + g * opg : nullptr;
-    d.alpha = 1.f;
-    d.beta = 0.f;
-    d.vec4 = (P % 4 == 0 && d.out_c == P && d.out_row == a.ow && d.out_off == 0 &&
-              d.out_img % 4 == 0 && d.res_img % 4 == 0 && g * opg * P % 4 == 0 &&
-              ((uintptr_t)a.y % 16) == 0 && (!a.residual || ((uintptr_t)a.residual % 16) == 0))
-                 ? 1
-                 : 0;
-    d.act = a.act;
-    d.act_lo = a.lo;
-    d.act_hi = a.hi;
     // 16-byte B copies: pointwise stride-1 convs (B[k][n] = x[img][k][p],
     // linear in k) whose 4-pixel groups stay inside one image.
-    const bool pointwise = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 &&
-                           a.Hp == a.oh && a.Wp == a.ow;
-    if (pointwise && dma_cfg_bvec(cfg) && P % 4 == 0 && K % tile.bk == 0 &&
-        (a.C * a.Hp * a.Wp) % 4 == 0 && ((uintptr_t)d.x % 16) == 0) {
+    const bool pointwise = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.Hp == a.oh && a.Wp == a.ow;
+    if (pointwise && dma_cfg_bvec(cfg) && P % 4 == 0 && K % tile.bk == 0 && (a.C * a.Hp * a.Wp) % 4 == 0 &&
+        ((uintptr_t)d.x % 16) == 0) {
       d.bvec = 1;
       d.kstride = (int)(a.Hp * a.Wp);
     }
     if (a.split) {
       const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
-      if (sp.split_tiles > 0 && a.ws && a.counters && sp.ws_floats <= a.ws_cap &&
-          sp.counters <= a.cnt_cap) {
+      if (sp.split_tiles > 0 && a.ws && a.counters && sp.ws_floats <= a.ws_cap && sp.counters <= a.cnt_cap) {
         d.split_tiles = sp.split_tiles;
         d.nkb = sp.nkb;
         d.ws = a.ws;
@@ -331,6 +370,14 @@ bool conv_takes_dma(const ConvPlan& p) {
 
 rtenhip_status pack_conv_weights(Ctx* c, const float* w, const ConvPlan& p, int cfg, float* out) {
   const int64_t opg = p.O / p.groups, K = (p.C / p.groups) * p.kh * p.kw;
+  if (is_lat_cfg(cfg)) {
+    const int64_t per = lat_packed_floats((int)opg, (int)K);
+    for (int64_t g = 0; g < p.groups; g++) {
+      rtenhip_status st = launch_pack_lat(w + g * opg * K, K, (int)opg, (int)K, out + g * per, c->stream);
+      if (st) return st;
+    }
+    return RTENHIP_OK;
+  }
   const DmaTile tile = dma_cfg_tile(cfg);
   const int64_t per_group = packed_a_floats((int)opg, (int)K, tile);
   for (int64_t g = 0; g < p.groups; g++) {
@@ -343,6 +390,7 @@ rtenhip_status pack_conv_weights(Ctx* c, const float* w, const ConvPlan& p, int 
 
 int64_t packed_conv_weight_floats(const ConvPlan& p, int cfg) {
   const int64_t opg = p.O / p.groups, K = (p.C / p.groups) * p.kh * p.kw;
+  if (is_lat_cfg(cfg)) return lat_packed_floats((int)opg, (int)K) * p.groups;
   return packed_a_floats((int)opg, (int)K, dma_cfg_tile(cfg)) * p.groups;
 }
 

@@ -87,6 +87,10 @@ struct ConvDmaArgs {
   int64_t H, W, pad_t, pad_l;
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
+// The latency GEMM's descriptor of an ungrouped conv (conv chains), without
+// split workspace: the caller sets d.ws / d.counters when K > 256.
+struct DmaDesc;
+rtenhip_status lat_conv_desc(Ctx* c, const ConvDmaArgs& a, DmaDesc& d);
 
 // Pointwise convs on the vector ALUs (conv_pointwise.hip): 1x1 / stride 1 /
 // unpadded / ungrouped, K <= 256, P % 4 == 0, unpadded output; mc = output
@@ -107,6 +111,11 @@ rtenhip_status conv_pw_valu(const ConvDmaArgs& a, int variant, hipStream_t s);
 // DMA-config numbers at and above this select the pointwise VALU kernel,
 // variant cfg - kPwCfgBase (graph tuner).
 constexpr int kPwCfgBase = 1000;
+// Config numbers in [kLatCfgBase, kPwCfgBase) select the latency GEMM
+// (gemm_lat.hip), variant cfg - kLatCfgBase; like the DMA configurations they
+// read the zero-bordered input and use the plan's split workspace.
+constexpr int kLatCfgBase = 500;
+inline bool is_lat_cfg(int cfg) { return cfg >= kLatCfgBase && cfg < kPwCfgBase; }
 bool conv_dma_eligible(int64_t N, int64_t C, int64_t Hp, int64_t Wp, int64_t O, int64_t groups,
                        int64_t K);
 

@@ -86,4 +86,15 @@ rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const Dm
                              float* out, hipStream_t s);
 rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s);
 
+// Latency GEMM (gemm_lat.hip): the same DmaDesc addressing and summation
+// order, one wave per 16x16 output tile and KC block (small-batch convs).
+// variant = 10 * (waves along M: 1, 2, 4) + (16-row tiles per wave: 1, 2);
+// A packed by launch_pack_lat; kstride > 0 selects koff(k) = k * kstride
+// (no K table); with K > 256, ws / counters sized by lat_split_plan.
+bool lat_variant_ok(int variant);
+int64_t lat_packed_floats(int M, int K);
+rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float* out, hipStream_t s);
+DmaSplit lat_split_plan(int M, int N, int K, int variant);
+rtenhip_status launch_gemm_lat(const DmaDesc& d, int variant, hipStream_t s);
+
 }  // namespace rtenhip

@@ -1,0 +1,150 @@
+// Latency GEMM for small-batch convolutions (ResNet-50 at batch 1).
+//
+// At batch 1 a ResNet-50 conv is 25..230 MFLOP: spread over 1024 SIMDs that
+// is 0.4..1.5 us of MFMA, so the DMA GEMM's 64x64 tiles (few blocks, each
+// paying an LDS-DMA prologue, 16 barriers per KC block and an LDS-staged
+// epilogue) leave most of the chip idle and the launch latency-bound.  This
+// kernel keeps the reference's summation contract (src/gemm.rs:733-1050, as
+// the DMA kernel states it: one fma chain per output element and KC = 256
+// block, starting from +0, the blocks folded in K order after the bias) and
+// instead cuts the work into the smallest units MFMA allows:
+//   - one wave = one 16-row x 16-column output tile of ONE KC block
+//     (v_mfma_f32_16x16x4_f32 is bitwise the k-ordered fmaf chain, see
+//     profiles/r2_mfma_shape_probe.txt), MI such tiles stacked along M;
+//   - every operand goes straight from global memory into registers (no LDS
+//     staging, no barriers in the K loop): A is pre-packed per (16 rows, KC
+//     block) so a lane's 4 MFMA steps are one float4, B is gathered with
+//     buffer loads whose per-lane offset is colbase(n) + koff(k) (the DMA
+//     kernel's addressing: zero-bordered inputs, out-of-range reads return 0);
+//   - all of a block's loads are issued before the first MFMA, so a unit
+//     costs one memory round trip plus 64 MFMA steps;
+//   - with K > 256 every tile's chains go to a workspace and the last KC
+//     block to arrive folds them in K order (agent-scope counter), exactly
+//     as the DMA kernel's split tiles do.
+// Workgroups of 4 waves: WMW waves along M (sharing B) x 4/WMW along N
+// (sharing A); workgroup ids are remapped XCD-contiguously so the units that
+// share an A panel run on one XCD's L2.
+#include "lat_unit.h"
+
+namespace rtenhip {
+
+template <int WMW, int MI>
+__global__ __launch_bounds__(256) void gemm_lat_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
+  constexpr int WNW = 4 / WMW;
+  __shared__ uint32_t ktl[4][LKC];  // per wave: this block's k offsets, [k % 4][k / 4]
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // XCD-contiguous remap (dispatch is round-robin over the 8 XCDs): XCD x
+  // owns a contiguous range of work ids, ordered (kb, tm, tn) with tn fastest.
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
+  const int o = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tn = o % wg_n;
+  const int t2 = o / wg_n;
+  const int tm = t2 % wg_m;
+  const int kb = t2 / wg_m;
+  const int wm = wave / WNW, wn = wave - (wave / WNW) * WNW;
+  const int sub0 = (tm * WMW + wm) * MI;  // first 16-row subtile of this wave
+  const int n0 = (tn * WNW + wn) * 16;
+  if (sub0 >= subs || n0 >= d.N) return;  // wave past the matrix edge (no counters touched)
+  const int wt = (tm * WMW + wm) * (wg_n * WNW) + (n0 >> 4);
+  lat_unit<MI, false>(d, sub0, n0, kb, nkb, subs, wt, ktl[wave], LatNoWait{}, LatNoDone{});
+}
+
+// A[M, K] (row stride lda) -> [ceil(M/16)][nkb][16 groups][64 lanes] float4:
+// lane (c, h) of group g of block kb holds row 16*sub + c, k = 256*kb + 16*g +
+// 4*j + h for j = 0..3; zero past M and K.
+__global__ __launch_bounds__(256) void pack_lat_kernel(const float* __restrict__ a, int64_t lda, int M, int K,
+                                                       int nkb, int64_t total4, float4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const int lane = (int)(i & 63);
+  const int g = (int)((i >> 6) & (LGROUPS - 1));
+  const int64_t t = i >> 10;
+  const int kb = (int)(t % nkb);
+  const int64_t sub = t / nkb;
+  const int64_t row = sub * 16 + (lane & 15);
+  const int kbase = kb * LKC + 16 * g + (lane >> 4);
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int k = kbase + 4 * j;
+    v[j] = (row < M && k < K) ? a[row * lda + k] : 0.f;
+  }
+  out[i] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+int64_t lat_packed_floats(int M, int K) {
+  const int64_t subs = (M + 15) / 16, nkb = (K + LKC - 1) / LKC;
+  return subs * nkb * LKC * 16;
+}
+
+rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float* out, hipStream_t s) {
+  const int64_t total4 = lat_packed_floats(M, K) / 4;
+  if (total4 == 0) return RTENHIP_OK;
+  const int nkb = (K + LKC - 1) / LKC;
+  hipLaunchKernelGGL(pack_lat_kernel, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, s, a, lda, M, K, nkb,
+                     total4, reinterpret_cast<float4*>(out));
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+bool lat_variant_ok(int v) {
+  const int wmw = v / 10, mi = v % 10;
+  return (wmw == 1 || wmw == 2 || wmw == 4) && (mi == 1 || mi == 2);
+}
+
+struct LatGrid {
+  int subs, wg_m, wg_n, nkb;
+  int64_t wgs, tiles;
+};
+static LatGrid lat_grid(int M, int N, int K, int v) {
+  const int wmw = v / 10, mi = v % 10, wnw = 4 / wmw;
+  LatGrid g;
+  g.subs = (M + 15) / 16;
+  g.wg_m = (g.subs + wmw * mi - 1) / (wmw * mi);
+  g.wg_n = ((N + 15) / 16 + wnw - 1) / wnw;
+  g.nkb = (K + LKC - 1) / LKC;
+  g.wgs = (int64_t)g.wg_m * g.wg_n * g.nkb;
+  g.tiles = (int64_t)g.wg_m * wmw * g.wg_n * wnw;
+  return g;
+}
+
+DmaSplit lat_split_plan(int M, int N, int K, int v) {
+  DmaSplit sp{0, 0, 0, 0};
+  if (!lat_variant_ok(v)) return sp;
+  const LatGrid g = lat_grid(M, N, K, v);
+  if (g.nkb < 2) return sp;
+  sp.split_tiles = (int)g.tiles;
+  sp.nkb = g.nkb;
+  sp.ws_floats = g.tiles * g.nkb * (v % 10) * 256;
+  sp.counters = g.tiles;
+  return sp;
+}
+
+template <int WMW, int MI>
+static void lat_launch(const DmaDesc& d, const LatGrid& g, hipStream_t s) {
+  hipLaunchKernelGGL((gemm_lat_kernel<WMW, MI>), dim3((unsigned)g.wgs), dim3(256), 0, s, d, g.wg_m, g.wg_n, g.nkb,
+                     g.subs);
+}
+
+rtenhip_status launch_gemm_lat(const DmaDesc& d, int v, hipStream_t s) {
+  if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty latency GEMM");
+  if (!lat_variant_ok(v)) return fail(RTENHIP_INVALID_VALUE, "unknown latency GEMM variant");
+  if (d.cin) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM: beta * C not supported");
+  if (d.kstride <= 0 && !d.ktab4) return fail(RTENHIP_INVALID_VALUE, "latency GEMM: no K table");
+  const LatGrid g = lat_grid(d.M, d.N, d.K, v);
+  if (g.wgs > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM grid too large");
+  if (g.nkb > 1 && (!d.ws || !d.counters)) return fail(RTENHIP_INVALID_VALUE, "latency GEMM needs its K-block workspace");
+  switch (v) {
+    case 41: lat_launch<4, 1>(d, g, s); break;
+    case 21: lat_launch<2, 1>(d, g, s); break;
+    case 11: lat_launch<1, 1>(d, g, s); break;
+    case 42: lat_launch<4, 2>(d, g, s); break;
+    case 22: lat_launch<2, 2>(d, g, s); break;
+    default: lat_launch<1, 2>(d, g, s); break;
+  }
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+}  // namespace rtenhip

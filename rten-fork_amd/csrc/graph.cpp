@@ -15,6 +15,7 @@
 //    hipEvent times aggregated by operator type.
 #include "graph.h"
 #include "gemm_dma.h"
+#include "chain.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -89,6 +90,19 @@ Plan::~Plan() {
     if (kv.second.first) (void)hipEventDestroy(kv.second.first);
     if (kv.second.second) (void)hipEventDestroy(kv.second.second);
   }
+  for (auto& c : chains) c.release();
+}
+
+void ConvChain::release() {
+  if (layers_dev) (void)hipFree(layers_dev);
+  if (ctrl) (void)hipFree(ctrl);
+  if (ws) (void)hipFree(ws);
+  for (float* b : packed) (void)hipFree(b);
+  layers_dev = nullptr;
+  ctrl = nullptr;
+  ws = nullptr;
+  packed.clear();
+  use = false;
 }
 
 // FusedTranspose: the permuted view of an operator input (PermuteSpec::apply,
@@ -1781,46 +1795,28 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
   return gemm_dense_dma(ctx, da);
 }
 
-// DMA conv with plan-owned packed weights and zero-bordered inputs/outputs.
-// On the plan's first (eager) run the kernel configuration is chosen by
-// timing the candidates on the real operands; all configurations give
-// bit-identical results, so this only affects speed.
-rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
+// Operands of a DMA / latency conv as the plan lays them out: the input
+// zero-bordered by its producer (PaddedValue) or as is (an unpadded conv, or
+// a padded one whose caller pads it into scratch), the output plain or into
+// its consumer's zero-bordered planes, bias, fused residual and activation.
+void Graph::conv_io_args(Plan& p, int op_id, ConvDmaArgs& a) {
   const Node& n = nodes[op_id];
-  const ConvPlan& g = ce.g;
-  hipStream_t s = ctx->stream;
+  const ConvPlan& g = p.convs.at(op_id).g;
   const int64_t P = g.oh * g.ow;
-  ConvDmaArgs a{};
-  // Input: zero-bordered by its producer, padded here, or used as is.
-  const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
   auto pin = p.padded.find(n.inputs[0]);
-  // A direct VALU conv reads the unpadded input and pads in place.
-  const bool direct_cfg = ce.cfg >= kPwCfgBase + kPwDirect;
   if (pin == p.padded.end()) {
     a.x_unpadded = ptr_of(p, n.inputs[0]);
     a.H = g.H;
     a.W = g.W;
     a.pad_t = g.pads[0];
     a.pad_l = g.pads[1];
-  }
-  if (pin != p.padded.end()) {
-    a.xin = pin->second.base;
-    a.Hp = pin->second.phys[2];
-    a.Wp = pin->second.phys[3];
-  } else if (has_pad && !direct_cfg) {
-    a.Hp = g.H + g.pads[0] + g.pads[2];
-    a.Wp = g.W + g.pads[1] + g.pads[3];
-    float* xp = ctx->scratch_floats((size_t)(g.N * g.C * a.Hp * a.Wp), 1);
-    if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
-    rtenhip_status st = launch_pad_nchw(ptr_of(p, n.inputs[0]), xp, g.N * g.C, (int)g.H, (int)g.W,
-                                        (int)g.pads[0], (int)g.pads[1], (int)g.pads[2],
-                                        (int)g.pads[3], s);
-    if (st) return st;
-    a.xin = xp;
-  } else {
     a.xin = ptr_of(p, n.inputs[0]);
     a.Hp = g.H;
     a.Wp = g.W;
+  } else {
+    a.xin = pin->second.base;
+    a.Hp = pin->second.phys[2];
+    a.Wp = pin->second.phys[3];
   }
   a.N = g.N;
   a.C = g.C;
@@ -1839,8 +1835,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   a.act = n.fused_act;
   a.lo = n.act_lo;
   a.hi = n.act_hi;
-  const int out = n.outputs[0];
-  auto pout = p.padded.find(out);
+  auto pout = p.padded.find(n.outputs[0]);
   if (pout != p.padded.end()) {
     const PaddedValue& pv = pout->second;
     a.y = pv.base;
@@ -1848,9 +1843,39 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     a.y_row = pv.phys[3];
     a.y_off = pv.pads[0] * pv.phys[3] + pv.pads[1];
   } else {
-    a.y = ptr_of(p, out);
+    a.y = ptr_of(p, n.outputs[0]);
     a.y_img = g.O * P;
   }
+}
+
+// DMA conv with plan-owned packed weights and zero-bordered inputs/outputs.
+// On the plan's first (eager) run the kernel configuration is chosen by
+// timing the candidates on the real operands; all configurations give
+// bit-identical results, so this only affects speed.
+rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
+  const Node& n = nodes[op_id];
+  const ConvPlan& g = ce.g;
+  hipStream_t s = ctx->stream;
+  const int64_t P = g.oh * g.ow;
+  ConvDmaArgs a{};
+  const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
+  auto pin = p.padded.find(n.inputs[0]);
+  // A direct VALU conv reads the unpadded input and pads in place.
+  const bool direct_cfg = ce.cfg >= kPwCfgBase + kPwDirect;
+  conv_io_args(p, op_id, a);
+  if (pin == p.padded.end() && has_pad && !direct_cfg) {
+    // Zero-bordered copy of the input in ctx scratch.
+    a.Hp = g.H + g.pads[0] + g.pads[2];
+    a.Wp = g.W + g.pads[1] + g.pads[3];
+    float* xp = ctx->scratch_floats((size_t)(g.N * g.C * a.Hp * a.Wp), 1);
+    if (!xp) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
+    rtenhip_status st = launch_pad_nchw(ptr_of(p, n.inputs[0]), xp, g.N * g.C, (int)g.H, (int)g.W,
+                                        (int)g.pads[0], (int)g.pads[1], (int)g.pads[2],
+                                        (int)g.pads[3], s);
+    if (st) return st;
+    a.xin = xp;
+  }
+  auto pout = p.padded.find(n.outputs[0]);
   const float* w = ptr_of(p, n.inputs[1]);
   const int64_t opg = g.O / g.groups, K = (g.C / g.groups) * g.kh * g.kw;
   // KC-split buffers for (cfg, split), plan-owned (no ctx scratch, so side-
@@ -1858,7 +1883,8 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   auto set_split = [&](ConvExec& e, int cfg, bool split) -> rtenhip_status {
     e.split = false;
     if (!split) return RTENHIP_OK;
-    const DmaSplit sp = dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg);
+    const DmaSplit sp = is_lat_cfg(cfg) ? lat_split_plan((int)opg, (int)(g.N * P), (int)K, cfg - kLatCfgBase)
+                                        : dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg);
     if (sp.split_tiles == 0) return RTENHIP_OK;
     if (sp.ws_floats > e.ws_floats) {
       if (e.ws) RTENHIP_HIP_CHECK(hipFree(e.ws));
@@ -1932,7 +1958,12 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     const bool pw_forced = (pw_ok && pw_valu_mode > 0 && pw_valu_mode < kPwDirect && pw_variant_ok(pw_valu_mode, K)) ||
                            (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32));
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
-    if (autotune && cs == hipStreamCaptureStatusNone && !pw_forced) {
+    const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode);
+    if (lat_forced) {
+      chosen = kLatCfgBase + lat_mode;
+      chosen_split = true;
+    }
+    if (autotune && cs == hipStreamCaptureStatusNone && !pw_forced && !lat_forced) {
       // Candidates are timed alone: a side-stream branch still running would
       // share the CUs and skew the choice.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
@@ -1993,6 +2024,29 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           st = time_it(3, false, ms);  // best of three: robust to one-off interference
           if (st) return st;
           cands.push_back({ms, cfg, split, trial.persist, pk});
+        }
+      }
+      // Latency GEMM variants (small batches: one wave per 16x16 tile and KC
+      // block); their K-block fold is part of the kernel (split always on).
+      if (lat_mode != 0) {
+        for (int v : {41, 21, 11, 42, 22, 12}) {
+          if (lat_mode > 0 && v != lat_mode) continue;
+          const int cfg = kLatCfgBase + v;
+          float* pk = nullptr;
+          RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
+          bufs.push_back(pk);
+          rtenhip_status st = pack_for(cfg, pk);
+          if (st) return st;
+          trial.persist = 0;
+          st = set_split(trial, cfg, true);
+          if (st) return st;
+          bind(trial);
+          a.packed_w = pk;
+          a.cfg = cfg;
+          float ms = 0;
+          st = time_it(3, false, ms);
+          if (st) return st;
+          cands.push_back({ms, cfg, 1, 0, pk});
         }
       }
       if (pw_ok && pw_valu_mode != 0) {
@@ -2092,7 +2146,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     st = set_split(ce, chosen, chosen_split && chosen < kPwCfgBase);
     if (st) return st;
     ce.cfg = chosen;
-    ce.persist = chosen >= kPwCfgBase ? 0 : persist_mode >= 0 ? persist_mode : chosen_persist;
+    ce.persist = (chosen >= kPwCfgBase || is_lat_cfg(chosen)) ? 0 : persist_mode >= 0 ? persist_mode : chosen_persist;
     if (chosen >= kPwCfgBase) {
       ce.fb_cfg = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
       RTENHIP_HIP_CHECK(hipMalloc(&ce.fb_packed, (size_t)packed_conv_weight_floats(g, ce.fb_cfg) * 4));
@@ -2244,6 +2298,29 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, ev_in, 0));
   ctx->stream = exec_stream;
   rtenhip_status st = RTENHIP_OK;
+  // Conv chains: formed once the first (tuning) run has chosen each conv's
+  // kernel, and again whenever the arena moved (descriptors hold its pointers).
+  if (plan->eager_runs >= 1 && (!plan->chains_built || plan->chains_arena != arena)) {
+    if (plan->exec) {
+      (void)hipGraphExecDestroy(plan->exec);
+      plan->exec = nullptr;
+      same_binding = false;
+    }
+    st = build_chains(*plan);
+    if (st) {
+      ctx->stream = caller;
+      return st;
+    }
+  }
+  // One op, or the chain it heads (the chain's other members are skipped).
+  auto run_op = [&](int op) -> rtenhip_status {
+    auto ci = plan->chain_of.find(op);
+    if (ci != plan->chain_of.end() && plan->chains[ci->second].use) {
+      ConvChain& c = plan->chains[ci->second];
+      return op == c.ops[0] ? exec_chain(*plan, c) : RTENHIP_OK;
+    }
+    return exec_op(*plan, op);
+  };
   // Launch one op on its stream: side ops fork from the main stream and
   // record completion; a join op first waits for the side ops it reads.
   // Timing runs keep every op on the main stream so per-op times do not
@@ -2310,7 +2387,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       if (e == hipSuccess) {
         for (int op : plan->ops) {
           st = before_op(op);
-          if (!st) st = exec_op(*plan, op);
+          if (!st) st = run_op(op);
           if (!st) st = after_op(op);
           if (st) break;
         }
@@ -2342,7 +2419,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         (void)hipEventCreate(&b);
         (void)hipEventRecord(a, stream_of(op));
       }
-      st = exec_op(*plan, op);
+      st = run_op(op);
       if (timing) {
         (void)hipEventRecord(b, stream_of(op));
         evs.push_back({a, b});
@@ -2359,6 +2436,18 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     if (!st) st = join_all();
     if (!st) st = copy_static_outputs();
     plan->eager_runs++;
+    // Eager runs check their chains' error word (a dependency wait that timed
+    // out means the grid was not resident; the outputs are not valid).
+    for (ConvChain& c : plan->chains) {
+      if (st || !c.use) continue;
+      int err = 0;
+      if (hipMemcpyAsync(&err, c.ctrl + chain_error_index((int)c.ops.size()), 4, hipMemcpyDeviceToHost,
+                         exec_stream) != hipSuccess ||
+          hipStreamSynchronize(exec_stream) != hipSuccess)
+        st = fail(RTENHIP_HIP_ERROR, "conv chain check failed");
+      else if (err)
+        st = fail(RTENHIP_HIP_ERROR, "conv chain: a dependency wait timed out");
+    }
     if (timing && !st) {
       (void)hipStreamSynchronize(exec_stream);
       std::map<std::string, std::pair<double, int>> tot;
@@ -2374,6 +2463,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
             (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0))
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
+        auto ci = plan->chain_of.find(plan->ops[i]);
+        if (ci != plan->chain_of.end() && plan->chains[ci->second].use)
+          key = plan->chains[ci->second].ops[0] == plan->ops[i] ? "ConvChain" : "Conv(chained)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -2386,7 +2478,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       for (auto& kv : tot) rows.push_back({kv.second.first, kv.first});
       std::sort(rows.rbegin(), rows.rend());
       std::ostringstream os;
-      char buf[256];
+      char buf[512];
       snprintf(buf, sizeof buf, "Graph run of %zu ops finished in %.3f ms (device time)\n",
                plan->ops.size(), total);
       os << buf;
@@ -2396,6 +2488,12 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         os << buf;
       }
       // Per-op rows (RTEN_TIMING "by-shape" analogue): name, type, output shape.
+      for (const ConvChain& c : plan->chains) {
+        snprintf(buf, sizeof buf, "conv chain %s .. %s (%zu convs, %d units, grid %d): %.4f ms as one launch, %.4f ms one by one%s\n",
+                 nodes[c.ops.front()].name.c_str(), nodes[c.ops.back()].name.c_str(), c.ops.size(), c.items, c.grid,
+                 c.chain_ms, c.ops_ms, c.use ? " (used)" : " (not used)");
+        os << buf;
+      }
       os << "--- per op ---\n";
       for (size_t i = 0; i < evs.size(); i++) {
         const Node& n = nodes[plan->ops[i]];
@@ -2415,7 +2513,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           const long long gm = cg.O, gn = cg.N * cg.oh * cg.ow, gk = cg.KC * cg.kh * cg.kw;
           const double fl = 2.0 * gm * (double)gn * gk;
           const int cc = ce->second.cfg;
-          const std::string cname = cc >= kPwCfgBase ? "valu" + std::to_string(cc - kPwCfgBase) : std::to_string(cc);
+          const std::string cname = cc >= kPwCfgBase   ? "valu" + std::to_string(cc - kPwCfgBase)
+                                    : is_lat_cfg(cc) ? "lat" + std::to_string(cc - kLatCfgBase)
+                                                     : std::to_string(cc);
           snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%s%s%s %.1f TF/s", gm, gn, gk,
                    cname.c_str(), ce->second.split ? " split" : "", pers_tag(ce->second.persist), ms > 0 ? fl / (ms * 1e9) : 0.0);
           os << buf;
@@ -2773,6 +2873,8 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->use_side_stream = s[0] != '0';
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
+  if (const char* s = getenv("RTENHIP_LAT")) g->lat_mode = atoi(s);
+  if (const char* s = getenv("RTENHIP_CHAIN")) g->chain_mode = atoi(s);
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

@@ -165,6 +165,22 @@ struct PaddedValue {
   Shape phys;
 };
 
+// A run of consecutive convs of a plan executed by one persistent launch of
+// latency-GEMM units (conv_chain.hip).  Built after the plan's first (eager,
+// tuning) run and kept when it times faster than the same convs one by one.
+struct ConvChain {
+  std::vector<int> ops;         // plan ops, in plan order; ops[0] launches the chain
+  void* layers_dev = nullptr;   // ChainLayer[ops.size()]
+  int* ctrl = nullptr;          // control words (chain.h), zeroed per launch
+  size_t ctrl_bytes = 0;
+  float* ws = nullptr;          // split-K workspaces of all layers
+  std::vector<float*> packed;   // chain-owned buffers: lat-packed weights, private activations
+  int items = 0, grid = 0;
+  bool use = false;
+  float chain_ms = 0, ops_ms = 0;  // build-time comparison
+  void release();
+};
+
 struct Plan {
   ~Plan();
   std::vector<int> ops;               // topological order
@@ -210,6 +226,12 @@ struct Plan {
   uint64_t scratch_gen = 0;                // Ctx::scratch_gen when exec was captured
   std::map<size_t, size_t> scratch_need;   // ctx scratch slot -> floats (eager runs)
   int eager_runs = 0;
+  // Conv chains (see ConvChain) and the chain of each member op; built once
+  // per arena (the layer descriptors hold arena pointers).
+  std::vector<ConvChain> chains;
+  std::map<int, int> chain_of;
+  bool chains_built = false;
+  void* chains_arena = nullptr;
 };
 
 struct Graph {
@@ -229,6 +251,8 @@ struct Graph {
   bool use_hip_graph = true;
   bool autotune = true;  // time DMA conv configurations on a plan's first run
   int persist_mode = -1; // DMA GEMM launches: -1 tuned, 0 never persistent, k: always, k blocks/CU
+  int lat_mode = -1;     // latency GEMM convs (gemm_lat.hip): -1 tuned, 0 never, v > 0 forced variant
+  int chain_mode = 0;    // conv chains: -1 kept when faster, 0 never (default: measured slower), 1 always (RTENHIP_CHAIN)
   int pw_valu_mode = -1; // pointwise convs on the VALU kernel: -1 tuned, 0 never, v > 0 forced variant (pw_variant_ok)
   std::string timing_report;
   std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
@@ -270,6 +294,9 @@ struct Graph {
                  int out_dtype, HostVal& out, rtenhip_status& st);
   rtenhip_status exec_data_op(Plan& p, int op_id, bool& handled);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
+  void conv_io_args(Plan& p, int op_id, ConvDmaArgs& a);
+  rtenhip_status build_chains(Plan& p);
+  rtenhip_status exec_chain(Plan& p, ConvChain& c);
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);

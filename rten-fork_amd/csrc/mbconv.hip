@@ -23,6 +23,9 @@
 // the channel's weights as scalar operands) and stores them to an LDS plane
 // (double-buffered, one barrier per channel); then the band's depthwise
 // outputs are computed from LDS and stored (coalesced rows).
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 #include "vecmath.h"
 
@@ -229,10 +232,20 @@ static bool flat_ok(int cin, int H, int W) {
 // dilation, pads <= 1, and either C_in in {16, 24, 32} with W a multiple of 4
 // (banded kernel, the x band in VGPRs) or a plane of at most 256 pixels whose
 // channels fit LDS (flat kernel).
+//
+// Measured at MobileNetV2 batch 128 (profiles/r3_mbconv_fused_vs_split.txt)
+// the expand's VALU fma chains run far below the MFMA pointwise conv, so only
+// the pair where the saved HBM round trip outweighs that is fused by default:
+// C_in = 16 (features.2, a 616 MB intermediate per batch).  RTENHIP_EXPAND_DW
+// = "all" takes every eligible pair (tests), "0" none.
 bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, int pr) {
   if (S != 1 && S != 2) return false;
   if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
+  const char* e = getenv("RTENHIP_EXPAND_DW");
+  const bool all = e && strcmp(e, "all") == 0;
+  if (e && strcmp(e, "0") == 0) return false;
   const bool banded = (cin == 16 || cin == 24 || cin == 32) && W % 4 == 0 && W / 4 <= 256 / 3;
+  if (!all) return banded && cin == 16;
   return banded || flat_ok(cin, H, W);
 }
 

@@ -169,7 +169,12 @@ def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
 
 def _expand_dw_fused(cin: int, h: int, w: int) -> bool:
     """Whether csrc/mbconv.hip runs an expand -> depthwise pair of these
-    shapes as one kernel (expand_dw_eligible: banded or whole-plane)."""
+    shapes as one kernel by default (expand_dw_eligible: C_in = 16 banded)."""
+    return cin == 16 and w % 4 == 0
+
+
+def _expand_dw_fusable(cin: int, h: int, w: int) -> bool:
+    """Every pair a fused kernel can take (RTENHIP_EXPAND_DW=all)."""
     banded = cin in (16, 24, 32) and w % 4 == 0
     p = h * w
     g = (4 * 8) if p <= 64 else 16

@@ -6,7 +6,9 @@ plan-time tuner's candidate launches; this keeps only the steady state: the
 trailing dispatches, cut into forwards by the period of the kernel-name
 sequence, and reports per kernel (template arguments dropped) the time and
 launches per forward and the average launch duration.
-usage: rocprof_per_forward.py run_kernel_trace.csv [forwards] [min_period]
+usage: rocprof_per_forward.py run_kernel_trace.csv [forwards] [min_period] [--seq]
+(--seq: also list one forward's dispatches in order, each with its duration
+and the gap since the previous dispatch ended, averaged over the forwards)
 (min_period: dispatches per forward at least -- BERT's layers repeat inside a
 forward, so its period is given as 12 layers x 13 dispatches = 156)"""
 import csv
@@ -21,9 +23,11 @@ def short(name):
 
 
 def main():
-    path = sys.argv[1]
-    want = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-    min_period = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    seq = "--seq" in sys.argv
+    argv = [a for a in sys.argv if a != "--seq"]
+    path = argv[1]
+    want = int(argv[2]) if len(argv) > 2 else 10
+    min_period = int(argv[3]) if len(argv) > 3 else 4
     rows = [r for r in csv.DictReader(open(path)) if "rocclr" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
@@ -60,6 +64,20 @@ def main():
           f"({(t1 - t0) / 1e6 / n:.4f} ms/forward), GPU busy (union of kernels) {busy / 1e6 / n:.4f} ms/forward")
     for k, (ns, c) in sorted(per.items(), key=lambda kv: -kv[1][0]):
         print(f"  {k:42s} {ns / 1e6 / n:8.4f} ms/forward {c // n:5d} launches/forward  avg {ns / c / 1e3:8.1f} us")
+    if seq:
+        print("--- one forward, in dispatch order (us, averaged over the forwards) ---")
+        for i in range(period):
+            durs, gaps = [], []
+            for f in range(n):
+                r = tail[f * period + i]
+                durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                if f * period + i > 0:
+                    prev = tail[f * period + i - 1]
+                    gaps.append(int(r["Start_Timestamp"]) - int(prev["End_Timestamp"]))
+            name = re.sub(r"^void (rtenhip::)?", "", tail[i]["Kernel_Name"])
+            name = re.sub(r"\(.*$", "", name)
+            g = sum(gaps) / len(gaps) / 1e3 if gaps else 0.0
+            print(f"  {i:3d} {sum(durs) / len(durs) / 1e3:8.2f} gap {g:6.2f}  {name[:90]}")
 
 
 if __name__ == "__main__":

@@ -20,3 +20,7 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r3_bench.jso
 cat gpurun_out/r3_bench.json
 timeout -k 10 300 python -u bench.py --batch 1 --steps 50 --no-cpu-baseline > gpurun_out/r3_bench_b1.json 2>> gpurun_out/r3_bench.err || exit 1
 cat gpurun_out/r3_bench_b1.json
+timeout -k 10 300 python -u bench.py --model mobilenet_v2 --batch 128 --no-cpu-baseline --timing-report > gpurun_out/r3_bench_mnv2.json 2>> gpurun_out/r3_bench.err || exit 1
+head -c 600 gpurun_out/r3_bench_mnv2.json
+timeout -k 10 300 python -u bench.py --model bert --batch 32 --no-cpu-baseline --timing-report > gpurun_out/r3_bench_bert.json 2>> gpurun_out/r3_bench.err || exit 1
+head -c 600 gpurun_out/r3_bench_bert.json

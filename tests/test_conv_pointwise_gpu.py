@@ -7,6 +7,8 @@ can pick (RTENHIP_PW_VALU forces one), including partial chunks (M not a
 multiple of it), K not a multiple of the kernel's 8-deep load group, K = 1,
 no bias, and a fused residual.
 """
+import re
+
 import numpy as np
 import pytest
 
@@ -113,7 +115,11 @@ def test_mobilenet_v2_pointwise_valu(rh, monkeypatch, mode):
         g.set_timing(True)
         g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
         torch.cuda.synchronize()
-        assert g.timing_report().count("cfg=valu16") >= 20
+        # the expand convs that run fused with their depthwise (mbconv.hip)
+        # no longer appear as pointwise convs
+        rep = g.timing_report()
+        m = re.search(r"Conv\(expand\+dw\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
+        assert rep.count("cfg=valu16") + (int(m.group(1)) if m else 0) >= 20, rep
 
 
 # Direct VALU conv (3-wide kernels): (N, C, H, W, O, kh, stride, pads, tail)
@@ -234,15 +240,22 @@ EXPAND_DW = [
 
 
 @pytest.mark.parametrize("case", EXPAND_DW, ids=lambda c: "x".join(map(str, c[:6])) + f"-{c[6]}-{c[7]}")
-def test_expand_depthwise_fused_bitexact(rh, case):
+@pytest.mark.parametrize("policy", ["all", "default"])
+def test_expand_depthwise_fused_bitexact(rh, monkeypatch, case, policy):
     """The fused expand -> depthwise kernel gives the two operators' bits
     (conv_2d_pointwise then conv_2d_depthwise_block, with the graph's Clip /
-    Relu after each), eager and replayed; shapes it does not take run unfused."""
+    Relu after each), eager and replayed; shapes it does not take run unfused.
+    RTENHIP_EXPAND_DW=all fuses every pair a fused kernel can take; the
+    default only the C_in = 16 pairs (see expand_dw_eligible)."""
     import torch
     import graph_runner
     from rten_hip.graph import ModelSpec
 
     N, C, H, W, M, s, act_e, act_d, biases = case
+    if policy == "all":
+        monkeypatch.setenv("RTENHIP_EXPAND_DW", "all")
+    else:
+        monkeypatch.delenv("RTENHIP_EXPAND_DW", raising=False)
     rng = np.random.default_rng(C * 7 + M + s)
     m = ModelSpec("mbconv")
     x = m.value("x")
@@ -273,4 +286,7 @@ def test_expand_depthwise_fused_bitexact(rh, case):
     g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
     torch.cuda.synchronize()
     fused = "Conv(expand+dw)" in g.timing_report()
-    assert fused == ((C in (16, 24, 32) and W % 4 == 0) or H * W <= 256), g.timing_report()
+    if policy == "all":
+        assert fused == ((C in (16, 24, 32) and W % 4 == 0) or H * W <= 256), g.timing_report()
+    else:
+        assert fused == (C == 16 and W % 4 == 0), g.timing_report()
