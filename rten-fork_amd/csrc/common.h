@@ -111,9 +111,12 @@ rtenhip_status launch_gemm_smallm(const GemmDesc& d, float* ws, hipStream_t s);
 rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s);
 
 // gemv with the reference's summation order (gemm.rs:651-704, kernels.rs:26-194).
+// cin (optional): the beta * C operand read from cin[c * cin_stride] instead
+// of out (a broadcast Gemm C without materialising it into out first).
 rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b, int64_t b_rs,
                            int64_t b_cs, float* out, float alpha, float beta, const float* bias,
-                           int64_t ref_threads, hipStream_t s);
+                           int64_t ref_threads, hipStream_t s, const float* cin = nullptr,
+                           int64_t cin_stride = 1);
 
 // Elementwise / pooling / normalisation (elementwise.hip, pool.hip, norm.hip).
 rtenhip_status launch_unary(int op, const float* x, float* y, int64_t n, float p0, float p1,

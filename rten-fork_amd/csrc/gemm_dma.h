@@ -88,7 +88,8 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s);
 
 // Latency GEMM (gemm_lat.hip): the same DmaDesc addressing and summation
 // order, one wave per 16x16 output tile and KC block (small-batch convs).
-// variant = 10 * (waves along M: 1, 2, 4) + (16-row tiles per wave: 1, 2);
+// variant = 10 * (waves along M: 1, 2, 4) + (16-row tiles per wave: 1, 2),
+// or 90 + (16-row tiles per wave) for the workgroup-fold kernel;
 // A packed by launch_pack_lat; kstride > 0 selects koff(k) = k * kstride
 // (no K table); with K > 256, ws / counters sized by lat_split_plan.
 bool lat_variant_ok(int variant);

@@ -23,7 +23,8 @@
 //     as the DMA kernel's split tiles do.
 // Workgroups of 4 waves: WMW waves along M (sharing B) x 4/WMW along N
 // (sharing A); workgroup ids are remapped XCD-contiguously so the units that
-// share an A panel run on one XCD's L2.
+// share an A panel run on one XCD's L2.  Variants 91 / 92 instead keep all
+// K blocks of a tile in one workgroup and fold them through LDS.
 #include "lat_unit.h"
 
 namespace rtenhip {
@@ -48,6 +49,48 @@ __global__ __launch_bounds__(256) void gemm_lat_kernel(DmaDesc d, int wg_m, int 
   if (sub0 >= subs || n0 >= d.N) return;  // wave past the matrix edge (no counters touched)
   const int wt = (tm * WMW + wm) * (wg_n * WNW) + (n0 >> 4);
   lat_unit<MI, false>(d, sub0, n0, kb, nkb, subs, wt, ktl[wave], LatNoWait{}, LatNoDone{});
+}
+
+// All K blocks of one tile in one workgroup: W = min(nkb, 8) waves, wave w
+// computes blocks w, w + W, ...; the chains meet in LDS and wave 0 folds them
+// in K order -- no workspace, no arrival atomics, no round trip through the
+// memory system between the blocks and the fold (variants 91 / 92).
+template <int MI>
+__global__ __launch_bounds__(512) void gemm_lat_wg_kernel(DmaDesc d, int n16, int nkb, int subs) {
+  extern __shared__ float4 lat_wg_lds[];  // [W][LKC] k offsets (uint32), then [nkb][MI][64] chains
+  const int W = blockDim.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  uint32_t* ktl = reinterpret_cast<uint32_t*>(lat_wg_lds) + wave * LKC;
+  float4* part = lat_wg_lds + W * (LKC / 4);
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
+  const int o = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int nt = o % n16, sub0 = (o / n16) * MI;
+  const LatCol col = lat_col(d, nt * 16);
+  for (int kb = wave; kb < nkb; kb += W) {
+    lat_f32x4 acc[MI];
+    lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, LatNoWait{}, false, acc);
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+      part[(kb * MI + mi) * 64 + lane] = make_float4(acc[mi][0], acc[mi][1], acc[mi][2], acc[mi][3]);
+  }
+  LatEpi<MI> e;
+  if (wave == 0) lat_epi_loads<MI>(d, sub0, col, false, e);
+  __syncthreads();
+  if (wave != 0) return;
+  lat_f32x4 sum[MI];
+  const float alpha = d.alpha;
+  for (int kb = 0; kb < nkb; kb++)
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++) {
+      const float4 v = part[(kb * MI + mi) * 64 + lane];
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        sum[mi][r] = kb == 0 ? lat_first_block(d, vv[r], e.bias[mi][r]) : __fmaf_rn(vv[r], alpha, sum[mi][r]);
+    }
+  lat_finish<MI>(d, sub0, col, e, sum, false);
 }
 
 // A[M, K] (row stride lda) -> [ceil(M/16)][nkb][16 groups][64 lanes] float4:
@@ -89,6 +132,7 @@ rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float*
 }
 
 bool lat_variant_ok(int v) {
+  if (v == 91 || v == 92) return true;  // workgroup fold
   const int wmw = v / 10, mi = v % 10;
   return (wmw == 1 || wmw == 2 || wmw == 4) && (mi == 1 || mi == 2);
 }
@@ -111,7 +155,7 @@ static LatGrid lat_grid(int M, int N, int K, int v) {
 
 DmaSplit lat_split_plan(int M, int N, int K, int v) {
   DmaSplit sp{0, 0, 0, 0};
-  if (!lat_variant_ok(v)) return sp;
+  if (!lat_variant_ok(v) || v >= 90) return sp;  // the workgroup-fold variants need no workspace
   const LatGrid g = lat_grid(M, N, K, v);
   if (g.nkb < 2) return sp;
   sp.split_tiles = (int)g.tiles;
@@ -132,6 +176,20 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d, int v, hipStream_t s) {
   if (!lat_variant_ok(v)) return fail(RTENHIP_INVALID_VALUE, "unknown latency GEMM variant");
   if (d.cin) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM: beta * C not supported");
   if (d.kstride <= 0 && !d.ktab4) return fail(RTENHIP_INVALID_VALUE, "latency GEMM: no K table");
+  if (v >= 90) {
+    const int mi = v - 90;
+    const int subs = (d.M + 15) / 16, n16 = (d.N + 15) / 16, nkb = (d.K + LKC - 1) / LKC;
+    const int64_t tiles = (int64_t)((subs + mi - 1) / mi) * n16;
+    const int W = nkb < 8 ? nkb : 8;
+    const size_t lds = (size_t)W * LKC * 4 + (size_t)nkb * mi * 64 * 16;
+    if (tiles > 0x7fffffff || lds > 64 * 1024) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM (workgroup fold) too large");
+    if (mi == 1)
+      hipLaunchKernelGGL((gemm_lat_wg_kernel<1>), dim3((unsigned)tiles), dim3(64 * W), lds, s, d, n16, nkb, subs);
+    else
+      hipLaunchKernelGGL((gemm_lat_wg_kernel<2>), dim3((unsigned)tiles), dim3(64 * W), lds, s, d, n16, nkb, subs);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   const LatGrid g = lat_grid(d.M, d.N, d.K, v);
   if (g.wgs > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM grid too large");
   if (g.nkb > 1 && (!d.ws || !d.counters)) return fail(RTENHIP_INVALID_VALUE, "latency GEMM needs its K-block workspace");

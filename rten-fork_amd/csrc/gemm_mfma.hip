@@ -507,7 +507,8 @@ rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s) {
 __global__ void gemv_kernel(int64_t N, int64_t K, const float* __restrict__ a,
                             const float* __restrict__ b, int64_t b_rs, int64_t b_cs,
                             float* __restrict__ out, float alpha, float beta,
-                            const float* __restrict__ bias, int64_t bbs) {
+                            const float* __restrict__ bias, int64_t bbs, const float* __restrict__ cin,
+                            int64_t cin_stride) {
   int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= N) return;
   // Column chunk handled by one gemv_kernel call in the reference.
@@ -516,7 +517,7 @@ __global__ void gemv_kernel(int64_t N, int64_t K, const float* __restrict__ a,
   const int64_t full8 = start + width / 8 * 8;
   const int64_t full32 = start + width / 32 * 32;
   const int64_t kbs = b_rs == 1 ? 512 : 8;
-  float o = beta == 0.f ? 0.f : out[c];
+  float o = beta == 0.f ? 0.f : (cin ? cin[c * cin_stride] : out[c]);
   float eb = beta;
   for (int64_t k0 = 0; k0 < K; k0 += kbs) {
     const int64_t k1 = min(K, k0 + kbs);
@@ -590,7 +591,8 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(int64_t N, int64_t K,
                                                      const float* __restrict__ b, int64_t b_cs,
                                                      float* __restrict__ out, float alpha,
                                                      float beta, const float* __restrict__ bias,
-                                                     int64_t bbs) {
+                                                     int64_t bbs, const float* __restrict__ cin,
+                                                     int64_t cin_stride) {
   const int lane = threadIdx.x & 63;
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= N) return;  // whole wave
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(int64_t N, int64_t K,
   const int64_t width = min(bbs, N - start);
   const bool tiled = c < start + width / 8 * 8;
   const float* col = b + c * b_cs;
-  float o = beta == 0.f ? 0.f : out[c];
+  float o = beta == 0.f ? 0.f : (cin ? cin[c * cin_stride] : out[c]);
   float eb = beta;
   constexpr int64_t KB = 512;
   const int64_t nkb = (K + KB - 1) / KB;
@@ -653,7 +655,7 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(int64_t N, int64_t K,
 
 rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b, int64_t b_rs,
                            int64_t b_cs, float* out, float alpha, float beta, const float* bias,
-                           int64_t ref_threads, hipStream_t s) {
+                           int64_t ref_threads, hipStream_t s, const float* cin, int64_t cin_stride) {
   // Column blocks (gemm.rs:673): b_block_size = max(ceil(N / threads), 128).
   // Which columns fall in a chunk's partial 8/32-wide tile depends on it,
   // so the reference's thread count (RTEN_NUM_THREADS semantics) is a
@@ -664,12 +666,12 @@ rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b,
   if (N <= 0) return RTENHIP_OK;
   if (b_rs == 1) {
     hipLaunchKernelGGL(gemv_t_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, N, K, a, b,
-                       b_cs, out, alpha, beta, bias, bbs);
+                       b_cs, out, alpha, beta, bias, bbs, cin, cin_stride);
     RTENHIP_LAUNCH_CHECK();
     return RTENHIP_OK;
   }
   hipLaunchKernelGGL(gemv_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, N, K, a, b,
-                     b_rs, b_cs, out, alpha, beta, bias, bbs);
+                     b_rs, b_cs, out, alpha, beta, bias, bbs, cin, cin_stride);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

@@ -2029,7 +2029,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Latency GEMM variants (small batches: one wave per 16x16 tile and KC
       // block); their K-block fold is part of the kernel (split always on).
       if (lat_mode != 0) {
-        for (int v : {41, 21, 11, 42, 22, 12}) {
+        for (int v : {41, 21, 11, 42, 22, 12, 91, 92}) {
           if (lat_mode > 0 && v != lat_mode) continue;
           const int cfg = kLatCfgBase + v;
           float* pk = nullptr;

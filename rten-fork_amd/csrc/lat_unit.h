@@ -1,8 +1,10 @@
-// One unit of the latency GEMM (gemm_lat.hip, conv_chain.hip): a wave
-// computes a (16*MI) x 16 output tile of one KC block and, with K > 256,
-// the last of the tile's KC blocks to arrive folds all blocks' chains in K
-// order.  Summation contract (src/gemm.rs:733-1050, as the DMA kernel states
-// it): one fma chain per element and KC = 256 block from +0, then
+// Building blocks of the latency GEMM (gemm_lat.hip, conv_chain.hip): a wave
+// computes the chains of a (16*MI) x 16 output tile for one KC block
+// (lat_chain); the blocks of a tile are folded in K order either by the last
+// block to arrive through a global workspace (lat_unit) or inside one
+// workgroup through LDS (gemm_lat_wg_kernel); lat_finish applies the
+// epilogue.  Summation contract (src/gemm.rs:733-1050, as the DMA kernel
+// states it): one fma chain per element and KC = 256 block from +0, then
 // alpha * chain (+ bias after block 0), later blocks fma'd in K order, then
 // the column bias, the residual and the activation.
 #pragma once
@@ -29,23 +31,38 @@ struct LatNoDone {
   __device__ void operator()() const {}
 };
 
-// The unit (sub0: first 16-row subtile, n0: first column, kb: KC block, wt:
-// the tile's index into ws / counters).  ktl: this wave's 256-word LDS slot.
-// wait(): called once the unit's weight and K-table loads are in flight and
-// before its first load of x or of the residual (chain: their producers run
-// in the same launch).  CHAIN: x and the residual are read with sc1 loads,
-// the output is stored sc1 and drained, and the wave that stored the tile
-// then calls done() (the inter-layer hand-off of conv_chain.hip).
-template <int MI, bool CHAIN, typename Wait, typename Done>
-__device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const int n0, const int kb, const int nkb,
-                                         const int subs, const int wt, uint32_t* ktl, Wait wait, Done done,
-                                         int dbg = 0) {
-  // dbg (timing experiments only, results not valid across XCDs): bit 0 plain
-  // x / residual loads, bit 1 plain output stores.
-  const bool sc1_ld = CHAIN && !(dbg & 1), sc1_st = CHAIN && !(dbg & 2);
+// The output column of this lane (c = lane % 16) of a tile starting at n0,
+// and its x offset colbase(n) in bytes (DMA_OOB past N).
+struct LatCol {
+  int n, img, p, oy, ox;
+  uint32_t vcol;
+};
+__device__ __forceinline__ LatCol lat_col(const DmaDesc& d, int n0) {
+  LatCol col;
+  col.n = n0 + ((threadIdx.x & 63) & 15);
+  col.img = col.p = col.oy = col.ox = 0;
+  col.vcol = DMA_OOB;
+  if (col.n < d.N) {
+    col.img = fdiv(col.n, d.fdP);
+    col.p = col.n - col.img * d.P;
+    col.oy = fdiv(col.p, d.fdOW);
+    col.ox = col.p - col.oy * d.OW;
+    col.vcol = (uint32_t)(((int64_t)col.img * d.x_img + (int64_t)col.oy * d.ystride + (int64_t)col.ox * d.xstride) * 4);
+  }
+  return col;
+}
+
+// The chains of KC block kb: acc[mi] = fma chains over the block's k, from
+// +0.  ktl: this wave's 256-word LDS slot.  wait() runs once the weight and
+// K-table loads are in flight and before the first load of x.  sc1_ld: x is
+// read with sc1 loads (chain hand-offs).
+template <int MI, typename Wait>
+__device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, const int kb, const int nkb, const int subs,
+                                          const LatCol& col, uint32_t* ktl, Wait wait, const bool sc1_ld,
+                                          lat_f32x4 (&acc)[MI]) {
   const int lane = threadIdx.x & 63;
-  const int c = lane & 15, h = lane >> 4;
-  const int M = d.M, N = d.N, K = d.K;
+  const int h = lane >> 4;
+  const int K = d.K;
   const int k0 = kb * LKC;
   const int ng = min(LGROUPS, (K - k0 + 15) >> 4);
   const bool linear = d.kstride > 0;
@@ -77,17 +94,6 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
       if (g < ng && sub0 + mi < subs)
         av[g][mi] = ap[(((int64_t)(sub0 + mi) * nkb + kb) * LGROUPS + g) * 64 + lane];
     }
-
-  const int n = n0 + c;
-  uint32_t vcol = DMA_OOB;
-  int img = 0, p = 0, oy = 0, ox = 0;
-  if (n < N) {
-    img = fdiv(n, d.fdP);
-    p = n - img * d.P;
-    oy = fdiv(p, d.fdOW);
-    ox = p - oy * d.OW;
-    vcol = (uint32_t)(((int64_t)img * d.x_img + (int64_t)oy * d.ystride + (int64_t)ox * d.xstride) * 4);
-  }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
 
   wait();
@@ -114,12 +120,11 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
       }
 #pragma unroll
       for (int j = 0; j < 4; j++)
-        bv[4 * g + j] = __uint_as_float(sc1_ld ? __builtin_amdgcn_raw_buffer_load_b32(xr, vcol + ko[j], 0, kLoadSc1)
-                                               : __builtin_amdgcn_raw_buffer_load_b32(xr, vcol + ko[j], 0, 0));
+        bv[4 * g + j] = __uint_as_float(sc1_ld ? __builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + ko[j], 0, kLoadSc1)
+                                               : __builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + ko[j], 0, 0));
     }
   }
 
-  lat_f32x4 acc[MI];
 #pragma unroll
   for (int mi = 0; mi < MI; mi++) acc[mi] = (lat_f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -132,43 +137,110 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
           acc[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(lat_f4(av[g][mi], j), bv[4 * g + j], acc[mi], 0, 0, 0);
     }
   }
+}
 
-  // Epilogue operands, issued before any store (vmcnt retires in order).
-  // Accumulator element r of lane (c, h) is row 4h + r, column c.
-  float bias_v[MI][4], res_v[MI][4];
-  const int64_t rbase = (int64_t)img * d.res_img + p;
+// Epilogue operands of this lane's accumulator elements: the row bias and the
+// residual (sc1 loads for chain hand-offs).  Element r of lane (c, h) is row
+// 4h + r, column c.
+template <int MI>
+struct LatEpi {
+  float bias[MI][4], res[MI][4];
+  float cbv;
+};
+template <int MI>
+__device__ __forceinline__ void lat_epi_loads(const DmaDesc& d, const int sub0, const LatCol& col, const bool sc1_ld,
+                                              LatEpi<MI>& e) {
+  const int h = (threadIdx.x & 63) >> 4;
+  const int64_t rbase = (int64_t)col.img * d.res_img + col.p;
 #pragma unroll
   for (int mi = 0; mi < MI; mi++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int m = (sub0 + mi) * 16 + 4 * h + r;
-      const int mc = min(m, M - 1);
-      bias_v[mi][r] = d.bias ? d.bias[mc] : 0.f;
-      res_v[mi][r] = 0.f;
-      if (d.residual && n < N) {
+      const int mc = min(m, d.M - 1);
+      e.bias[mi][r] = d.bias ? d.bias[mc] : 0.f;
+      e.res[mi][r] = 0.f;
+      if (d.residual && col.n < d.N) {
         const float* rp = d.residual + rbase + (int64_t)mc * d.res_c;
-        res_v[mi][r] = sc1_ld ? __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *rp;
+        e.res[mi][r] = sc1_ld ? __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *rp;
       }
     }
-  const float cbv = (d.colbias && n < N) ? d.colbias[p] : 0.f;
+  e.cbv = (d.colbias && col.n < d.N) ? d.colbias[col.p] : 0.f;
+}
+
+// End of K block 0: alpha * chain + bias (gemm.rs:1004-1050).
+__device__ __forceinline__ float lat_first_block(const DmaDesc& d, float a, float b) {
+  float x = d.alpha == 1.f ? a : __fmul_rn(a, d.alpha);
+  if (d.bias) x = __fadd_rn(x, b);
+  return x;
+}
+
+// Column bias, residual, activation and the store of the folded tile.
+template <int MI>
+__device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, const LatCol& col, const LatEpi<MI>& e,
+                                           const lat_f32x4 (&sum)[MI], const bool sc1_st) {
+  const int h = (threadIdx.x & 63) >> 4;
+  const bool act_relu = d.act == RTENHIP_ACT_RELU, act_clip = d.act == RTENHIP_ACT_CLIP;
+  const bool act_gelu = d.act == RTENHIP_ACT_GELU;
+  const float lo = d.act_lo, hi = d.act_hi;
+  const int64_t obase = (int64_t)col.img * d.out_img + (int64_t)col.oy * d.out_row + col.ox + d.out_off;
+  if (col.n >= d.N) return;
+#pragma unroll
+  for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int m = (sub0 + mi) * 16 + 4 * h + r;
+      float x = sum[mi][r];
+      if (d.colbias) x = __fadd_rn(x, e.cbv);
+      if (d.residual) x = __fadd_rn(x, e.res[mi][r]);
+      if (act_gelu) {
+        x = vm_gelu(x);
+      } else {
+        const float rl = fmaxf(x, 0.f);
+        const float cl = x < lo ? lo : (x > hi ? hi : x);
+        x = act_relu ? rl : (act_clip ? cl : x);
+      }
+      if (m < d.M) {
+        float* op = d.out + obase + (int64_t)m * d.out_c;
+        if (sc1_st)
+          __hip_atomic_store(op, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *op = x;
+      }
+    }
+}
+
+// One unit (sub0: first 16-row subtile, n0: first column, kb: KC block, wt:
+// the tile's index into ws / counters) with the global fold: with K > 256
+// this block's chains go to the workspace ([tile][kb][mi][lane] x 16 bytes,
+// 8-byte agent-scope stores), drained before the arrival count, and the last
+// block of the tile to arrive folds all chains in K order.  wait(): see
+// lat_chain.  CHAIN: x and the residual are read with sc1 loads, the output is
+// stored sc1 and drained, and the wave that stored the tile then calls done()
+// (the inter-layer hand-off of conv_chain.hip).
+template <int MI, bool CHAIN, typename Wait, typename Done>
+__device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const int n0, const int kb, const int nkb,
+                                         const int subs, const int wt, uint32_t* ktl, Wait wait, Done done,
+                                         int dbg = 0) {
+  // dbg (timing experiments only, results not valid across XCDs): bit 0 plain
+  // x / residual loads, bit 1 plain output stores.
+  const bool sc1_ld = CHAIN && !(dbg & 1), sc1_st = CHAIN && !(dbg & 2);
+  const int lane = threadIdx.x & 63;
+  const LatCol col = lat_col(d, n0);
+  lat_f32x4 acc[MI];
+  lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, wait, sc1_ld, acc);
+  // Epilogue operands, issued before any store (vmcnt retires in order).
+  LatEpi<MI> e;
+  lat_epi_loads<MI>(d, sub0, col, sc1_ld, e);
   const float alpha = d.alpha;
-  // End of K block 0: alpha * chain + bias (gemm.rs:1004-1050).
-  auto first_block = [&](float a, float b) __attribute__((always_inline)) {
-    float x = alpha == 1.f ? a : __fmul_rn(a, alpha);
-    if (d.bias) x = __fadd_rn(x, b);
-    return x;
-  };
 
   lat_f32x4 sum[MI];
   if (nkb == 1) {
 #pragma unroll
     for (int mi = 0; mi < MI; mi++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) sum[mi][r] = first_block(acc[mi][r], bias_v[mi][r]);
+      for (int r = 0; r < 4; r++) sum[mi][r] = lat_first_block(d, acc[mi][r], e.bias[mi][r]);
   } else {
-    // This block's chains to the workspace ([tile][kb][mi][lane] x 16 bytes,
-    // as 8-byte agent-scope stores), drained before the arrival count; the
-    // last block of the tile to arrive folds all chains in K order.
     unsigned long long* wsq = reinterpret_cast<unsigned long long*>(d.ws);
     auto qi = [&](int kbi, int mi) { return ((((int64_t)wt * nkb + kbi) * MI + mi) * 64 + lane) * 2; };
 #pragma unroll
@@ -212,42 +284,14 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
           v[3] = __uint_as_float((unsigned)(part[i][mi][1] >> 32));
 #pragma unroll
           for (int r = 0; r < 4; r++)
-            sum[mi][r] = kb0 + i == 0 ? first_block(v[r], bias_v[mi][r]) : __fmaf_rn(v[r], alpha, sum[mi][r]);
+            sum[mi][r] = kb0 + i == 0 ? lat_first_block(d, v[r], e.bias[mi][r]) : __fmaf_rn(v[r], alpha, sum[mi][r]);
         }
       }
     }
     if (lane == 0) __hip_atomic_store(d.counters + wt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
-  const bool act_relu = d.act == RTENHIP_ACT_RELU, act_clip = d.act == RTENHIP_ACT_CLIP;
-  const bool act_gelu = d.act == RTENHIP_ACT_GELU;
-  const float lo = d.act_lo, hi = d.act_hi;
-  const int64_t obase = (int64_t)img * d.out_img + (int64_t)oy * d.out_row + ox + d.out_off;
-  if (n < N) {
-#pragma unroll
-    for (int mi = 0; mi < MI; mi++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int m = (sub0 + mi) * 16 + 4 * h + r;
-        float x = sum[mi][r];
-        if (d.colbias) x = __fadd_rn(x, cbv);
-        if (d.residual) x = __fadd_rn(x, res_v[mi][r]);
-        if (act_gelu) {
-          x = vm_gelu(x);
-        } else {
-          const float rl = fmaxf(x, 0.f);
-          const float cl = x < lo ? lo : (x > hi ? hi : x);
-          x = act_relu ? rl : (act_clip ? cl : x);
-        }
-        if (m < M) {
-          float* op = d.out + obase + (int64_t)m * d.out_c;
-          if (sc1_st)
-            __hip_atomic_store(op, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            *op = x;
-        }
-      }
-  }
+  lat_finish<MI>(d, sub0, col, e, sum, sc1_st);
   if (CHAIN) {
     // Every store of the tile drained, then one lane publishes it.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

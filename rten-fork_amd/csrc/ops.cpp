@@ -164,7 +164,12 @@ rtenhip_status rtenhip_gemm_op_f32(rtenhip_ctx* ctx, const rtenhip_tensor* a,
     d.shape[0] = M;
     d.shape[1] = N;
     bcast_strides(cz, os, 2, d.sb);
-    // copy via binary "Mul by 1"? No: a plain strided copy of the broadcast view.
+    // One output row (the FC layer at batch 1): the gemv reads the broadcast
+    // C itself (same beta * C + alpha * acc arithmetic, no copy launch).
+    if (M == 1 && K > 0 && a_cs == 1)
+      return launch_gemv(N, K, a->data, b->data, b_rs, b_cs, y->data, alpha, beta, nullptr, cx->ref_threads,
+                         cx->stream, c->data, d.sb[1]);
+    // A plain strided copy of the broadcast view.
     rtenhip_tensor view{};
     view.data = c->data;
     view.ndim = 2;

@@ -45,7 +45,7 @@ def _case_id(c):
     return "x".join(map(str, c[:6])) + f"s{c[6]}g{c[8]}-{c[9]}"
 
 
-@pytest.mark.parametrize("mode", ["41", "22", "12"])
+@pytest.mark.parametrize("mode", ["41", "22", "12", "91", "92"])
 @pytest.mark.parametrize("case", CASES, ids=_case_id)
 def test_lat_conv_bitexact(rh, monkeypatch, mode, case):
     import torch

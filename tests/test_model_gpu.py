@@ -348,6 +348,7 @@ def test_conv_transpose_graph_and_file_bitexact(rh):
     (3, 17, 10, None),        # short K, no C
     (5, 300, 130, "vec"),     # two KC blocks, the second partial
     (1, 2048, 1000, "vec"),   # batch 1: the reference's gemv order (general path)
+    (1, 300, 130, "row"),     # batch 1, C as [1, O], read by the gemv in place of a copy
 ])
 def test_gemm_fc_bitexact(rh, B, K, O, c_kind):
     """Gemm with a constant transposed weight (the classifier layer): batch >= 2
