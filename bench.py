@@ -122,11 +122,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    backend = os.environ.get("RTENHIP_DIST_BACKEND", "nccl")  # "gloo": one-GPU multi-rank rehearsal
     if world > 1:
         import torch.distributed as dist
 
+        # One rank per GPU; with fewer GPUs than ranks (a gloo rehearsal on a
+        # one-GPU box) ranks share devices round-robin.
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
 
@@ -183,7 +190,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], device=x.device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=x.device if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -266,7 +273,8 @@ def main():
             "config": {"workload": workload,
                        "model": spec.name, "global_batch": world * B,
                        "seq_len": args.seq if args.model == "bert" else None,
-                       "parallelism": f"batch-shard x{world} (replicated weights, RCCL all-gather of logits)"},
+                       "parallelism": f"batch-shard x{world} (replicated weights, "
+                                          f"{'RCCL' if backend == 'nccl' else backend} all-gather of logits)"},
             "roofline": roofline,
         }
         if not args.no_cpu_baseline and world == 1:

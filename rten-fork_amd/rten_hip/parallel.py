@@ -53,11 +53,18 @@ class BatchShardRunner:
     def run(self, full_batch_local_view, total: int):
         """full_batch_local_view: this rank's slice of the inputs (already
         resident on its device).  Returns the gathered [total, ...] output."""
-        import torch
-
         out = self.fn(full_batch_local_view)
         if self.dist is None:
             return out
+        if out.is_cuda and self.dist.get_backend(self.group) == "gloo":
+            # gloo moves host tensors only (the CPU tests and the one-GPU
+            # multi-rank rehearsal); RCCL gathers device tensors directly.
+            return self._gather(out.cpu(), total).to(out.device)
+        return self._gather(out, total)
+
+    def _gather(self, out, total: int):
+        import torch
+
         sizes = shard_sizes(total, self.world)
         if len(set(sizes)) == 1:
             gathered = torch.empty((total,) + tuple(out.shape[1:]), dtype=out.dtype,

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export RTEN_NUM_THREADS=8
 PYT="python -u -m pytest -x -v --timeout 300 --timeout-method thread"
-timeout -k 10 400 $PYT tests/test_optimizer_gpu.py tests/test_threads.py tests/test_conv_pointwise_gpu.py -k "not test_pointwise_valu_bitexact and not test_direct_valu" \
+timeout -k 10 400 $PYT tests/test_parallel_gpu.py tests/test_optimizer_gpu.py tests/test_threads.py tests/test_conv_pointwise_gpu.py -k "not test_pointwise_valu_bitexact and not test_direct_valu" \
   > gpurun_out/r3_quick.log 2>&1 || { echo "quick tests failed"; tail -40 gpurun_out/r3_quick.log; exit 1; }
 tail -3 gpurun_out/r3_quick.log
 timeout -k 10 900 $PYT tests -m gpu --deselect tests/test_full_size_gpu.py > gpurun_out/r3_suite.log 2>&1 \
@@ -24,3 +24,6 @@ timeout -k 10 300 python -u bench.py --model mobilenet_v2 --batch 128 --no-cpu-b
 head -c 600 gpurun_out/r3_bench_mnv2.json
 timeout -k 10 300 python -u bench.py --model bert --batch 32 --no-cpu-baseline --timing-report > gpurun_out/r3_bench_bert.json 2>> gpurun_out/r3_bench.err || exit 1
 head -c 600 gpurun_out/r3_bench_bert.json
+RTENHIP_DIST_BACKEND=gloo timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+  bench.py --gpus 2 --steps 10 --warmup 3 > gpurun_out/r3_bench_rehearsal2.json 2>> gpurun_out/r3_bench.err || exit 1
+cat gpurun_out/r3_bench_rehearsal2.json

@@ -1,0 +1,92 @@
+"""N>1 path with the device graph: two ranks (world_size 2, gloo process
+group, both on cuda:0 of the one-GPU box) each run the device graph executor
+(librten_hip.so, hipGraph replay) on their contiguous batch slice, and
+BatchShardRunner all-gathers the logits.  The gathered result must be
+bit-identical to the oracle running the whole batch in one process -- the
+sharded path changes no arithmetic.  The RCCL leg is the same
+code with device tensors; it needs distinct GPUs and runs in the driver's
+multi-GPU bench.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, total, q):
+    for p in (os.path.join(ROOT, "rten-fork_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import rten_hip
+        from rten_hip.parallel import BatchShardRunner
+        from test_parallel import tiny_spec
+
+        torch.cuda.set_device(0)
+        rten_hip.default_context()
+        spec = tiny_spec()
+        g = spec.to_graph()
+        x = np.random.default_rng(1234).random((total, 4, 6, 6), dtype=np.float32)
+
+        def fn(xb):
+            outs = None
+            for _ in range(3):  # eager, capture + replay, replay
+                outs = g.run({g.input_ids[0]: xb}, g.output_ids, out=outs)
+            torch.cuda.synchronize()
+            return outs[0]
+
+        runner = BatchShardRunner(fn)
+        a, b = runner.local_slice(total)
+        got = runner.run(torch.from_numpy(x[a:b]).cuda(), total)
+        torch.cuda.synchronize()
+        q.put((rank, got.device.type, got.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total", [6, 5])
+def test_world2_device_graph_matches_oracle(total):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+
+    import graph_runner
+    from test_parallel import tiny_spec
+
+    spec = tiny_spec()
+    x = np.random.default_rng(1234).random((total, 4, 6, 6), dtype=np.float32)
+    expect = np.ascontiguousarray(graph_runner.run(spec, {"input": x})[spec.outputs[0]], np.float32)
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, dev, got in results:
+        assert dev == "cuda", f"rank {rank}: gathered logits left the device"
+        assert got.shape == expect.shape
+        assert (got.view(np.uint32) == expect.view(np.uint32)).all(), f"rank {rank}: gathered logits differ"
