@@ -99,18 +99,30 @@ def cpu_baseline(spec, seconds: float, batch: int, feed_fn):
     }
 
 
+# Kernel families the roofline's dominant-kernel time covers, per model (the
+# ops bench.py sums: Conv / Gemm / MatMul (incl. its A pack) / FusedAttention).
+_ROOF_KERNELS = {
+    "resnet50": ("gemm_dma_kernel", "gemm_lat", "gemv"),
+    "bert": ("gemm_dma_kernel", "pack_a_kernel", "attention_kernel"),
+    "mobilenet_v2": ("gemm_dma_kernel", "gemm_lat", "gemv", "conv_pw_valu_kernel", "conv_direct_valu_kernel",
+                     "depthwise", "expand_dw_kernel"),
+}
+
+
 def traffic_bytes(model, batch):
-    """HBM bytes per step of the conv GEMM kernels, from the committed
-    rocprofv3 PMC summary (scripts/gpu_traffic.sh -> tools/pmc_traffic.py):
-    FETCH_SIZE x2 (gfx950) + WRITE_SIZE.  None when no summary exists for
-    this workload."""
-    path = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
-    if model != "resnet50" or batch != 64 or not os.path.exists(path):
+    """HBM bytes per step of the roofline's kernels, from the committed
+    rocprofv3 PMC summary of this workload (scripts/gpu_r3_prof.sh ->
+    tools/pmc_traffic.py --marker): FETCH_SIZE x2 (gfx950) + WRITE_SIZE,
+    eager forwards.  None when no summary exists for this workload."""
+    path = os.path.join(ROOT, "profiles", f"r3_pmc_traffic_{model}_b{batch}.json")
+    if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path))["conv_gemm_bytes_per_forward"]
+        by = json.load(open(path))["by_kernel"]
     except (OSError, ValueError, KeyError):
         return None
+    fams = _ROOF_KERNELS[model]
+    return round(sum(v for k, v in by.items() if any(f in k for f in fams)))
 
 
 def main():

@@ -58,43 +58,54 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   const float* v = d.v + b * d.v_b + hd * d.v_h;
 
   // Stage K (row = key) and V (row = key), zero rows past S; rows of 64
-  // contiguous floats are read as float4 when 16-byte aligned.
+  // contiguous floats are read as float4 when 16-byte aligned.  All of a
+  // thread's loads are issued before its LDS stores (one memory round trip
+  // for the whole staging, not one per row group).
   const bool v4 = ((uintptr_t)v % 16 == 0) && d.v_s % 4 == 0;
   const bool k4 = d.k_d == 1 && ((uintptr_t)kt % 16 == 0) && d.k_s % 4 == 0;
-  for (int t = tid; t < AT_S * (AT_D / 4); t += AT_THREADS) {
+  constexpr int ST = AT_S * (AT_D / 4) / AT_THREADS;  // float4 positions per thread (8)
+  float4 kk[ST], vv[ST];
+#pragma unroll
+  for (int u = 0; u < ST; u++) {
+    const int t = tid + u * AT_THREADS;
     const int j = t >> 4, c = (t & 15) * 4;
-    float4 kk = make_float4(0.f, 0.f, 0.f, 0.f), w = kk;
+    kk[u] = vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (FULL || j < S) {
       const float* vp = v + (int64_t)j * d.v_s + c;
-      w = v4 ? *(const float4*)vp : make_float4(vp[0], vp[1], vp[2], vp[3]);
+      vv[u] = v4 ? *(const float4*)vp : make_float4(vp[0], vp[1], vp[2], vp[3]);
       if (k4) {
-        kk = *(const float4*)(kt + (int64_t)j * d.k_s + c);
+        kk[u] = *(const float4*)(kt + (int64_t)j * d.k_s + c);
       } else {
         const float* kp = kt + (int64_t)j * d.k_s + (int64_t)c * d.k_d;
-        kk = make_float4(kp[0], kp[d.k_d], kp[2 * d.k_d], kp[3 * d.k_d]);
+        kk[u] = make_float4(kp[0], kp[d.k_d], kp[2 * d.k_d], kp[3 * d.k_d]);
       }
     }
-    float* kd = Ks + j * KS + c;
-    kd[0] = kk.x;
-    kd[1] = kk.y;
-    kd[2] = kk.z;
-    kd[3] = kk.w;
-    *(float4*)(Vs + j * VS + c) = w;
   }
-  __syncthreads();
-
+#pragma unroll
+  for (int u = 0; u < ST; u++) {
+    const int t = tid + u * AT_THREADS;
+    const int j = t >> 4, c = (t & 15) * 4;
+    float* kd = Ks + j * KS + c;
+    kd[0] = kk[u].x;
+    kd[1] = kk[u].y;
+    kd[2] = kk[u].z;
+    kd[3] = kk[u].w;
+    *(float4*)(Vs + j * VS + c) = vv[u];
+  }
   const int i0 = wave * 32;
-  if (i0 >= S) return;  // no barrier follows
   const int i = i0 + l32;  // this lane's query row
   const bool row_ok = FULL || i < S;
-
-  // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand).
+  // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand),
+  // loaded while the K / V stores land.
   float qf[AT_D / 2];
   {
     const float* qr = q + (int64_t)(row_ok ? i : 0) * d.q_s + h;
 #pragma unroll
     for (int s = 0; s < AT_D / 2; s++) qf[s] = row_ok ? qr[2 * s] : 0.f;
   }
+  __syncthreads();
+  if (i0 >= S) return;  // no barrier follows
+
 
   // acc[t][e]: score of (row i, key 32t + (e & 3) + 8(e >> 2) + 4h).
   f32x16 acc[4];

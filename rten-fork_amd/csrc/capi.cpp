@@ -178,6 +178,13 @@ static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaT
   d.act_lo = a.lo;
   d.act_hi = a.hi;
   if (lat && a.kh == 1 && a.kw == 1) d.kstride = (int)(a.Hp * a.Wp);
+  if (lat && a.kh == 3 && a.kw == 3) {
+    // Same offsets as the table (Ctx::dtab), formed in the kernel.
+    d.k3x3 = 1;
+    d.kt_plane = (int)(a.Hp * a.Wp);
+    d.kt_row = (int)(a.dh * a.Wp);
+    d.kt_col = (int)a.dw;
+  }
 }
 
 rtenhip_status lat_conv_desc(Ctx* c, const ConvDmaArgs& a, DmaDesc& d) {
@@ -595,6 +602,19 @@ bool dense_dma_eligible(int64_t M, int64_t N, int64_t K, int64_t a_cs, int64_t b
          K * b_rs < (int64_t(1) << 29) && M < (int64_t(1) << 30);
 }
 
+static bool dense_vec4(const DenseDmaArgs& a) {
+  return a.out_rs % 4 == 0 && (uintptr_t)a.out % 16 == 0 &&
+         (!a.residual || (a.res_rs % 4 == 0 && (uintptr_t)a.residual % 16 == 0)) &&
+         (!a.colbias || (uintptr_t)a.colbias % 16 == 0);
+}
+
+bool dense_dma_pk_out_ok(const DenseDmaArgs& a, int cfg) {
+  const DmaTile& t = a.pk_tile;
+  auto pow2 = [](int v) { return v > 0 && (v & (v - 1)) == 0; };
+  return cfg >= 0 && cfg < dma_num_cfgs() && dense_vec4(a) && dma_cfg_vec_epilogue(cfg) && a.N % 4 == 0 &&
+         a.pk_K == a.N && pow2(t.bm) && pow2(t.bk) && t.bk >= 8 && t.bm >= 32;
+}
+
 rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
   hipStream_t s = c->stream;
   const int cfg = a.cfg >= 0 ? a.cfg : dma_default_cfg((int)a.M, (int)a.N, (int)a.K);
@@ -643,11 +663,14 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
   d.act_lo = a.lo;
   d.act_hi = a.hi;
   // 16-byte epilogue: rows contiguous in memory segments of 4.
-  d.vec4 = (a.out_rs % 4 == 0 && (uintptr_t)a.out % 16 == 0 &&
-            (!a.residual || (a.res_rs % 4 == 0 && (uintptr_t)a.residual % 16 == 0)) &&
-            (!a.colbias || (uintptr_t)a.colbias % 16 == 0))
-               ? 1
-               : 0;
+  d.vec4 = dense_vec4(a) ? 1 : 0;
+  if (a.pk_out) {
+    if (!dense_dma_pk_out_ok(a, cfg)) return fail(RTENHIP_INVALID_VALUE, "packed-A output not possible here");
+    d.pk_out = a.pk_out;
+    d.pk_lbm = __builtin_ctz(a.pk_tile.bm);
+    d.pk_lbk = __builtin_ctz(a.pk_tile.bk);
+    d.pk_tiles_k = (int)((a.pk_K + a.pk_tile.bk - 1) / a.pk_tile.bk);
+  }
   if (dma_cfg_bvec(cfg) && a.K % tile.bk == 0 && ((uintptr_t)a.b % 16) == 0) {
     d.bvec = 1;
     d.kstride = (int)a.b_rs;

@@ -8,6 +8,7 @@
 #include <tuple>
 
 #include "common.h"
+#include "gemm_dma.h"
 
 namespace rtenhip {
 
@@ -176,7 +177,13 @@ struct DenseDmaArgs {
   int* counters;
   int64_t cnt_cap;
   int persist_k;   // persistent launch (see ConvDmaArgs::persist_k)
+  float* pk_out;   // store C as the next MatMul's packed A (DmaDesc::pk_out) ...
+  DmaTile pk_tile; // ... for this tile shape,
+  int64_t pk_K;    // ... whose K is this GEMM's N
 };
+// Whether gemm_dense_dma with these operands and cfg can store its output as
+// a packed A (DenseDmaArgs::pk_out): the vectorised epilogue runs.
+bool dense_dma_pk_out_ok(const DenseDmaArgs& a, int cfg);
 bool dense_dma_eligible(int64_t M, int64_t N, int64_t K, int64_t a_cs, int64_t b_rs, int64_t b_cs);
 rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a);
 

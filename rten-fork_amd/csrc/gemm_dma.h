@@ -64,6 +64,14 @@ struct DmaDesc {
   int kstride;              // elements between consecutive k rows of B (bvec)
   int vec4;                 // outputs/residual row-contiguous with P % 4 == 0, unpadded:
                             // 16-byte epilogue accesses (no cin)
+  // Dense MatMul whose output is the next MatMul's A: the vectorised
+  // epilogue stores the values in that MatMul's packed-A layout
+  // ([tiles_m][tiles_k][BK/4][BM][4] k-quads, see pack_a_kernel) at pk_out
+  // instead of row-major at out (column n = that MatMul's k, row m its row).
+  float* pk_out;
+  int pk_lbm, pk_lbk, pk_tiles_k;  // log2 BM, log2 BK and tiles_k of the consumer's packing
+  int k3x3;                 // latency GEMM: 3x3 window, koff(k) computed from k = 9c + 3ky + kx
+  int kt_plane, kt_row, kt_col;  // ... as c * kt_plane + ky * kt_row + kx * kt_col (elements)
   int dbg;                  // tuning experiments only: 1 = no K-loop DMA, 2 = no MFMA
   unsigned long long* stamps;  // placement experiment builds only (RTENHIP_DMA_EXPERIMENT 5):
                                // per block {hw ids, start, end, block}; null otherwise
@@ -79,6 +87,8 @@ DmaSplit dma_split_plan(int M, int N, int K, int cfg);
 // Kernel configurations (all bit-identical; see gemm_dma.hip).
 int dma_num_cfgs();
 bool dma_cfg_bvec(int cfg);
+// Whether cfg's kernel has the vectorised (LDS-transposed, 16-byte) epilogue.
+bool dma_cfg_vec_epilogue(int cfg);
 int dma_default_cfg(int M, int N, int K);
 DmaTile dma_cfg_tile(int cfg);
 int64_t packed_a_floats(int M, int K, const DmaTile& t);

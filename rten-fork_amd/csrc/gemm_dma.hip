@@ -34,6 +34,18 @@ bool dma_cfg_bvec(int cfg) {
   }
 }
 
+bool dma_cfg_vec_epilogue(int cfg) {
+  switch (cfg) {
+#define RTENHIP_DMA_VE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) \
+  case id:                                                  \
+    return (NT / 64) * 1024 <= ST * (BM + BN) * BK;
+    RTENHIP_DMA_CONFIGS(RTENHIP_DMA_VE)
+#undef RTENHIP_DMA_VE
+    default:
+      return false;
+  }
+}
+
 DmaTile dma_cfg_tile(int cfg) {
   const DmaCfgInfo& c = kDmaCfgs[cfg];
   return DmaTile{c.bm, c.bk, 1};  // k-quad layout, independent of the wave tile
@@ -76,6 +88,8 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
   if (cfg < 0 || cfg >= kNumDmaCfgs) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
   if (!(dma_cfg_tile(cfg) == d.tile))
     return fail(RTENHIP_INVALID_VALUE, "A packed for another tile shape");
+  if (d.pk_out && (!d.vec4 || !dma_cfg_vec_epilogue(cfg) || d.P != d.N || d.pk_lbk < 3))
+    return fail(RTENHIP_INVALID_VALUE, "packed-A output needs the vectorised epilogue of a dense GEMM");
   DmaDesc dd = d;
   dd.dbg = g_dma_dbg;
   dd.stamps = g_dma_stamps;

@@ -83,6 +83,8 @@ Plan::~Plan() {
     if (kv.second.counters) (void)hipFree(kv.second.counters);
   }
   if (mm_pack) (void)hipFree(mm_pack);
+  for (auto& kv : mm_prebuf)
+    if (kv.second.first) (void)hipFree(kv.second.first);
   for (auto& kv : conv_unfused)
     if (kv.second.first) (void)hipFree(kv.second.first);
 
@@ -913,6 +915,21 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     me.K = K;
     me.b_rs = b_rs;
     p.matmuls[op] = me;
+  }
+  // MatMul -> MatMul pairs (Plan::mm_next): the consumer reads the producer's
+  // output as A, and nothing else reads it.
+  if (!getenv("RTENHIP_NO_PK_OUT")) {
+    std::map<int, int> producer;  // value -> op
+    for (int op : p.ops)
+      for (int o : nodes[op].outputs) producer[o] = op;
+    for (auto& kv : p.matmuls) {
+      const int v = nodes[kv.first].inputs[0];
+      if (outset.count(v) || uses[v] != 1 || !producer.count(v)) continue;
+      const int pr = producer[v];
+      auto pit = p.matmuls.find(pr);
+      if (pit == p.matmuls.end() || pit->second.M != kv.second.M || pit->second.N != kv.second.K) continue;
+      p.mm_next[pr] = kv.first;
+    }
   }
   // Values produced by a DMA conv and read only (as input 0) by padded DMA
   // convs that agree on the padding get a persistent zero-bordered buffer.
@@ -1786,9 +1803,52 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     me.cfg = chosen;
     me.persist = persist_mode >= 0 ? persist_mode : chosen_persist;
     p.mm_pack_value = -1;  // tuning overwrote the buffer
+    // The A buffer a producer (Plan::mm_next) stores into from the next run
+    // on: allocated here, on the eager first run (later runs may be captured).
+    for (auto& kv : p.mm_next) {
+      if (kv.second != op_id) continue;
+      const int64_t need = packed_a_floats((int)me.M, (int)me.K, dma_cfg_tile(chosen));
+      auto& buf = p.mm_prebuf[op_id];
+      if (buf.second < need) {
+        RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
+        if (buf.first) RTENHIP_HIP_CHECK(hipFree(buf.first));
+        buf.first = nullptr;
+        RTENHIP_HIP_CHECK(hipMalloc(&buf.first, (size_t)need * 4));
+        RTENHIP_HIP_CHECK(hipMemset(buf.first, 0, (size_t)need * 4));  // tile padding stays zero
+        buf.second = need;
+      }
+    }
   }
   bind(me, me.cfg);
   const DmaTile tile = dma_cfg_tile(me.cfg);
+  // A stored packed by its producer earlier in this run (Plan::mm_next).
+  auto pre = p.mm_prepacked.find(op_id);
+  if (pre != p.mm_prepacked.end()) {
+    const bool same = pre->second == tile;
+    p.mm_prepacked.erase(pre);
+    if (!same) return fail(RTENHIP_INVALID_VALUE, "MatMul: A was stored packed for another tile shape");
+    da.pk = p.mm_prebuf.at(op_id).first;
+    da.pack = false;
+    return gemm_dense_dma(ctx, da);
+  }
+  // Producer of the next MatMul's A: once that MatMul's tile is known, store
+  // this output in its packed layout instead of row-major.
+  auto nx = p.mm_next.find(op_id);
+  if (nx != p.mm_next.end()) {
+    const MatMulExec& ce = p.matmuls.at(nx->second);
+    if (ce.cfg >= 0) {
+      DenseDmaArgs pk = da;
+      pk.pk_tile = dma_cfg_tile(ce.cfg);
+      pk.pk_K = me.N;
+      auto buf = p.mm_prebuf.find(nx->second);
+      if (buf != p.mm_prebuf.end() && buf->second.second >= packed_a_floats((int)me.M, (int)me.N, pk.pk_tile) &&
+          dense_dma_pk_out_ok(pk, me.cfg)) {
+        pk.pk_out = buf->second.first;
+        da = pk;
+        p.mm_prepacked[nx->second] = pk.pk_tile;
+      }
+    }
+  }
   da.pack = !(p.mm_pack_value == n.inputs[0] && p.mm_pack_tile == tile);
   p.mm_pack_value = n.inputs[0];
   p.mm_pack_tile = tile;
@@ -2376,6 +2436,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     return RTENHIP_OK;
   };
   plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
+  plan->mm_prepacked.clear();
   if (replay) {
     if (!same_binding) {
       if (plan->exec) {

@@ -201,6 +201,14 @@ struct Plan {
   // projections -- pack it once) and the tile shape; -1 = nothing.
   int mm_pack_value = -1;
   DmaTile mm_pack_tile{0, 0, 0};
+  // Dense MatMul -> MatMul pairs where the producer's output is read only as
+  // the consumer's A (BERT's FFN1 -> FFN2): producer op -> consumer op.  Once
+  // the consumer's tile is chosen (first run) the producer stores straight
+  // into the consumer's packed-A buffer (consumer op -> buffer, floats; zeroed
+  // once, so the tile padding stays zero) and the consumer skips its pack.
+  std::map<int, int> mm_next;
+  std::map<int, std::pair<float*, int64_t>> mm_prebuf;
+  std::map<int, DmaTile> mm_prepacked;  // consumer op -> tile its A was stored in during this run
   // Ops launched on the side stream (independent branches such as the
   // ResNet downsample conv), and for each op the side ops it must wait for.
   std::set<int> side;

@@ -66,12 +66,34 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
   const int k0 = kb * LKC;
   const int ng = min(LGROUPS, (K - k0 + 15) >> 4);
   const bool linear = d.kstride > 0;
+  const bool k3 = !linear && d.k3x3;
+
+  // 3x3 windows: koff(k) for k = 9c + 3ky + kx is c * plane + ky * row +
+  // kx * col -- the table's entries (Ctx::dtab) formed here, so the B gathers
+  // do not wait for a table load.  This lane visits k = k0 + h + 4s and
+  // koff(k + 36) = koff(k) + 4 * plane: nine offsets, the rest by adds.
+  uint32_t k3off[9];
+  const uint32_t k3step = 16u * (uint32_t)d.kt_plane;  // bytes per +36 in k
+  if (k3) {
+    const uint32_t kh0 = (uint32_t)(k0 + h);
+    const int c0 = (int)(__umulhi(kh0, 0x38E38E39u) >> 1);  // kh0 / 9
+    const int r0 = (int)kh0 - 9 * c0;
+#pragma unroll
+    for (int s = 0; s < 9; s++) {
+      const int kk = r0 + 4 * s;          // < 41
+      const int q = (kk * 57) >> 9;       // kk / 9
+      const int rr = kk - 9 * q;
+      const int ky = (rr * 11) >> 5;      // rr / 3
+      const int kx = rr - 3 * ky;
+      k3off[s] = (uint32_t)((c0 + q) * d.kt_plane + ky * d.kt_row + kx * d.kt_col) * 4u;
+    }
+  }
 
   // Table mode: lane L loads entries 4L..4L+3 of the block and stores entry
   // k at [k % 4][k / 4], so the lane with k parity h reads the offsets of 4
   // consecutive MFMA steps as one 16-byte LDS read.  (The slot is private to
   // the wave and LDS operations of a wave complete in order.)
-  if (!linear) {
+  if (!linear && !k3) {
     const int kpad = (K + DMA_KTAB_PAD - 1) / DMA_KTAB_PAD * DMA_KTAB_PAD;
     int4 t = make_int4((int)DMA_OOB, (int)DMA_OOB, (int)DMA_OOB, (int)DMA_OOB);
     if (k0 + lane * 4 < kpad) t = *(const int4*)(d.ktab4 + k0 + lane * 4);
@@ -110,6 +132,13 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
         for (int j = 0; j < 4; j++) {
           const int k = k0 + 16 * g + 4 * j + h;
           ko[j] = k < K ? (uint32_t)k * (uint32_t)d.kstride * 4u : DMA_OOB;
+        }
+      } else if (k3) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int st = 4 * g + j;
+          const int k = k0 + 16 * g + 4 * j + h;
+          ko[j] = k < K ? k3off[st % 9] + (uint32_t)(st / 9) * k3step : DMA_OOB;
         }
       } else {
         const uint4 t = *(const uint4*)&ktl[h * 64 + 4 * g];
@@ -227,11 +256,14 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
   const bool sc1_ld = CHAIN && !(dbg & 1), sc1_st = CHAIN && !(dbg & 2);
   const int lane = threadIdx.x & 63;
   const LatCol col = lat_col(d, n0);
+  // Epilogue operands, issued before any store (vmcnt retires in order); a
+  // standalone launch issues them with the operand loads (one memory round
+  // trip fewer on the unit's path), a chain after its dependency wait.
+  LatEpi<MI> e;
+  if (!CHAIN) lat_epi_loads<MI>(d, sub0, col, false, e);
   lat_f32x4 acc[MI];
   lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, wait, sc1_ld, acc);
-  // Epilogue operands, issued before any store (vmcnt retires in order).
-  LatEpi<MI> e;
-  lat_epi_loads<MI>(d, sub0, col, sc1_ld, e);
+  if (CHAIN) lat_epi_loads<MI>(d, sub0, col, sc1_ld, e);
   const float alpha = d.alpha;
 
   lat_f32x4 sum[MI];

@@ -55,18 +55,36 @@ __device__ __forceinline__ float ed_act(float v, int act, float lo, float hi) {
 
 constexpr int kEdMargin = 4;  // floats before each LDS plane (never read: colok)
 
-template <int CIN, int S>
+constexpr int kEdMaxQ = 4;  // depthwise outputs per thread and channel (TR * OW <= 1024)
+
+// CP channels per pass (one barrier per pass).  The block's expand and
+// depthwise weights and biases are staged in LDS once (wave-uniform reads are
+// LDS broadcasts); each thread's depthwise outputs -- their LDS tap offsets and
+// the 9-bit mask of taps the reference visits -- are fixed before the channel
+// loop, so a channel's depthwise step is 9 LDS reads and selects per output.
+template <int CIN, int S, int CP>
 __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   extern __shared__ float4 ed_lds4[];
   float* lds = reinterpret_cast<float*>(ed_lds4);
-  const int plane = d.rows_in * d.W + 2 * kEdMargin;  // one buffer of the double buffer
+  const int plane = d.rows_in * d.W + 2 * kEdMargin;  // one expand plane (2 * CP of them)
   const int n = blockIdx.y;
   const int oy0 = blockIdx.x * d.TR;
   const int iy_lo = oy0 * S - d.pt;  // input row of LDS row 0
   const int c_begin = blockIdx.z * d.cpb;
   const int c_end = min(d.hidden, c_begin + d.cpb);
-  const int W4 = d.W >> 2;
+  const int cnt = c_end - c_begin;
+  float* w_e = lds + 2 * CP * plane;  // [cnt][CIN]
+  float* w_d = w_e + d.cpb * CIN;     // [cnt][9]
+  float* b_e = w_d + d.cpb * 9;       // [cnt]
+  float* b_d = b_e + d.cpb;           // [cnt]
   const int t = threadIdx.x;
+  for (int i = t; i < cnt * CIN; i += 256) w_e[i] = d.we[(int64_t)c_begin * CIN + i];
+  for (int i = t; i < cnt * 9; i += 256) w_d[i] = d.wd[(int64_t)c_begin * 9 + i];
+  for (int i = t; i < cnt; i += 256) {
+    b_e[i] = d.be ? d.be[c_begin + i] : 0.f;
+    b_d[i] = d.bd ? d.bd[c_begin + i] : 0.f;
+  }
+  const int W4 = d.W >> 2;
   const int er = t / W4, ec = (t - er * W4) * 4;  // this thread's expand pixels: LDS row er, cols ec..ec+3
   const int iy = iy_lo + er;
   const bool e_on = er < d.rows_in && iy >= 0 && iy < d.H;
@@ -77,56 +95,99 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
 #pragma unroll
     for (int k = 0; k < CIN; k++) xr[k] = *(const float4*)(xp + k * HW);
   }
-  const int oh_blk = min(d.TR, d.OH - oy0);
-  const int n_out = oh_blk * d.OW;
-  for (int c = c_begin; c < c_end; c++) {
-    float* eb = lds + (c & 1) * plane + kEdMargin;
-    if (e_on) {
-      const float* __restrict__ wc = d.we + (int64_t)c * CIN;
-      f32x2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+  // Depthwise outputs o = t + 256 q of the band: LDS offset of tap (0, 0)
+  // (input row oy*S - pt is LDS row ol*S) and the taps inside the image rows
+  // and the min_max_out_x_coords columns.
+  const int n_out = min(d.TR, d.OH - oy0) * d.OW;
+  int toff[kEdMaxQ];
+  uint32_t tmask[kEdMaxQ];
 #pragma unroll
-      for (int k = 0; k < CIN; k++) {
-        const f32x2 wv = {wc[k], wc[k]};
-        a0 = __builtin_elementwise_fma(wv, (f32x2){xr[k].x, xr[k].y}, a0);
-        a1 = __builtin_elementwise_fma(wv, (f32x2){xr[k].z, xr[k].w}, a1);
-      }
-      float4 v = make_float4(a0.x, a0.y, a1.x, a1.y);
-      if (d.be) {
-        const float b = d.be[c];
-        v.x = __fadd_rn(v.x, b);
-        v.y = __fadd_rn(v.y, b);
-        v.z = __fadd_rn(v.z, b);
-        v.w = __fadd_rn(v.w, b);
-      }
-      v.x = ed_act(v.x, d.act_e, d.lo_e, d.hi_e);
-      v.y = ed_act(v.y, d.act_e, d.lo_e, d.hi_e);
-      v.z = ed_act(v.z, d.act_e, d.lo_e, d.hi_e);
-      v.w = ed_act(v.w, d.act_e, d.lo_e, d.hi_e);
-      *(float4*)(eb + er * d.W + ec) = v;
-    }
-    // One barrier per channel: the plane written next iteration is the other
-    // buffer, and the one after that is only written once every thread has
-    // passed the next barrier, i.e. finished reading this one.
-    __syncthreads();
-    const float* __restrict__ wk = d.wd + (int64_t)c * 9;
-    const float b0 = d.bd ? d.bd[c] : 0.f;
-    float* yc = d.y + ((int64_t)n * d.hidden + c) * d.OH * d.OW;
-    for (int o = t; o < n_out; o += 256) {
-      const int ol = o / d.OW, ox = o - ol * d.OW;
-      const int oy = oy0 + ol;
-      float acc = b0;
+  for (int q = 0; q < kEdMaxQ; q++) {
+    const int o = t + 256 * q;
+    const int ol = o / d.OW, ox = o - ol * d.OW;
+    const int oy = oy0 + ol;
+    toff[q] = ol * S * d.W + ox * S - d.pl;
+    uint32_t m = 0;
+    if (o < n_out) {
+      m = 1u << 9;  // an output of this band
 #pragma unroll
       for (int ky = 0; ky < 3; ky++) {
-        const int r = oy * S + ky - d.pt;  // input row
+        const int r = oy * S + ky - d.pt;
         if (r < 0 || r >= d.H) continue;
-        const float* row = eb + (r - iy_lo) * d.W + ox * S - d.pl;
 #pragma unroll
-        for (int kx = 0; kx < 3; kx++) {
-          if (ox < d.omin[kx] || ox >= d.omax[kx]) continue;
-          acc = __fadd_rn(acc, __fmul_rn(row[kx], wk[ky * 3 + kx]));
-        }
+        for (int kx = 0; kx < 3; kx++)
+          if (ox >= d.omin[kx] && ox < d.omax[kx]) m |= 1u << (ky * 3 + kx);
       }
-      yc[(int64_t)oy * d.OW + ox] = ed_act(acc, d.act_d, d.lo_d, d.hi_d);
+    }
+    tmask[q] = m;
+  }
+  const bool e_act_relu = d.act_e == RTENHIP_ACT_RELU, e_act_clip = d.act_e == RTENHIP_ACT_CLIP;
+  const bool d_act_relu = d.act_d == RTENHIP_ACT_RELU, d_act_clip = d.act_d == RTENHIP_ACT_CLIP;
+  auto act = [](float v, bool relu, bool clip, float lo, float hi) __attribute__((always_inline)) {
+    const float r = rust_max(v, 0.f);
+    const float c = rust_clamp(v, lo, hi);
+    return relu ? r : (clip ? c : v);
+  };
+  __syncthreads();  // weights staged
+  for (int c0 = c_begin, pass = 0; c0 < c_end; c0 += CP, pass++) {
+    float* ebuf = lds + (pass & 1) * CP * plane + kEdMargin;
+    if (e_on) {
+#pragma unroll
+      for (int j = 0; j < CP; j++) {
+        const int cl = min(c0 + j, c_end - 1) - c_begin;  // a pass past c_end recomputes the last channel (unused)
+        const float* __restrict__ wc = w_e + cl * CIN;
+        f32x2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < CIN; k++) {
+          const f32x2 wv = {wc[k], wc[k]};
+          a0 = __builtin_elementwise_fma(wv, (f32x2){xr[k].x, xr[k].y}, a0);
+          a1 = __builtin_elementwise_fma(wv, (f32x2){xr[k].z, xr[k].w}, a1);
+        }
+        float4 v = make_float4(a0.x, a0.y, a1.x, a1.y);
+        if (d.be) {
+          const float b = b_e[cl];
+          v.x = __fadd_rn(v.x, b);
+          v.y = __fadd_rn(v.y, b);
+          v.z = __fadd_rn(v.z, b);
+          v.w = __fadd_rn(v.w, b);
+        }
+        v.x = act(v.x, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+        v.y = act(v.y, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+        v.z = act(v.z, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+        v.w = act(v.w, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+        *(float4*)(ebuf + j * plane + er * d.W + ec) = v;
+      }
+    }
+    // One barrier per pass: the planes written next pass are the other
+    // buffer, and the ones after that are only written once every thread has
+    // passed the next barrier, i.e. finished reading these.
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CP; j++) {
+      const int c = c0 + j;
+      if (c >= c_end) break;
+      const int cl = c - c_begin;
+      const float* eb = ebuf + j * plane;
+      float wk[9];
+#pragma unroll
+      for (int i = 0; i < 9; i++) wk[i] = w_d[cl * 9 + i];
+      const float b0 = b_d[cl];
+      float* yc = d.y + ((int64_t)n * d.hidden + c) * d.OH * d.OW + (int64_t)oy0 * d.OW;
+#pragma unroll
+      for (int q = 0; q < kEdMaxQ; q++) {
+        const uint32_t m = tmask[q];
+        if (!(m >> 9)) continue;  // not an output of this band
+        float acc = b0;
+#pragma unroll
+        for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+          for (int kx = 0; kx < 3; kx++) {
+            const bool on = (m >> (ky * 3 + kx)) & 1u;
+            const float v = eb[on ? toff[q] + ky * d.W + kx : 0];
+            acc = on ? __fadd_rn(acc, __fmul_rn(v, wk[ky * 3 + kx])) : acc;
+          }
+        yc[t + 256 * q] = act(acc, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+      }
     }
   }
 }
@@ -316,12 +377,14 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
   int chunks = 1;
   while ((int64_t)bands * N * chunks < 1024 && hidden / (chunks * 2) >= 16) chunks *= 2;
   d.cpb = (hidden + chunks - 1) / chunks;
-  const size_t lds = 2 * ((size_t)d.rows_in * W + 2 * kEdMargin) * sizeof(float);
-  if (lds > 64 * 1024 || N > 65535 || chunks > 65535) return fail(RTENHIP_UNSUPPORTED_VALUE, "expand+depthwise tile too large");
+  constexpr int CP = 2;
+  const size_t lds = (2 * CP * ((size_t)d.rows_in * W + 2 * kEdMargin) + (size_t)d.cpb * (cin + 9 + 2)) * sizeof(float);
+  if (lds > 64 * 1024 || N > 65535 || chunks > 65535 || (int64_t)d.TR * OW > 256 * kEdMaxQ)
+    return fail(RTENHIP_UNSUPPORTED_VALUE, "expand+depthwise tile too large");
   dim3 grid((unsigned)bands, (unsigned)N, (unsigned)chunks);
 #define ED_CASE(C, SS) \
   if (cin == C && S == SS) { \
-    hipLaunchKernelGGL((expand_dw_kernel<C, SS>), grid, dim3(256), lds, s, d); \
+    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP>), grid, dim3(256), lds, s, d); \
     RTENHIP_LAUNCH_CHECK(); \
     return RTENHIP_OK; \
   }

@@ -14,7 +14,7 @@ from collections import defaultdict
 
 def load(pattern):
     rows = []
-    for f in glob.glob(pattern):
+    for f in glob.glob(pattern, recursive=True):
         rows += list(csv.DictReader(open(f)))
     per = defaultdict(float)
     names = {}
@@ -26,9 +26,12 @@ def load(pattern):
 
 
 def main():
-    root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/traffic"
-    runs = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    ops_per_forward = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    root = args[0] if len(args) > 0 else "gpurun_out/traffic"
+    runs = int(args[1]) if len(args) > 1 else 2
+    ops_per_forward = int(args[2]) if len(args) > 2 else 0
+    if "--marker" in sys.argv:
+        return marker_mode(root, runs)
     res = {}
     for ctr, mult in (("fetch", 2.0), ("write", 1.0)):
         per, names = load(f"{root}/{ctr}*counter_collection.csv")
@@ -51,6 +54,34 @@ def main():
         "all_kernels_bytes_per_forward": res["fetch"]["all_bytes_per_forward"] + res["write"]["all_bytes_per_forward"],
         "detail": res,
         "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB->bytes; ResNet-50 b64 eager forward",
+    }
+    print(json.dumps(out, indent=1))
+
+
+def marker_mode(root, runs):
+    """Every dispatch after the marker fill of tools/model_once.py, per
+    forward, by kernel family."""
+    res = {}
+    fam_all = defaultdict(float)
+    for ctr, mult in (("fetch", 2.0), ("write", 1.0)):
+        per, names = load(f"{root}/**/{ctr}*counter_collection.csv")
+        ids = sorted(per)
+        # the torch fill (at::native kernel) of model_once.py; the forwards
+        # themselves launch librten_hip kernels and HIP's own memset kernels
+        last_marker = max((d for d in ids if "at::" in names[d]), default=-1)
+        tail = [d for d in ids if d > last_marker]
+        fam = defaultdict(float)
+        for d in tail:
+            k = names[d].split("(")[0].split("<")[0].replace("void ", "").strip()
+            fam[k] += per[d] * 1024 * mult / runs
+            fam_all[k] += per[d] * 1024 * mult / runs
+        res[ctr] = {"bytes_per_forward": sum(fam.values()), "dispatches_per_forward": len(tail) / runs,
+                    "by_kernel": dict(sorted(fam.items(), key=lambda kv: -kv[1]))}
+    out = {
+        "all_kernels_bytes_per_forward": res["fetch"]["bytes_per_forward"] + res["write"]["bytes_per_forward"],
+        "by_kernel": dict(sorted(fam_all.items(), key=lambda kv: -kv[1])),
+        "detail": res,
+        "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KB->bytes; eager forwards after the tuning run",
     }
     print(json.dumps(out, indent=1))
 

@@ -38,11 +38,15 @@ CASES = [
     (1, 1030, 7, 7, 24, 1, 1, [0, 0, 0, 0], 1, "none", True),         # K = 1030: ragged last block
     (1, 512, 7, 7, 512, 3, 1, [1, 1, 1, 1], 1, "relu", True),         # K = 4608: 18 blocks, N = 49
     (1, 128, 7, 7, 2048, 1, 1, [0, 0, 0, 0], 1, "add_relu", True),    # M = 2048
+    # 3x3 windows (offsets formed in the kernel, no K table):
+    (1, 37, 12, 10, 24, 3, 2, [1, 1, 1, 1], 1, "relu", True),         # strided, K = 333 ragged
+    (1, 30, 13, 11, 20, 3, 1, [2, 2, 2, 2], 1, "none", True, 2),      # dilation 2, K = 270
+    (1, 3, 9, 9, 16, 3, 1, [0, 1, 2, 0], 1, "none", False),           # K = 27, asymmetric pads
 ]
 
 
 def _case_id(c):
-    return "x".join(map(str, c[:6])) + f"s{c[6]}g{c[8]}-{c[9]}"
+    return "x".join(map(str, c[:6])) + f"s{c[6]}g{c[8]}-{c[9]}" + (f"d{c[11]}" if len(c) > 11 else "")
 
 
 @pytest.mark.parametrize("mode", ["41", "22", "12", "91", "92"])
@@ -52,7 +56,8 @@ def test_lat_conv_bitexact(rh, monkeypatch, mode, case):
     import graph_runner
     from rten_hip.graph import ModelSpec
 
-    N, C, H, W, O, kh, st, pads, groups, tail, bias = case
+    N, C, H, W, O, kh, st, pads, groups, tail, bias = case[:11]
+    dil = case[11] if len(case) > 11 else 1
     monkeypatch.setenv("RTENHIP_LAT", mode)
     rng = np.random.default_rng(C * 31 + O + kh + groups)
     m = ModelSpec("lat")
@@ -63,10 +68,10 @@ def test_lat_conv_bitexact(rh, monkeypatch, mode, case):
     args = [x, w]
     if bias:
         args.append(m.const("b", rng.uniform(-0.2, 0.2, (O,)).astype(np.float32)))
-    y = m.op("Conv", args, {"pads": pads, "strides": [st, st], "groups": groups})
+    y = m.op("Conv", args, {"pads": pads, "strides": [st, st], "groups": groups, "dilations": [dil, dil]})
     if tail == "add_relu":
-        oh = (H + pads[0] + pads[2] - kh) // st + 1
-        ow = (W + pads[1] + pads[3] - kh) // st + 1
+        oh = (H + pads[0] + pads[2] - dil * (kh - 1) - 1) // st + 1
+        ow = (W + pads[1] + pads[3] - dil * (kh - 1) - 1) // st + 1
         r = m.value("r")
         m.inputs.append("r")
         ins["r"] = rng.uniform(-1, 1, (N, O, oh, ow)).astype(np.float32)

@@ -472,3 +472,46 @@ def test_transpose_invalid_perm(rh):
         g.add_op("t", "Transpose", [x], [y], {"perm": perm})
         with pytest.raises(rh.OpError, match="Permutation is invalid"):
             g.run({x: torch.zeros(2, 3, 4, device="cuda")}, [y])
+
+
+@pytest.mark.parametrize("case", [(300, 256, 520, 132, True), (256, 128, 512, 256, False)],
+                         ids=["ragged-gelu", "even-plain"])
+@pytest.mark.parametrize("pk_out", ["1", "0"])
+def test_matmul_chain_packed_a_bitexact(rh, monkeypatch, case, pk_out):
+    """MatMul -> (Add bias, Gelu) -> MatMul, the producer's output read only as
+    the consumer's A (BERT's FFN1 -> FFN2): from the second run on the
+    producer stores its output in the consumer's packed-A layout and the
+    consumer skips its pack (Plan::mm_next).  Ragged M and a consumer K that is
+    not a whole number of its k tiles check the zero padding.  Bit-exact
+    against the oracle, eager, captured and replayed; RTENHIP_NO_PK_OUT=1 is
+    the unfused reference path."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    M, K1, N1, N2, gelu = case
+    if pk_out == "0":
+        monkeypatch.setenv("RTENHIP_NO_PK_OUT", "1")
+    else:
+        monkeypatch.delenv("RTENHIP_NO_PK_OUT", raising=False)
+    rng = np.random.default_rng(M + N1)
+    m = ModelSpec("mmchain")
+    x = m.value("x")
+    m.inputs = ["x"]
+    w1 = m.const("w1", rng.uniform(-0.1, 0.1, (K1, N1)).astype(np.float32))
+    b1 = m.const("b1", rng.uniform(-0.1, 0.1, (N1,)).astype(np.float32))
+    w2 = m.const("w2", rng.uniform(-0.1, 0.1, (N1, N2)).astype(np.float32))
+    h = m.op("Add", [m.op("MatMul", [x, w1]), b1])
+    if gelu:
+        h = m.op("Gelu", [h])
+    m.outputs = [m.op("MatMul", [h, w2])]
+    ins = {"x": rng.uniform(-1, 1, (2, M // 2, K1)).astype(np.float32)}
+    exp = graph_runner.run(m, ins)[m.outputs[0]]
+    g = m.to_graph()
+    xd = torch.from_numpy(ins["x"]).cuda()
+    out = None
+    for r in range(4):  # eager (tuning), capture, replays
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        got = out[0].cpu().numpy()
+        assert _bits_equal(got, exp), f"run {r}: max abs {np.abs(got - exp).max():.3g}"
