@@ -143,9 +143,13 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
                                 hipStream_t s);
 rtenhip_status launch_softmax(const float* x, float* y, int64_t rows, int64_t len,
                               hipStream_t s);
+struct PackedOut;
+// pk: also store y as a MatMul's packed A (packed_a.h); only the rows kernel
+// does (layer_norm_rows_ok), the call fails otherwise.
 rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
                                  const float* scale, const float* bias, float eps,
-                                 hipStream_t s);
+                                 hipStream_t s, const PackedOut* pk = nullptr);
+bool layer_norm_rows_ok(const float* x, float* y, int64_t len, const float* scale, const float* bias);
 rtenhip_status launch_copy_strided(const rtenhip_tensor& src, float* dst, hipStream_t s);
 // Strided view -> strided view copy of 4-byte elements (either dtype).
 rtenhip_status launch_copy_view(const float* src, const int64_t* shape, const int64_t* src_strides, int ndim,

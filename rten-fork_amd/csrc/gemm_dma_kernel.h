@@ -26,6 +26,7 @@
 #include "common.h"
 #include "gemm_dma.h"
 #include "fastdiv_dev.h"
+#include "packed_a.h"
 #include "vecmath.h"
 
 namespace rtenhip {
@@ -753,16 +754,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
             x.w = apply_act_sel(x.w);
           }
           if (ok) {
-            if (d.pk_out) {
-              // Consumer's packed A: k = n .. n + 3 (n % 4 == 0) are k-quad
-              // planes q = 2g, 2g + 1 (k parity), slots j = 2u, 2u + 1.
-              const int kk = n & ((1 << d.pk_lbk) - 1);
-              const int q0 = 2 * (kk >> 3), u = (kk >> 2) & 1;
-              const int r = m & ((1 << d.pk_lbm) - 1);
-              float* tb = d.pk_out + (((int64_t)(m >> d.pk_lbm) * d.pk_tiles_k + (n >> d.pk_lbk))
-                                      << (d.pk_lbm + d.pk_lbk));
-              *(float2*)(tb + (((int64_t)q0 << d.pk_lbm) + r) * 4 + 2 * u) = make_float2(x.x, x.z);
-              *(float2*)(tb + (((int64_t)(q0 + 1) << d.pk_lbm) + r) * 4 + 2 * u) = make_float2(x.y, x.w);
+            if (d.pk_out) {  // the consumer MatMul's packed A (row m, k = n .. n + 3)
+              store_packed_a4(d.pk_out, d.pk_lbm, d.pk_lbk, d.pk_tiles_k, m, n, x);
             } else {
               *(float4*)(d.out + obase + (int64_t)m * d.out_c) = x;
             }

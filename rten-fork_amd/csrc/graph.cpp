@@ -83,7 +83,7 @@ Plan::~Plan() {
     if (kv.second.counters) (void)hipFree(kv.second.counters);
   }
   if (mm_pack) (void)hipFree(mm_pack);
-  for (auto& kv : mm_prebuf)
+  for (auto& kv : pk_buf)
     if (kv.second.first) (void)hipFree(kv.second.first);
   for (auto& kv : conv_unfused)
     if (kv.second.first) (void)hipFree(kv.second.first);
@@ -916,19 +916,34 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     me.b_rs = b_rs;
     p.matmuls[op] = me;
   }
-  // MatMul -> MatMul pairs (Plan::mm_next): the consumer reads the producer's
-  // output as A, and nothing else reads it.
+  // A operands their producer stores packed (Plan::pk_cons), keyed to the
+  // first dense MatMul (in plan order) that reads them as A.
   if (!getenv("RTENHIP_NO_PK_OUT")) {
     std::map<int, int> producer;  // value -> op
     for (int op : p.ops)
       for (int o : nodes[op].outputs) producer[o] = op;
-    for (auto& kv : p.matmuls) {
-      const int v = nodes[kv.first].inputs[0];
-      if (outset.count(v) || uses[v] != 1 || !producer.count(v)) continue;
+    for (int op : p.ops) {
+      auto cit = p.matmuls.find(op);
+      if (cit == p.matmuls.end()) continue;
+      const int v = nodes[op].inputs[0];
+      if (p.pk_cons.count(v) || !producer.count(v)) continue;
       const int pr = producer[v];
+      const Node& pn = nodes[pr];
       auto pit = p.matmuls.find(pr);
-      if (pit == p.matmuls.end() || pit->second.M != kv.second.M || pit->second.N != kv.second.K) continue;
-      p.mm_next[pr] = kv.first;
+      if (pit != p.matmuls.end()) {
+        if (outset.count(v) || uses[v] != 1 || pit->second.M != cit->second.M || pit->second.N != cit->second.K)
+          continue;
+        p.pk_only.insert(v);
+      } else if (pn.op_type == "LayerNormalization") {
+        const Shape* xs = shape_of(pn.inputs[0]);
+        const int64_t ax = (int64_t)pn.attrs.num("axis", -1);
+        if (!xs || xs->empty() || (ax != -1 && ax != (int64_t)xs->size() - 1) || xs->back() != cit->second.K ||
+            prod(*xs) != cit->second.M * cit->second.K)
+          continue;
+      } else {
+        continue;
+      }
+      p.pk_cons[v] = op;
     }
   }
   // Values produced by a DMA conv and read only (as input 0) by padded DMA
@@ -982,7 +997,13 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   // before the conv3 that consumes it) moves up to just after its last
   // producer and runs on the side stream, concurrently with the main chain;
   // its first consumer joins it.  Only convs that need no ctx scratch.
-  if (use_side_stream) {
+  bool side = side_stream_mode > 0;
+  if (side_stream_mode < 0) {
+    constexpr int64_t kSideStreamMaxBatch = 4;
+    side = !p.convs.empty();
+    for (auto& kv : p.convs) side = side && kv.second.g.N <= kSideStreamMaxBatch;
+  }
+  if (side) {
     std::map<int, int> producer_op;
     for (int op : p.ops)
       for (int o : nodes[op].outputs) producer_op[o] = op;
@@ -1411,6 +1432,19 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     rtenhip_tensor bi{};
     bool has_b = n.inputs.size() > 2 && n.inputs[2] >= 0;
     if (has_b) bi = T(n.inputs[2]);
+    // Also stored as the next MatMul's packed A (Plan::pk_cons).
+    PackedOut po;
+    DmaTile pt{0, 0, 0};
+    const int64_t len = x.ndim ? x.shape[x.ndim - 1] : 0;
+    if (p.pk_cons.count(n.outputs[0]) && is_contiguous(x) && numel(sc) == len && (!has_b || numel(bi) == len) &&
+        packed_out_for(p, n.outputs[0], len ? numel(x) / len : 0, len, po, pt) &&
+        layer_norm_rows_ok(x.data, y.data, len, sc.data, has_b ? bi.data : nullptr)) {
+      rtenhip_status st = launch_layer_norm(x.data, y.data, numel(x) / len, len, sc.data, has_b ? bi.data : nullptr,
+                                            (float)n.attrs.num("epsilon", 1e-5), ctx->stream, &po);
+      if (st) return st;
+      p.pk_ready[n.outputs[0]] = pt;
+      return RTENHIP_OK;
+    }
     return rtenhip_layer_norm_f32(c, &x, &sc, has_b ? &bi : nullptr, (int64_t)n.attrs.num("axis", -1),
                                   (float)n.attrs.num("epsilon", 1e-5), &y);
   }
@@ -1803,12 +1837,12 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     me.cfg = chosen;
     me.persist = persist_mode >= 0 ? persist_mode : chosen_persist;
     p.mm_pack_value = -1;  // tuning overwrote the buffer
-    // The A buffer a producer (Plan::mm_next) stores into from the next run
+    // The A buffer a producer (Plan::pk_cons) stores into from the next run
     // on: allocated here, on the eager first run (later runs may be captured).
-    for (auto& kv : p.mm_next) {
-      if (kv.second != op_id) continue;
+    auto pc = p.pk_cons.find(n.inputs[0]);
+    if (pc != p.pk_cons.end() && pc->second == op_id) {
       const int64_t need = packed_a_floats((int)me.M, (int)me.K, dma_cfg_tile(chosen));
-      auto& buf = p.mm_prebuf[op_id];
+      auto& buf = p.pk_buf[n.inputs[0]];
       if (buf.second < need) {
         RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
         if (buf.first) RTENHIP_HIP_CHECK(hipFree(buf.first));
@@ -1821,31 +1855,29 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
   }
   bind(me, me.cfg);
   const DmaTile tile = dma_cfg_tile(me.cfg);
-  // A stored packed by its producer earlier in this run (Plan::mm_next).
-  auto pre = p.mm_prepacked.find(op_id);
-  if (pre != p.mm_prepacked.end()) {
-    const bool same = pre->second == tile;
-    p.mm_prepacked.erase(pre);
-    if (!same) return fail(RTENHIP_INVALID_VALUE, "MatMul: A was stored packed for another tile shape");
-    da.pk = p.mm_prebuf.at(op_id).first;
+  // A stored packed by its producer earlier in this run (Plan::pk_cons).
+  auto pre = p.pk_ready.find(n.inputs[0]);
+  if (pre != p.pk_ready.end() && pre->second == tile) {
+    da.pk = p.pk_buf.at(n.inputs[0]).first;
     da.pack = false;
     return gemm_dense_dma(ctx, da);
   }
-  // Producer of the next MatMul's A: once that MatMul's tile is known, store
-  // this output in its packed layout instead of row-major.
-  auto nx = p.mm_next.find(op_id);
-  if (nx != p.mm_next.end()) {
-    const MatMulExec& ce = p.matmuls.at(nx->second);
-    if (ce.cfg >= 0) {
+  if (pre != p.pk_ready.end() && p.pk_only.count(n.inputs[0]))
+    return fail(RTENHIP_INVALID_VALUE, "MatMul: A was stored packed for another tile shape");
+  // Producer of a MatMul's A: store this output in that MatMul's packed
+  // layout instead of row-major (its only reader).
+  {
+    PackedOut po;
+    DmaTile pt{0, 0, 0};
+    const int v = n.outputs[0];
+    if (p.pk_only.count(v) && packed_out_for(p, v, me.M, me.N, po, pt)) {
       DenseDmaArgs pk = da;
-      pk.pk_tile = dma_cfg_tile(ce.cfg);
+      pk.pk_tile = pt;
       pk.pk_K = me.N;
-      auto buf = p.mm_prebuf.find(nx->second);
-      if (buf != p.mm_prebuf.end() && buf->second.second >= packed_a_floats((int)me.M, (int)me.N, pk.pk_tile) &&
-          dense_dma_pk_out_ok(pk, me.cfg)) {
-        pk.pk_out = buf->second.first;
+      if (dense_dma_pk_out_ok(pk, me.cfg)) {
+        pk.pk_out = po.p;
         da = pk;
-        p.mm_prepacked[nx->second] = pk.pk_tile;
+        p.pk_ready[v] = pt;
       }
     }
   }
@@ -1853,6 +1885,21 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
   p.mm_pack_value = n.inputs[0];
   p.mm_pack_tile = tile;
   return gemm_dense_dma(ctx, da);
+}
+
+bool Graph::packed_out_for(Plan& p, int v, int64_t M, int64_t K, PackedOut& po, DmaTile& tile) {
+  auto pc = p.pk_cons.find(v);
+  auto pb = p.pk_buf.find(v);
+  if (pc == p.pk_cons.end() || pb == p.pk_buf.end()) return false;
+  const MatMulExec& ce = p.matmuls.at(pc->second);
+  if (ce.cfg < 0 || ce.M != M || ce.K != K) return false;
+  tile = dma_cfg_tile(ce.cfg);
+  if (pb->second.second < packed_a_floats((int)M, (int)K, tile) || tile.bk < 8) return false;
+  po.p = pb->second.first;
+  po.lbm = __builtin_ctz(tile.bm);
+  po.lbk = __builtin_ctz(tile.bk);
+  po.tiles_k = (int)((K + tile.bk - 1) / tile.bk);
+  return true;
 }
 
 // Operands of a DMA / latency conv as the plan lays them out: the input
@@ -2436,7 +2483,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     return RTENHIP_OK;
   };
   plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
-  plan->mm_prepacked.clear();
+  plan->pk_ready.clear();
   if (replay) {
     if (!same_binding) {
       if (plan->exec) {
@@ -2931,7 +2978,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTEN_TIMING")) g->timing = s[0] != 0 && s[0] != '0';
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
-  if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->use_side_stream = s[0] != '0';
+  if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->side_stream_mode = atoi(s) > 0 ? 1 : 0;
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   if (const char* s = getenv("RTENHIP_LAT")) g->lat_mode = atoi(s);

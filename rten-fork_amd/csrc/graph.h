@@ -14,6 +14,7 @@
 #include "common.h"
 #include "ctx.h"
 #include "gemm_dma.h"
+#include "packed_a.h"
 
 namespace rtenhip {
 
@@ -201,14 +202,18 @@ struct Plan {
   // projections -- pack it once) and the tile shape; -1 = nothing.
   int mm_pack_value = -1;
   DmaTile mm_pack_tile{0, 0, 0};
-  // Dense MatMul -> MatMul pairs where the producer's output is read only as
-  // the consumer's A (BERT's FFN1 -> FFN2): producer op -> consumer op.  Once
-  // the consumer's tile is chosen (first run) the producer stores straight
-  // into the consumer's packed-A buffer (consumer op -> buffer, floats; zeroed
-  // once, so the tile padding stays zero) and the consumer skips its pack.
-  std::map<int, int> mm_next;
-  std::map<int, std::pair<float*, int64_t>> mm_prebuf;
-  std::map<int, DmaTile> mm_prepacked;  // consumer op -> tile its A was stored in during this run
+  // A operands stored packed by their producer (packed_a.h), so the dense
+  // MatMuls reading them skip pack_a: value -> its first dense-MatMul reader
+  // (whose tile, chosen on the first run, fixes the layout).  Producers: a
+  // dense MatMul whose output nothing else reads (BERT's FFN1 -> FFN2; it then
+  // stores only the packed layout, pk_only) or a LayerNormalization over the
+  // rows (row-major for its other readers, and packed: BERT's LN -> Q/K/V and
+  // FFN1).  pk_buf: value -> buffer, floats (zeroed once, so the tile padding
+  // stays zero); pk_ready: value -> tile stored during this run.
+  std::map<int, int> pk_cons;
+  std::set<int> pk_only;
+  std::map<int, std::pair<float*, int64_t>> pk_buf;
+  std::map<int, DmaTile> pk_ready;
   // Ops launched on the side stream (independent branches such as the
   // ResNet downsample conv), and for each op the side ops it must wait for.
   std::set<int> side;
@@ -253,7 +258,11 @@ struct Graph {
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
   hipStream_t side_stream = nullptr;
-  bool use_side_stream = false;  // RTENHIP_SIDE_STREAM=1: downsample branches on a second stream (measured 0.5% slower on ResNet-50 b64: the concurrent kernels were tuned alone)
+  // Downsample branches on a second stream: 1 always, 0 never, -1 (default)
+  // for plans whose image batch is at most kSideStreamMaxBatch -- latency-bound
+  // convs that leave most CUs idle (measured 0.5% slower on ResNet-50 b64,
+  // where the concurrent kernels were tuned alone).  RTENHIP_SIDE_STREAM.
+  int side_stream_mode = -1;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
   bool use_hip_graph = true;
@@ -308,6 +317,8 @@ struct Graph {
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
+  // The packed-A store a producer of value v makes this run, or false.
+  bool packed_out_for(Plan& p, int v, int64_t M, int64_t K, PackedOut& po, DmaTile& tile);
   rtenhip_status exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& a,
                                  const rtenhip_tensor& b, const rtenhip_tensor& y, MatMulExec& me);
   float* ptr_of(Plan& p, int value_id);

@@ -25,6 +25,7 @@
 // outputs are computed from LDS and stored (coalesced rows).
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "common.h"
 #include "vecmath.h"
@@ -55,18 +56,26 @@ __device__ __forceinline__ float ed_act(float v, int act, float lo, float hi) {
 
 constexpr int kEdMargin = 4;  // floats before each LDS plane (never read: colok)
 
-constexpr int kEdMaxQ = 4;  // depthwise outputs per thread and channel (TR * OW <= 1024)
+constexpr int kEdMaxQ = 4;   // depthwise outputs per thread and channel (TR * OW <= 1024)
+constexpr int kEdZs = 16;    // floats before a plane's interior: the 9 zero slots (+ pad)
 
-// CP channels per pass (one barrier per pass).  The block's expand and
-// depthwise weights and biases are staged in LDS once (wave-uniform reads are
-// LDS broadcasts); each thread's depthwise outputs -- their LDS tap offsets and
-// the 9-bit mask of taps the reference visits -- are fixed before the channel
-// loop, so a channel's depthwise step is 9 LDS reads and selects per output.
-template <int CIN, int S, int CP>
+// Expand plane size in floats (zero slots, rows_in rows of W, a tail margin).
+__host__ __device__ inline int ed_plane(int rows_in, int W) { return kEdZs + rows_in * W + 4; }
+
+// CP channels per pass (one barrier per pass); PLANE = ed_plane(...) when
+// compile-time (every LDS offset an immediate), 0 = runtime.  The block's
+// expand and depthwise weights and biases are staged in LDS once; each
+// thread's depthwise outputs have their 9 tap addresses fixed before the
+// channel loop.  A tap the reference skips (a row outside the image, a column
+// outside min_max_out_x_coords) is pointed at a per-channel "zero slot"
+// holding copysign(0, -w): its product is exactly -0, and x + (-0) == x for
+// every x (+-0, inf and NaN included), so adding it is the skip -- for finite
+// w.  A channel with a non-finite tap weight takes the select path instead.
+template <int CIN, int S, int CP, int PLANE, int NQ>
 __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   extern __shared__ float4 ed_lds4[];
   float* lds = reinterpret_cast<float*>(ed_lds4);
-  const int plane = d.rows_in * d.W + 2 * kEdMargin;  // one expand plane (2 * CP of them)
+  const int plane = PLANE > 0 ? PLANE : ed_plane(d.rows_in, d.W);
   const int n = blockIdx.y;
   const int oy0 = blockIdx.x * d.TR;
   const int iy_lo = oy0 * S - d.pt;  // input row of LDS row 0
@@ -77,12 +86,16 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   float* w_d = w_e + d.cpb * CIN;     // [cnt][9]
   float* b_e = w_d + d.cpb * 9;       // [cnt]
   float* b_d = b_e + d.cpb;           // [cnt]
+  int* fin = reinterpret_cast<int*>(b_d + d.cpb);  // [cnt]: every tap weight finite
   const int t = threadIdx.x;
   for (int i = t; i < cnt * CIN; i += 256) w_e[i] = d.we[(int64_t)c_begin * CIN + i];
   for (int i = t; i < cnt * 9; i += 256) w_d[i] = d.wd[(int64_t)c_begin * 9 + i];
   for (int i = t; i < cnt; i += 256) {
     b_e[i] = d.be ? d.be[c_begin + i] : 0.f;
     b_d[i] = d.bd ? d.bd[c_begin + i] : 0.f;
+    bool f = true;
+    for (int k = 0; k < 9; k++) f = f && __builtin_isfinite(d.wd[(int64_t)(c_begin + i) * 9 + k]);
+    fin[i] = f;
   }
   const int W4 = d.W >> 2;
   const int er = t / W4, ec = (t - er * W4) * 4;  // this thread's expand pixels: LDS row er, cols ec..ec+3
@@ -95,28 +108,27 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
 #pragma unroll
     for (int k = 0; k < CIN; k++) xr[k] = *(const float4*)(xp + k * HW);
   }
-  // Depthwise outputs o = t + 256 q of the band: LDS offset of tap (0, 0)
-  // (input row oy*S - pt is LDS row ol*S) and the taps inside the image rows
-  // and the min_max_out_x_coords columns.
+  // Depthwise outputs o = t + 256 q of the band: tap addresses (floats from
+  // the plane start; a skipped tap -> its zero slot) and the skip mask.
   const int n_out = min(d.TR, d.OH - oy0) * d.OW;
-  int toff[kEdMaxQ];
-  uint32_t tmask[kEdMaxQ];
+  int taddr[NQ][9];
+  uint32_t tmask[NQ];
 #pragma unroll
-  for (int q = 0; q < kEdMaxQ; q++) {
+  for (int q = 0; q < NQ; q++) {
     const int o = t + 256 * q;
     const int ol = o / d.OW, ox = o - ol * d.OW;
     const int oy = oy0 + ol;
-    toff[q] = ol * S * d.W + ox * S - d.pl;
-    uint32_t m = 0;
-    if (o < n_out) {
-      m = 1u << 9;  // an output of this band
+    const int base = kEdZs + ol * S * d.W + ox * S - d.pl;  // tap (0, 0), LDS row ol * S
+    uint32_t m = o < n_out ? 1u << 9 : 0u;  // bit 9: an output of this band
 #pragma unroll
-      for (int ky = 0; ky < 3; ky++) {
-        const int r = oy * S + ky - d.pt;
-        if (r < 0 || r >= d.H) continue;
+    for (int ky = 0; ky < 3; ky++) {
+      const int r = oy * S + ky - d.pt;
+      const bool row_ok = r >= 0 && r < d.H;
 #pragma unroll
-        for (int kx = 0; kx < 3; kx++)
-          if (ox >= d.omin[kx] && ox < d.omax[kx]) m |= 1u << (ky * 3 + kx);
+      for (int kx = 0; kx < 3; kx++) {
+        const bool on = o < n_out && row_ok && ox >= d.omin[kx] && ox < d.omax[kx];
+        m |= on ? 1u << (ky * 3 + kx) : 0u;
+        taddr[q][ky * 3 + kx] = on ? base + ky * d.W + kx : ky * 3 + kx;
       }
     }
     tmask[q] = m;
@@ -129,8 +141,12 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
     return relu ? r : (clip ? c : v);
   };
   __syncthreads();  // weights staged
-  for (int c0 = c_begin, pass = 0; c0 < c_end; c0 += CP, pass++) {
-    float* ebuf = lds + (pass & 1) * CP * plane + kEdMargin;
+
+  // One pass: CP channels from c0 into buffer B (compile-time, so with a
+  // compile-time PLANE the buffer / channel offsets are LDS immediates).
+  auto pass = [&](const int c0, auto Bc) __attribute__((always_inline)) {
+    constexpr int B = decltype(Bc)::value;
+    float* ebuf = lds + B * CP * plane;
     if (e_on) {
 #pragma unroll
       for (int j = 0; j < CP; j++) {
@@ -155,8 +171,13 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
         v.y = act(v.y, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
         v.z = act(v.z, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
         v.w = act(v.w, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
-        *(float4*)(ebuf + j * plane + er * d.W + ec) = v;
+        *(float4*)(ebuf + j * plane + kEdZs + er * d.W + ec) = v;
       }
+    }
+    if (t < 9 * CP) {  // zero slots: copysign(0, -w) per tap
+      const int j = t / 9, k = t - 9 * j;
+      const int cl = min(c0 + j, c_end - 1) - c_begin;
+      ebuf[j * plane + k] = copysignf(0.f, -w_d[cl * 9 + k]);
     }
     // One barrier per pass: the planes written next pass are the other
     // buffer, and the ones after that are only written once every thread has
@@ -173,22 +194,34 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
       for (int i = 0; i < 9; i++) wk[i] = w_d[cl * 9 + i];
       const float b0 = b_d[cl];
       float* yc = d.y + ((int64_t)n * d.hidden + c) * d.OH * d.OW + (int64_t)oy0 * d.OW;
+      if (fin[cl]) {
 #pragma unroll
-      for (int q = 0; q < kEdMaxQ; q++) {
-        const uint32_t m = tmask[q];
-        if (!(m >> 9)) continue;  // not an output of this band
-        float acc = b0;
+        for (int q = 0; q < NQ; q++) {
+          if (!(tmask[q] >> 9)) continue;  // not an output of this band
+          float acc = b0;
 #pragma unroll
-        for (int ky = 0; ky < 3; ky++)
+          for (int i = 0; i < 9; i++) acc = __fadd_rn(acc, __fmul_rn(eb[taddr[q][i]], wk[i]));
+          yc[t + 256 * q] = act(acc, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+        }
+      } else {
 #pragma unroll
-          for (int kx = 0; kx < 3; kx++) {
-            const bool on = (m >> (ky * 3 + kx)) & 1u;
-            const float v = eb[on ? toff[q] + ky * d.W + kx : 0];
-            acc = on ? __fadd_rn(acc, __fmul_rn(v, wk[ky * 3 + kx])) : acc;
+        for (int q = 0; q < NQ; q++) {
+          const uint32_t m = tmask[q];
+          if (!(m >> 9)) continue;
+          float acc = b0;
+#pragma unroll
+          for (int i = 0; i < 9; i++) {
+            const float pr = __fmul_rn(eb[taddr[q][i]], wk[i]);
+            acc = (m >> i) & 1u ? __fadd_rn(acc, pr) : acc;
           }
-        yc[t + 256 * q] = act(acc, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+          yc[t + 256 * q] = act(acc, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+        }
       }
     }
+  };
+  for (int c0 = c_begin; c0 < c_end; c0 += 2 * CP) {
+    pass(c0, std::integral_constant<int, 0>{});
+    if (c0 + CP < c_end) pass(c0 + CP, std::integral_constant<int, 1>{});
   }
 }
 
@@ -378,13 +411,28 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
   while ((int64_t)bands * N * chunks < 1024 && hidden / (chunks * 2) >= 16) chunks *= 2;
   d.cpb = (hidden + chunks - 1) / chunks;
   constexpr int CP = 2;
-  const size_t lds = (2 * CP * ((size_t)d.rows_in * W + 2 * kEdMargin) + (size_t)d.cpb * (cin + 9 + 2)) * sizeof(float);
+  const int plane = ed_plane(d.rows_in, W);
+  const size_t lds = (2 * CP * (size_t)plane + (size_t)d.cpb * (cin + 9 + 3)) * sizeof(float);
   if (lds > 64 * 1024 || N > 65535 || chunks > 65535 || (int64_t)d.TR * OW > 256 * kEdMaxQ)
     return fail(RTENHIP_UNSUPPORTED_VALUE, "expand+depthwise tile too large");
   dim3 grid((unsigned)bands, (unsigned)N, (unsigned)chunks);
+  // Compile-time planes for MobileNetV2's pairs (features.2 / .3 / .4 / .5-6 / .7).
+  const int nq = (int)((d.TR * OW + 255) / 256);  // depthwise outputs per thread and channel
+#define ED_PL(C, SS, PL, Q)                                                                   \
+  if (cin == C && S == SS && plane == PL && nq <= Q) {                                       \
+    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, PL, Q>), grid, dim3(256), lds, s, d);   \
+    RTENHIP_LAUNCH_CHECK();                                                                  \
+    return RTENHIP_OK;                                                                       \
+  }
+  ED_PL(16, 2, 1028, 1)
+  ED_PL(24, 1, 1028, 4)
+  ED_PL(24, 2, 972, 1)
+  ED_PL(32, 1, 860, 4)
+  ED_PL(32, 2, 832, 1)
+#undef ED_PL
 #define ED_CASE(C, SS) \
   if (cin == C && S == SS) { \
-    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP>), grid, dim3(256), lds, s, d); \
+    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, 0, kEdMaxQ>), grid, dim3(256), lds, s, d); \
     RTENHIP_LAUNCH_CHECK(); \
     return RTENHIP_OK; \
   }

@@ -11,6 +11,7 @@
 //    1/sqrt(iter_sum(d*d)/n + eps) (iter_sum: groups of 4,
 //    slice_reductions.rs:57-84), then * inv, * scale, + bias.
 #include "common.h"
+#include "packed_a.h"
 #include "vecmath.h"
 
 #include <algorithm>
@@ -198,7 +199,7 @@ __device__ __forceinline__ float strided_sum_n(const float* p, int s) {
 template <int LEN>
 __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const float* __restrict__ x, float* __restrict__ y, int64_t rows, int len_arg, int R,
-    const float* __restrict__ scale, const float* __restrict__ bias, float eps) {
+    const float* __restrict__ scale, const float* __restrict__ bias, float eps, PackedOut pk) {
   const int len = LEN > 0 ? LEN : len_arg;
   extern __shared__ float4 lds4[];
   const int q = len >> 2;              // float4s per row
@@ -283,14 +284,47 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         o.w = __fadd_rn(o.w, bb.w);
       }
       y4[r * q + c] = o;
+      if (pk.p) lds4[r * q + c] = o;  // this thread's own element: no hazard
+    }
+  }
+  if (pk.p) {
+    // The MatMul's packed A (packed_a.h): one 16-byte chunk per (k tile,
+    // plane, row) with the row fastest, so consecutive threads write
+    // consecutive chunks of a plane (rows are 16 bytes apart in it).
+    __syncthreads();
+    const int BK = 1 << pk.lbk, nq = BK >> 2;
+    const int ktiles = (len + BK - 1) >> pk.lbk;
+    const int total = nr * nq * ktiles;
+    for (int i = threadIdx.x; i < total; i += 256) {
+      const int r = i % nr, t2 = i / nr;
+      const int qq = t2 % nq, tk = t2 / nq;
+      const int kb = tk * BK + 8 * (qq >> 1) + (qq & 1);
+      const float* xr = xs + r * len;
+      const float4 v = make_float4(kb < len ? xr[kb] : 0.f, kb + 2 < len ? xr[kb + 2] : 0.f,
+                                   kb + 4 < len ? xr[kb + 4] : 0.f, kb + 6 < len ? xr[kb + 6] : 0.f);
+      const int64_t m = row0 + r;
+      float* tb = pk.p + (((m >> pk.lbm) * pk.tiles_k + tk) << (pk.lbm + pk.lbk));
+      *(float4*)(tb + (((int64_t)qq << pk.lbm) + (m & ((1 << pk.lbm) - 1))) * 4) = v;
     }
   }
 }
 
+bool layer_norm_rows_ok(const float* x, float* y, int64_t len, const float* scale, const float* bias) {
+  if (len % 8 != 0 || (uintptr_t)x % 16 || (uintptr_t)y % 16 || (uintptr_t)scale % 16 ||
+      (bias && (uintptr_t)bias % 16))
+    return false;
+  const int R = (int)std::max<int64_t>(1, std::min<int64_t>(16, 6144 / len));
+  const int64_t ngroups = (len - 1) / 4;
+  return ((size_t)R * len + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float) <= 64 * 1024;
+}
+
 rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
                                  const float* scale, const float* bias, float eps,
-                                 hipStream_t s) {
+                                 hipStream_t s, const PackedOut* pk) {
   if (rows == 0 || len == 0) return RTENHIP_OK;
+  if (pk && (!layer_norm_rows_ok(x, y, len, scale, bias) || getenv("RTENHIP_LN_ROWS")))
+    return fail(RTENHIP_UNSUPPORTED_VALUE, "LayerNorm: packed output needs the rows kernel");
+  const PackedOut pko = pk ? *pk : PackedOut{};
   const bool rows_ok = len % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
                        (uintptr_t)scale % 16 == 0 && (!bias || (uintptr_t)bias % 16 == 0);
   if (rows_ok) {
@@ -309,7 +343,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                   : len == 1024 ? layer_norm_rows_kernel<1024>
                                 : layer_norm_rows_kernel<0>;
       hipLaunchKernelGGL(kern, dim3((unsigned)rblocks), dim3(256), rshm, s, x, y, rows, (int)len, R,
-                         scale, bias, eps);
+                         scale, bias, eps, pko);
       RTENHIP_LAUNCH_CHECK();
       return RTENHIP_OK;
     }

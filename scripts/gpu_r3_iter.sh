@@ -8,7 +8,7 @@ O=gpurun_out/iter; mkdir -p $O
 export RTEN_NUM_THREADS=8
 PYT="python -u -m pytest -x -q --timeout 200 --timeout-method thread"
 timeout -k 10 600 $PYT tests/test_conv_lat_gpu.py tests/test_conv_pointwise_gpu.py tests/test_model_gpu.py \
-  -k "lat or chain or expand or attention or bert or mobilenet or matmul" > $O/tests.log 2>&1 \
+  -k "lat or chain or expand or attention or bert or mobilenet or matmul or side or layernorm" > $O/tests.log 2>&1 \
   || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 bench() {  # name, args
@@ -17,6 +17,7 @@ bench() {  # name, args
   python3 -c "import json;d=json.load(open('$O/$n.json'));print('$n', d['value'], d['ms_per_step'])"
 }
 bench b1 --batch 1 --steps 200 --warmup 20
+RTENHIP_SIDE_STREAM=0 bench b1_noside --batch 1 --steps 200 --warmup 20
 bench mnv2 --model mobilenet_v2 --batch 128
 bench bert --model bert --batch 32
 if [ -n "$FULL" ]; then

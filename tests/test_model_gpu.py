@@ -85,12 +85,14 @@ def test_resnet50_batch64_full_size(rh, monkeypatch):
             assert _bits_equal(out[0].cpu().numpy(), exp), f"RTENHIP_PERSIST={mode}"
 
 
-def test_resnet50_side_stream(rh, monkeypatch):
-    """The downsample branch on the executor's second stream (off by
-    default, RTENHIP_SIDE_STREAM=1): same bits, eager and replayed."""
+@pytest.mark.parametrize("side", ["1", "0"])
+def test_resnet50_side_stream(rh, monkeypatch, side):
+    """The downsample branch on the executor's second stream (the default
+    for batches up to 4, forced by RTENHIP_SIDE_STREAM=1, off with 0): same
+    bits, eager and replayed."""
     from rten_hip import models
 
-    monkeypatch.setenv("RTENHIP_SIDE_STREAM", "1")
+    monkeypatch.setenv("RTENHIP_SIDE_STREAM", side)
     exp, outs = _run_both(rh, models.resnet50(), batch=2, runs=3)
     for o in outs:
         assert _bits_equal(o, exp), np.abs(o - exp).max()
@@ -515,3 +517,44 @@ def test_matmul_chain_packed_a_bitexact(rh, monkeypatch, case, pk_out):
         torch.cuda.synchronize()
         got = out[0].cpu().numpy()
         assert _bits_equal(got, exp), f"run {r}: max abs {np.abs(got - exp).max():.3g}"
+
+
+@pytest.mark.parametrize("pk_out", ["1", "0"])
+def test_layernorm_packed_a_bitexact(rh, monkeypatch, pk_out):
+    """LayerNormalization -> two MatMuls reading it as A (BERT's LN -> Q / K)
+    with the LN output also the second MatMul's fused residual: from the
+    second run on the LN stores its rows both row-major and in the MatMuls'
+    packed-A layout, and neither MatMul packs A (Plan::pk_cons).  Ragged M
+    (300 rows).  Bit-exact, eager, captured and replayed."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    if pk_out == "0":
+        monkeypatch.setenv("RTENHIP_NO_PK_OUT", "1")
+    else:
+        monkeypatch.delenv("RTENHIP_NO_PK_OUT", raising=False)
+    rng = np.random.default_rng(5)
+    M, K, N = 300, 256, 256
+    m = ModelSpec("lnmm")
+    x = m.value("x")
+    m.inputs = ["x"]
+    sc = m.const("sc", rng.uniform(0.5, 1.5, (K,)).astype(np.float32))
+    bi = m.const("bi", rng.uniform(-0.1, 0.1, (K,)).astype(np.float32))
+    h = m.op("LayerNormalization", [x, sc, bi], {"axis": -1, "epsilon": 1e-12})
+    w1 = m.const("w1", rng.uniform(-0.1, 0.1, (K, N)).astype(np.float32))
+    w2 = m.const("w2", rng.uniform(-0.1, 0.1, (K, N)).astype(np.float32))
+    q = m.op("MatMul", [h, w1])
+    k = m.op("Add", [m.op("MatMul", [h, w2]), h])
+    m.outputs = [q, k]
+    ins = {"x": rng.uniform(-1, 1, (3, M // 3, K)).astype(np.float32)}
+    res = graph_runner.run(m, ins)
+    g = m.to_graph()
+    xd = torch.from_numpy(ins["x"]).cuda()
+    out = None
+    for r in range(4):  # eager (tuning), capture, replays
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        for i, name in enumerate(m.outputs):
+            got = out[i].cpu().numpy()
+            assert _bits_equal(got, res[name]), f"run {r} output {i}: max abs {np.abs(got - res[name]).max():.3g}"
