@@ -178,7 +178,10 @@ static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaT
   d.act_lo = a.lo;
   d.act_hi = a.hi;
   if (lat && a.kh == 1 && a.kw == 1) d.kstride = (int)(a.Hp * a.Wp);
-  if (lat && a.kh == 3 && a.kw == 3) {
+  static const bool lat_ktab = getenv("RTENHIP_LAT_KTAB") != nullptr;  // A/B experiments: table offsets
+  static const int lat_dbg = getenv("RTENHIP_LAT_DBG") ? atoi(getenv("RTENHIP_LAT_DBG")) : 0;
+  if (lat) d.dbg = lat_dbg;
+  if (lat && a.kh == 3 && a.kw == 3 && !lat_ktab) {
     // Same offsets as the table (Ctx::dtab), formed in the kernel.
     d.k3x3 = 1;
     d.kt_plane = (int)(a.Hp * a.Wp);

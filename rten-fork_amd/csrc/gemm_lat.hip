@@ -69,7 +69,8 @@ __global__ __launch_bounds__(512) void gemm_lat_wg_kernel(DmaDesc d, int n16, in
   const int nt = o % n16, sub0 = (o / n16) * MI;
   const LatCol col = lat_col(d, nt * 16);
   LatEpi<MI> e;  // wave 0's epilogue operands, loaded along with its first block's operands
-  if (wave == 0) lat_epi_loads<MI>(d, sub0, col, false, e);
+  const bool early = !(d.dbg & 4);  // (d.dbg & 4: A/B experiments only, loaded after the chains)
+  if (wave == 0 && early) lat_epi_loads<MI>(d, sub0, col, false, e);
   for (int kb = wave; kb < nkb; kb += W) {
     lat_f32x4 acc[MI];
     lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, LatNoWait{}, false, acc);
@@ -77,6 +78,7 @@ __global__ __launch_bounds__(512) void gemm_lat_wg_kernel(DmaDesc d, int n16, in
     for (int mi = 0; mi < MI; mi++)
       part[(kb * MI + mi) * 64 + lane] = make_float4(acc[mi][0], acc[mi][1], acc[mi][2], acc[mi][3]);
   }
+  if (wave == 0 && !early) lat_epi_loads<MI>(d, sub0, col, false, e);
   __syncthreads();
   if (wave != 0) return;
   lat_f32x4 sum[MI];

@@ -2978,7 +2978,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTEN_TIMING")) g->timing = s[0] != 0 && s[0] != '0';
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
-  if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->side_stream_mode = atoi(s) > 0 ? 1 : 0;
+  if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->side_stream_mode = atoi(s) > 0 ? 1 : (atoi(s) < 0 ? -1 : 0);
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   if (const char* s = getenv("RTENHIP_LAT")) g->lat_mode = atoi(s);

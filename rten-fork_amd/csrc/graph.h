@@ -258,11 +258,12 @@ struct Graph {
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
   hipStream_t side_stream = nullptr;
-  // Downsample branches on a second stream: 1 always, 0 never, -1 (default)
-  // for plans whose image batch is at most kSideStreamMaxBatch -- latency-bound
-  // convs that leave most CUs idle (measured 0.5% slower on ResNet-50 b64,
-  // where the concurrent kernels were tuned alone).  RTENHIP_SIDE_STREAM.
-  int side_stream_mode = -1;
+  // Downsample branches on a second stream: 1 always, 0 never (default), -1
+  // for plans whose image batch is at most kSideStreamMaxBatch.  Measured
+  // slower at both ends: 0.5% on ResNet-50 b64 (the concurrent kernels were
+  // tuned alone) and 5% at batch 1 (0.591 -> 0.623 ms, the cross-stream
+  // event waits cost more than the overlap gains).  RTENHIP_SIDE_STREAM.
+  int side_stream_mode = 0;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
   bool use_hip_graph = true;

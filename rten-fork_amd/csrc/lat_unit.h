@@ -259,11 +259,13 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
   // Epilogue operands, issued before any store (vmcnt retires in order); a
   // standalone launch issues them with the operand loads (one memory round
   // trip fewer on the unit's path), a chain after its dependency wait.
+  // (d.dbg & 4: A/B experiments only, the loads after the chain.)
+  const bool early = !CHAIN && !(d.dbg & 4);
   LatEpi<MI> e;
-  if (!CHAIN) lat_epi_loads<MI>(d, sub0, col, false, e);
+  if (early) lat_epi_loads<MI>(d, sub0, col, false, e);
   lat_f32x4 acc[MI];
   lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, wait, sc1_ld, acc);
-  if (CHAIN) lat_epi_loads<MI>(d, sub0, col, sc1_ld, e);
+  if (!early) lat_epi_loads<MI>(d, sub0, col, sc1_ld, e);
   const float alpha = d.alpha;
 
   lat_f32x4 sum[MI];

@@ -5,10 +5,13 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/b1p; mkdir -p $O
 export RTEN_NUM_THREADS=8
+# variants: side stream on/off; latency GEMM K table / late epilogue loads (the round-2 forms)
 for i in 1 2; do
-  for side in 0 1; do
-    RTENHIP_SIDE_STREAM=$side timeout -k 10 200 python -u bench.py --batch 1 --steps 300 --warmup 30 --no-cpu-baseline > $O/b1_s${side}_$i.json 2> $O/b1.err || { tail $O/b1.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/b1_s${side}_$i.json'));print('side=$side', d['value'], d['ms_per_step'])"
+  for v in "s0:RTENHIP_SIDE_STREAM=0" "s1:RTENHIP_SIDE_STREAM=1" "ktab:RTENHIP_SIDE_STREAM=0 RTENHIP_LAT_KTAB=1" \
+           "late:RTENHIP_SIDE_STREAM=0 RTENHIP_LAT_DBG=4" "old:RTENHIP_SIDE_STREAM=0 RTENHIP_LAT_KTAB=1 RTENHIP_LAT_DBG=4"; do
+    name=${v%%:*}
+    env ${v#*:} timeout -k 10 200 python -u bench.py --batch 1 --steps 300 --warmup 30 --no-cpu-baseline > $O/b1_${name}_$i.json 2> $O/b1.err || { tail $O/b1.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$O/b1_${name}_$i.json'));print('$name', d['value'], d['ms_per_step'])"
   done
 done
 RTENHIP_SIDE_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv \

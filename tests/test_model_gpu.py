@@ -85,10 +85,10 @@ def test_resnet50_batch64_full_size(rh, monkeypatch):
             assert _bits_equal(out[0].cpu().numpy(), exp), f"RTENHIP_PERSIST={mode}"
 
 
-@pytest.mark.parametrize("side", ["1", "0"])
+@pytest.mark.parametrize("side", ["1", "-1"])
 def test_resnet50_side_stream(rh, monkeypatch, side):
-    """The downsample branch on the executor's second stream (the default
-    for batches up to 4, forced by RTENHIP_SIDE_STREAM=1, off with 0): same
+    """The downsample branch on the executor's second stream (off by
+    default; RTENHIP_SIDE_STREAM=1 always, -1 for batches up to 4): same
     bits, eager and replayed."""
     from rten_hip import models
 
