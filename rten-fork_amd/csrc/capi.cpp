@@ -254,6 +254,32 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
   return RTENHIP_OK;
 }
 
+// ResNet's conv3 + downsample pair as one dual DMA GEMM (gemm_dma_kernel
+// DUAL): y = act((W3·h + b3) + (Wd·x + bd)), both ungrouped, same output.
+// a3: conv3 (its residual is ignored: the downsample's value takes its
+// place), ad: the downsample; both packed for cfg.
+bool conv_dual_ok(const ConvDmaArgs& a3, const ConvDmaArgs& ad, int cfg) {
+  return cfg >= 0 && cfg < dma_num_cfgs() && dma_cfg_dual(cfg) && a3.groups == 1 && ad.groups == 1 &&
+         a3.O == ad.O && a3.N == ad.N && a3.oh == ad.oh && a3.ow == ad.ow && !a3.split &&
+         conv_dma_eligible(a3.N, a3.C, a3.Hp, a3.Wp, a3.O, 1, a3.C * a3.kh * a3.kw) &&
+         conv_dma_eligible(ad.N, ad.C, ad.Hp, ad.Wp, ad.O, 1, ad.C * ad.kh * ad.kw);
+}
+
+rtenhip_status conv_dma_dual(Ctx* c, const ConvDmaArgs& a3, const ConvDmaArgs& ad) {
+  const int cfg = a3.cfg;
+  if (!conv_dual_ok(a3, ad, cfg)) return fail(RTENHIP_UNSUPPORTED_VALUE, "conv pair not supported by the dual GEMM");
+  const DmaTile tile = dma_cfg_tile(cfg);
+  const int* t3 = c->dtab((int)a3.C, (int)a3.Hp, (int)a3.Wp, (int)a3.kh, (int)a3.kw, (int)a3.dh, (int)a3.dw);
+  const int* td = c->dtab((int)ad.C, (int)ad.Hp, (int)ad.Wp, (int)ad.kh, (int)ad.kw, (int)ad.dh, (int)ad.dw);
+  if (!t3 || !td) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
+  DmaDesc d3, dd;
+  fill_conv_desc(a3, 0, false, tile, t3, d3);
+  fill_conv_desc(ad, 0, false, tile, td, dd);
+  d3.residual = nullptr;
+  d3.persist_k = a3.persist_k;
+  return launch_gemm_dma(d3, cfg, c->stream, &dd);
+}
+
 const int2* Ctx::ktab(int C, int H, int W, int kh, int kw, int dh, int dw) {
   auto key = std::make_tuple(C, H, W, kh, kw, dh, dw);
   std::lock_guard<std::mutex> g(mu);

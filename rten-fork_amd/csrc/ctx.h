@@ -88,6 +88,10 @@ struct ConvDmaArgs {
   int64_t H, W, pad_t, pad_l;
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
+// conv3 + downsample as one dual DMA GEMM (see capi.cpp); cfg = a3.cfg, both
+// packed for it.
+bool conv_dual_ok(const ConvDmaArgs& a3, const ConvDmaArgs& ad, int cfg);
+rtenhip_status conv_dma_dual(Ctx* c, const ConvDmaArgs& a3, const ConvDmaArgs& ad);
 // The latency GEMM's descriptor of an ungrouped conv (conv chains), without
 // split workspace: the caller sets d.ws / d.counters when K > 256.
 struct DmaDesc;

@@ -94,7 +94,10 @@ DmaTile dma_cfg_tile(int cfg);
 int64_t packed_a_floats(int M, int K, const DmaTile& t);
 rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const DmaTile& t,
                              float* out, hipStream_t s);
-rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s);
+// d2: dual GEMM (gemm_dma_kernel DUAL) -- d2's folded values are added to
+// d's in d's epilogue (d2 = ResNet's downsample conv, d = conv3).
+rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const DmaDesc* d2 = nullptr);
+bool dma_cfg_dual(int cfg);
 
 // Latency GEMM (gemm_lat.hip): the same DmaDesc addressing and summation
 // order, one wave per 16x16 output tile and KC block (small-batch convs).

@@ -34,6 +34,18 @@ bool dma_cfg_bvec(int cfg) {
   }
 }
 
+bool dma_cfg_dual(int cfg) {
+  switch (cfg) {
+#define RTENHIP_DMA_DU(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) \
+  case id:                                                  \
+    return dma_dual_ok<NT, BM, BN, BK, WMW, WNW>();
+    RTENHIP_DMA_CONFIGS(RTENHIP_DMA_DU)
+#undef RTENHIP_DMA_DU
+    default:
+      return false;
+  }
+}
+
 bool dma_cfg_vec_epilogue(int cfg) {
   switch (cfg) {
 #define RTENHIP_DMA_VE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) \
@@ -83,7 +95,7 @@ DmaSplit dma_split_plan(int M, int N, int K, int cfg) {
   return sp;
 }
 
-rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
+rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const DmaDesc* d2) {
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty DMA GEMM");
   if (cfg < 0 || cfg >= kNumDmaCfgs) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
   if (!(dma_cfg_tile(cfg) == d.tile))
@@ -104,14 +116,26 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s) {
   } else {
     dd.n_full = tiles;
   }
-  bool launched = false;
-  switch (cfg % DMA_PARTS) {
-    case 0: launched = dma_launch_part<0>(cfg, dd, s); break;
-    case 1: launched = dma_launch_part<1>(cfg, dd, s); break;
-    case 2: launched = dma_launch_part<2>(cfg, dd, s); break;
-    default: launched = dma_launch_part<3>(cfg, dd, s); break;
+  DmaDesc dd2{};
+  if (d2) {
+    // Dual GEMM: same output tiles, no KC split, both segments through the
+    // multi-block fold with 4-byte B copies.
+    if (d2->M != d.M || d2->N != d.N || d2->K <= 0 || !(d2->tile == d.tile) || d.split_tiles || d.residual ||
+        d.cin || d2->cin || d.bvec || d2->bvec || d.pk_out)
+      return fail(RTENHIP_INVALID_VALUE, "bad dual DMA GEMM");
+    dd2 = *d2;
+    dd2.dbg = dd.dbg;
+    dd2.n_full = dd.n_full;
   }
-  if (!launched) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
+  bool launched = false;
+  const DmaDesc* p2 = d2 ? &dd2 : nullptr;
+  switch (cfg % DMA_PARTS) {
+    case 0: launched = dma_launch_part<0>(cfg, dd, s, p2); break;
+    case 1: launched = dma_launch_part<1>(cfg, dd, s, p2); break;
+    case 2: launched = dma_launch_part<2>(cfg, dd, s, p2); break;
+    default: launched = dma_launch_part<3>(cfg, dd, s, p2); break;
+  }
+  if (!launched) return fail(RTENHIP_INVALID_VALUE, d2 ? "DMA config has no dual instance" : "unknown DMA config");
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

@@ -94,9 +94,18 @@ __device__ __forceinline__ float f4_at(const float4& v, int j) {
 
 // One block computes a BM x BN tile with WAVES_M x WAVES_N waves, each owning
 // a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 32x32 MFMA accumulators.
+//
+// DUAL (d.dual): two GEMMs over the same output tile, summed in the
+// epilogue -- ResNet's conv3 + downsample pair, y = act((W3·h + b3) + (Wd·x
+// + bd)).  Segment 1 (d2: the downsample) runs its whole K fold first and
+// keeps the folded value (bias included) in registers; segment 2 (d: conv3)
+// then runs its own K loop and adds it where the unfused graph adds the
+// residual: the same per-element operations as the two convs and the Add,
+// without the downsample output's round trip through HBM.
 template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES, int HEAD_,
-          bool MULTI_KB, bool BVEC>
-__global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles_m, int tiles_n) {
+          bool MULTI_KB, bool BVEC, bool DUAL = false>
+__global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d2, int tiles_m, int tiles_n) {
+  static_assert(!DUAL || (MULTI_KB && !BVEC), "dual GEMMs fold through the multi-block path, 4-byte B copies");
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int NW = NT / 64;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -153,7 +162,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
 
   // One work item: output tile wg (kb_split < 0), or K block kb_split of split
   // tile split_idx (wg = n_full + split_idx).
-  auto process = [&](const KDesc& d, const int wg, const int kb_split, const int split_idx) __attribute__((always_inline)) {
+  // Dual: segment 1's folded values, carried into segment 2's epilogue.
+  f32x16 carry[DUAL ? MI : 1][DUAL ? NI : 1];
+  // mode 0: one GEMM; 1: dual segment 1 (fold into carry, no epilogue);
+  // 2: dual segment 2 (epilogue adds carry).
+  auto process = [&](const KDesc& d, const int wg, const int kb_split, const int split_idx, const int mode) __attribute__((always_inline)) {
   // Lane-derived values are recomputed per item: hoisted out of the item loop
   // they would stay live across it and spill.
   int tid = tid_o;
@@ -614,7 +627,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
   } else {
     // K > DKC: block 0 is peeled so the bias/beta fold sits outside the loop.
     static_assert(TPB % 2 == 0, "register-set parity across K blocks");
-    run(0, TPB);
+    run(0, DUAL ? min(TPB, tiles_k) : TPB);  // (only a dual segment can have K <= DKC here)
 #pragma unroll
     for (int mi = 0; mi < MI; mi++)
 #pragma unroll
@@ -635,6 +648,15 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     }
   }
 
+  if constexpr (DUAL) {
+    if (mode == 1) {
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++) carry[mi][ni] = sum[mi][ni];
+      return;
+    }
+  }
   if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_kend = __builtin_amdgcn_s_memrealtime();
   // ---- epilogue ----
   auto apply_act = [&](float x) __attribute__((always_inline)) {
@@ -708,6 +730,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
           if (!bias_late && d.bias) first_block(v, acc[mi][ni], mi, ni);
         } else {
           first_block(v, acc[mi][ni], mi, ni, !bias_late);
+        }
+        if constexpr (DUAL) {
+          // (the bias is in v already: MULTI_KB; no column bias or residual)
+#pragma unroll
+          for (int j = 0; j < 16; j++) v[j] = __fadd_rn(v[j], carry[mi][ni][j]);
         }
 #pragma unroll
         for (int j = 0; j < 16; j++) slot[((j & 3) + 8 * (j >> 2) + 4 * half) * 32 + l32] = v[j];
@@ -801,6 +828,10 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
       } else {
         first_block(v, acc[mi][ni], mi, ni, !bias_late);
       }
+      if constexpr (DUAL) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) v[j] = __fadd_rn(v[j], carry[mi][ni][j]);
+      }
 #pragma unroll
       for (int j = 0; j < 16; j++) {
         const int ml = lrow(mi, j);
@@ -878,7 +909,14 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, int tiles
     // across it, they spill).
     const KDesc* dp = (const KDesc*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(dp));
-    process(*dp, wg, kbs, si);
+    if constexpr (DUAL) {
+      process(dp[1], wg, -1, -1, 1);  // d2 (the second kernel argument): segment 1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // segment 1's LDS stages are free
+      process(dp[0], wg, -1, -1, 2);
+    } else {
+      process(*dp, wg, kbs, si, 0);
+    }
     if (!persistent) break;
     // Every wave is done with this item's LDS before the next item's DMAs.
     __syncthreads();
@@ -918,9 +956,11 @@ static void persistent_shape(Kern kern, int nt, int static_lds, int want_k, int&
   grid = k * cus;
 }
 
-template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES, int HD, bool MKB, bool BV>
-static void launch_dma_variant(const DmaDesc& d, int tiles_m, int tiles_n, hipStream_t s) {
-  auto kern = gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, MKB, BV>;
+template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES, int HD, bool MKB, bool BV,
+          bool DUAL = false>
+static void launch_dma_variant(const DmaDesc& d, int tiles_m, int tiles_n, hipStream_t s,
+                               const DmaDesc* d2 = nullptr) {
+  auto kern = gemm_dma_kernel<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, MKB, BV, DUAL>;
   const int items = d.n_full + d.split_tiles * d.nkb;
   int grid = items;
   size_t pad = 0;
@@ -929,25 +969,39 @@ static void launch_dma_variant(const DmaDesc& d, int tiles_m, int tiles_n, hipSt
     persistent_shape(kern, NT, static_lds, d.persist_k, grid, pad);
     if (items < grid) grid = items;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), pad, s, d, tiles_m, tiles_n);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), pad, s, d, d2 ? *d2 : d, tiles_m, tiles_n);
+}
+
+// Configurations with a dual-GEMM instance (64x64 tiles, 4 waves).
+template <int NT, int BM, int BN, int BK, int WM_, int WN_>
+constexpr bool dma_dual_ok() {
+  return NT == 256 && BM == 64 && BN == 64;
 }
 
 template <int NT, int BM, int BN, int BK, int WM_, int WN_, int MINW, int STAGES, int HD>
-static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
+static bool launch_dma_cfg(const DmaDesc& d, hipStream_t s, const DmaDesc* d2) {
   const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
+  if (d2) {
+    if constexpr (dma_dual_ok<NT, BM, BN, BK, WM_, WN_>()) {
+      launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, false, true>(d, tiles_m, tiles_n, s, d2);
+      return true;
+    }
+    return false;
+  }
   if constexpr (dma_bvec_ok<NT, BM, BN, BK, WM_, WN_>()) {
     if (d.bvec) {
       if (d.K > DKC)
         launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, true>(d, tiles_m, tiles_n, s);
       else
         launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, false, true>(d, tiles_m, tiles_n, s);
-      return;
+      return true;
     }
   }
   if (d.K > DKC)
     launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, false>(d, tiles_m, tiles_n, s);
   else
     launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, false, false>(d, tiles_m, tiles_n, s);
+  return true;
 }
 
 // DMA tile configurations:
@@ -990,13 +1044,12 @@ static void launch_dma_cfg(const DmaDesc& d, hipStream_t s) {
 // (cfg % DMA_PARTS == PART; each gemm_dma_p*.hip instantiates one part).
 constexpr int DMA_PARTS = 4;
 template <int PART>
-bool dma_launch_part(int cfg, const DmaDesc& d, hipStream_t s) {
+bool dma_launch_part(int cfg, const DmaDesc& d, hipStream_t s, const DmaDesc* d2) {
   switch (cfg) {
 #define RTENHIP_DMA_PART_CASE(id, NT, BM, BN, BK, WMW, WNW, MINW, ST, HD) \
   case id:                                                              \
     if constexpr ((id) % DMA_PARTS == PART) {                            \
-      launch_dma_cfg<NT, BM, BN, BK, WMW, WNW, MINW, ST, HD>(d, s);      \
-      return true;                                                      \
+      return launch_dma_cfg<NT, BM, BN, BK, WMW, WNW, MINW, ST, HD>(d, s, d2); \
     } else {                                                            \
       return false;                                                     \
     }
@@ -1006,9 +1059,9 @@ bool dma_launch_part(int cfg, const DmaDesc& d, hipStream_t s) {
       return false;
   }
 }
-extern template bool dma_launch_part<0>(int, const DmaDesc&, hipStream_t);
-extern template bool dma_launch_part<1>(int, const DmaDesc&, hipStream_t);
-extern template bool dma_launch_part<2>(int, const DmaDesc&, hipStream_t);
-extern template bool dma_launch_part<3>(int, const DmaDesc&, hipStream_t);
+extern template bool dma_launch_part<0>(int, const DmaDesc&, hipStream_t, const DmaDesc*);
+extern template bool dma_launch_part<1>(int, const DmaDesc&, hipStream_t, const DmaDesc*);
+extern template bool dma_launch_part<2>(int, const DmaDesc&, hipStream_t, const DmaDesc*);
+extern template bool dma_launch_part<3>(int, const DmaDesc&, hipStream_t, const DmaDesc*);
 
 }  // namespace rtenhip

@@ -3,5 +3,5 @@
 #include "gemm_dma_kernel.h"
 
 namespace rtenhip {
-template bool dma_launch_part<0>(int, const DmaDesc&, hipStream_t);
+template bool dma_launch_part<0>(int, const DmaDesc&, hipStream_t, const DmaDesc*);
 }  // namespace rtenhip

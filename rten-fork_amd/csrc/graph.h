@@ -195,6 +195,20 @@ struct Plan {
   // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
   // the expand's input value, which the depthwise op then reads.
   std::map<int, int> expand_fused;
+  // ResNet's conv3 + downsample pairs: conv3 op -> downsample op (its fused
+  // residual's producer, read by nothing else).  On the first run conv3 times
+  // the dual GEMM (gemm_dma_kernel DUAL, both convs in one launch) against
+  // the two launches as tuned; when it wins (dual_on) the downsample op is
+  // skipped and conv3 computes both.
+  std::map<int, int> conv_dual;
+  struct DualExec {
+    int cfg = -1;
+    float* pk3 = nullptr;  // conv3 / downsample weights packed for cfg
+    float* pkd = nullptr;
+    int persist = 0;
+  };
+  std::map<int, DualExec> dual_on;   // conv3 op -> its dual launch
+  std::set<int> dual_skip;           // downsample ops computed by their conv3
   float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
   int64_t mm_pack_floats = 0;
   // What mm_pack holds during a run: the A value it was packed from (value
@@ -312,6 +326,9 @@ struct Graph {
                  int out_dtype, HostVal& out, rtenhip_status& st);
   rtenhip_status exec_data_op(Plan& p, int op_id, bool& handled);
   rtenhip_status exec_conv_dma(Plan& p, int op_id, ConvExec& ce);
+  // conv3 of a Plan::conv_dual pair: the dual launch, or (first run) the
+  // choice between it and the unfused pair.
+  rtenhip_status exec_conv_dual(Plan& p, int op_id, bool& handled);
   void conv_io_args(Plan& p, int op_id, ConvDmaArgs& a);
   rtenhip_status build_chains(Plan& p);
   rtenhip_status exec_chain(Plan& p, ConvChain& c);

@@ -58,6 +58,7 @@ rtenhip_status Graph::build_chains(Plan& p) {
     const ConvExec& ce = it->second;
     if (ce.fc || ce.cfg < 0 || ce.cfg >= kPwCfgBase || ce.g.groups != 1) return false;
     if (p.expand_fused.count(op) || p.conv_unfused.count(op)) return false;
+    if (p.dual_on.count(op) || p.dual_skip.count(op)) return false;
     const Node& n = nodes[op];
     const ConvPlan& g = ce.g;
     const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];

@@ -558,3 +558,63 @@ def test_layernorm_packed_a_bitexact(rh, monkeypatch, pk_out):
         for i, name in enumerate(m.outputs):
             got = out[i].cpu().numpy()
             assert _bits_equal(got, res[name]), f"run {r} output {i}: max abs {np.abs(got - res[name]).max():.3g}"
+
+
+# conv3 + downsample pairs as one dual DMA GEMM (Plan::conv_dual):
+# (N, C_in, H, W, C_mid, C_out, stride)
+DUAL_BLOCKS = [
+    (2, 64, 20, 20, 64, 256, 1),     # layer1.0 shape family, K = 64 + 64
+    (2, 256, 18, 18, 128, 512, 2),   # layer2.0: strided downsample, K = 128 + 256
+    (1, 512, 9, 9, 256, 1024, 2),    # layer3.0: K = 256 + 512 (downsample folds 2 KC blocks)
+    (1, 96, 7, 11, 48, 136, 1),      # ragged M (136), K not a multiple of 16, N = 77
+]
+
+
+@pytest.mark.parametrize("case", DUAL_BLOCKS, ids=lambda c: "x".join(map(str, c)))
+@pytest.mark.parametrize("mode", ["force", "off"])
+def test_bottleneck_dual_gemm_bitexact(rh, monkeypatch, case, mode):
+    """ResNet bottleneck with a downsample branch: relu(conv3(h) + b3 +
+    downsample(x)) with conv3 and the downsample in one dual GEMM launch
+    (RTENHIP_DUAL=1 forces it; the default takes it when faster) or apart
+    (RTENHIP_NO_DUAL=1).  Bit-exact against the oracle, eager and replayed."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, C, H, W, Cm, Co, s = case
+    monkeypatch.delenv("RTENHIP_DUAL", raising=False)
+    monkeypatch.delenv("RTENHIP_NO_DUAL", raising=False)
+    if mode == "force":
+        monkeypatch.setenv("RTENHIP_DUAL", "1")
+    else:
+        monkeypatch.setenv("RTENHIP_NO_DUAL", "1")
+    rng = np.random.default_rng(C + Cm + Co)
+    m = ModelSpec("block")
+    x = m.value("x")
+    m.inputs = ["x"]
+
+    def conv(v, ci, co, k, st, name, pad):
+        w = m.const(name + ".w", rng.uniform(-0.3, 0.3, (co, ci, k, k)).astype(np.float32))
+        b = m.const(name + ".b", rng.uniform(-0.1, 0.1, (co,)).astype(np.float32))
+        return m.op("Conv", [v, w, b], {"pads": [pad] * 4, "strides": [st, st]}, name=name)
+
+    h = m.op("Relu", [conv(x, C, Cm, 1, 1, "c1", 0)])
+    h = m.op("Relu", [conv(h, Cm, Cm, 3, s, "c2", 1)])
+    y = conv(h, Cm, Co, 1, 1, "c3", 0)
+    d = conv(x, C, Co, 1, s, "ds", 0)
+    m.outputs = [m.op("Relu", [m.op("Add", [y, d])])]
+    ins = {"x": rng.uniform(-1, 1, (N, C, H, W)).astype(np.float32)}
+    exp = graph_runner.run(m, ins)[m.outputs[0]]
+    g = m.to_graph()
+    xd = torch.from_numpy(ins["x"]).cuda()
+    out = None
+    for r in range(3):  # eager (tuning + the dual decision), capture, replay
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        got = out[0].cpu().numpy()
+        assert _bits_equal(got, exp), f"run {r}: max abs {np.abs(got - exp).max():.3g}"
+    g.set_timing(True)
+    g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    rep = g.timing_report()
+    assert ("Conv(dual)" in rep) == (mode == "force"), rep
