@@ -2353,7 +2353,9 @@ rtenhip_status Graph::exec_conv_dual(Plan& p, int op_id, bool& handled) {
   // DMA path this run: the normal conv3 path.
   if (getenv("RTENHIP_DUAL_DEBUG"))
     fprintf(stderr, "dual %s: c3.cfg %d ds.cfg %d capture %d\n", nodes[op_id].name.c_str(), c3.cfg, cd.cfg, (int)cs);
-  if (c3.cfg >= 0 || cd.cfg < 0 || !autotune || cs != hipStreamCaptureStatusNone) return RTENHIP_OK;
+  // (A forced latency / VALU variant keeps every conv on it.)
+  if (c3.cfg >= 0 || cd.cfg < 0 || !autotune || cs != hipStreamCaptureStatusNone || lat_mode > 0 || pw_valu_mode > 0)
+    return RTENHIP_OK;
 
   // First (eager) run: conv3 tunes and runs as usual (the downsample already
   // ran, tuned), then the unfused pair is timed against the dual candidates.

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/big; mkdir -p $O
 export RTEN_NUM_THREADS=8
-RTENHIP_DUAL_DEBUG=1 timeout -k 10 300 python -u -m pytest -q -s --timeout 200 --timeout-method thread tests/test_model_gpu.py -k "dual" > $O/dual_tests.log 2>&1
+RTENHIP_DUAL_DEBUG=1 timeout -k 10 300 python -u -m pytest -q -s --timeout 200 --timeout-method thread tests/test_model_gpu.py -k "dual or lat" > $O/dual_tests.log 2>&1
 echo "dual tests rc=$?"; grep -E "^dual|passed|failed|Error" $O/dual_tests.log | head -40
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu --deselect tests/test_full_size_gpu.py -k "not dual" > $O/suite.log 2>&1 \
   || { echo "gpu suite failed"; tail -40 $O/suite.log; exit 1; }
