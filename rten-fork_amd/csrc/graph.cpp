@@ -2766,7 +2766,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         auto ci = plan->chain_of.find(plan->ops[i]);
         if (ci != plan->chain_of.end() && plan->chains[ci->second].use)
           key = plan->chains[ci->second].ops[0] == plan->ops[i] ? "ConvChain" : "Conv(chained)";
-        if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in dual)";
+        if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
         tot[key].first += ms;
         tot[key].second++;
