@@ -17,8 +17,11 @@
 // once at plan time so one k's weights are contiguous), packed f32 FMAs on
 // pixel pairs.  Outputs are 16-byte stores, 1 KB per wave-instruction.
 // Passes over further channel chunks re-read x from L2.
+#include <algorithm>
+
 #include "common.h"
 #include "ctx.h"
+#include "fastdiv_dev.h"
 #include "vecmath.h"
 
 // Timing-experiment builds only (build_pw_exp.sh, never shipped): 1 = stores
@@ -270,6 +273,151 @@ __global__ __launch_bounds__(256) void conv_direct_valu_kernel(const float* __re
   }
 }
 
+// The same direct conv with the block's input rows staged in LDS (variant mc
+// + 100; MobileNetV2's stem: 3 channels, 3x3, stride 2, pad 1).  A block owns
+// TR output rows x the whole output width of one image for all channel
+// chunks; its C x R input rows (R = (TR - 1) * SW + kh) are copied into LDS
+// once, zero-filled where the window leaves the image, by coalesced 4-byte
+// loads all in flight together (no per-channel round trips, no padded copy of
+// the input).  LDS row layout: position j holds input column j - 4, so a
+// lane's 4 outputs read their window as three aligned 16-byte LDS reads.
+// Same chain order k = (c, ky, kx) and the same fma(w, 0, acc) at padding
+// positions as conv_direct_valu_kernel, so the two are bit-identical.
+constexpr int kDirLdsQ = 52;  // staged floats per thread: 52 KB of LDS, three blocks per CU
+struct DirLdsDesc {
+  int TR, R, LROW, tiles_y;
+  FastDiv fdLROW, fdR;
+};
+
+template <int MC, int SW, int PL>
+__global__ __launch_bounds__(256) void conv_direct_lds_kernel(const float* __restrict__ x,
+                                                              const float* __restrict__ wt,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ residual,
+                                                              float* __restrict__ y, DirDesc d, DirLdsDesc e) {
+  extern __shared__ float4 dir_lds4[];
+  float* lds = reinterpret_cast<float*>(dir_lds4);
+  const int tid = threadIdx.x;
+  const int img = (int)blockIdx.x / e.tiles_y;
+  const int oy0 = ((int)blockIdx.x - img * e.tiles_y) * e.TR;
+  const int64_t HW = (int64_t)d.H * d.W;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)(d.x_elems * 4), 0x00020000);
+  const uint32_t img_off = (uint32_t)img * (uint32_t)d.C * (uint32_t)HW * 4u;
+  const int iy0 = oy0 * SW - d.pt;
+  const int total = d.C * e.R * e.LROW;
+  // Stage: element i = (c * R + r) * LROW + j <- x[img][c][iy0 + r][j - 4].
+  float v[kDirLdsQ];
+#pragma unroll
+  for (int q = 0; q < kDirLdsQ; q++) {
+    const int i = tid + 256 * q;
+    const int cr = fdiv(i, e.fdLROW);
+    const int j = i - cr * e.LROW;
+    const int c = fdiv(cr, e.fdR);
+    const int iy = iy0 + cr - c * e.R, ix = j - 4;
+    const bool ok = i < total && iy >= 0 && iy < d.H && ix >= 0 && ix < d.W;
+    const uint32_t off = ok ? img_off + (uint32_t)(c * (int)HW + iy * d.W + ix) * 4u : 0x80000000u;
+    v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0));
+  }
+#pragma unroll
+  for (int q = 0; q < kDirLdsQ; q++)
+    if (tid + 256 * q < total) lds[tid + 256 * q] = v[q];
+  __syncthreads();
+
+  const int tr = tid / d.OW4, t = tid - tr * d.OW4;
+  const int oy = oy0 + tr;
+  if (tr >= e.TR || oy >= d.OH) return;
+  // Window of output column 4t + i, tap kx: LDS position SW * (4t + i) + kx
+  // + 4 - PL = base + o + SW * i + kx.
+  constexpr int o = (4 - PL) & 3;
+  const int base = SW * 4 * t + 4 - PL - o;
+  const int nchunk = (d.M + MC - 1) / MC;
+  const int64_t OP = (int64_t)d.OH * d.OW4 * 4;
+  for (int ch = 0; ch < nchunk; ch++) {
+    const int o0 = ch * MC;
+    f32x2 acc[MC][2];
+#pragma unroll
+    for (int m = 0; m < MC; m++) acc[m][0] = acc[m][1] = (f32x2){0.f, 0.f};
+    // (Weights as scalar operands: staged in LDS and read as broadcast
+    // 16-byte loads instead, the stem conv measured 0.104 -> 0.153 ms.)
+    const float* __restrict__ wk = wt + o0;
+    int k = 0;
+    for (int c = 0; c < d.C; c++) {
+      // (ky not unrolled: 160 VGPRs, three waves per SIMD)
+      for (int ky = 0; ky < d.kh; ky++, k += 3) {
+        // (LROW and base are multiples of 4: 16-byte reads)
+        const float4* rp = dir_lds4 + (((c * e.R + tr * SW + ky) * e.LROW + base) >> 2);
+        const float4 s0 = rp[0], s1 = rp[1], s2 = rp[2];
+        const float seg[12] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w, s2.x, s2.y, s2.z, s2.w};
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++) {
+          const f32x2 xa = {seg[o + kx], seg[o + SW + kx]}, xb = {seg[o + 2 * SW + kx], seg[o + 3 * SW + kx]};
+          const float* __restrict__ wr = wk + (k + kx) * d.Mpad;
+#pragma unroll
+          for (int m = 0; m < MC; m++) {
+            const f32x2 wv = {wr[m], wr[m]};
+            acc[m][0] = __builtin_elementwise_fma(wv, xa, acc[m][0]);
+            acc[m][1] = __builtin_elementwise_fma(wv, xb, acc[m][1]);
+          }
+        }
+      }
+    }
+    const int64_t pix = (int64_t)oy * d.OW4 * 4 + 4 * t;
+    float* __restrict__ yp = y + ((int64_t)img * d.M + o0) * OP + pix;
+    const float* __restrict__ rq = residual ? residual + ((int64_t)img * d.M + o0) * OP + pix : nullptr;
+    const int olim = d.M - 1 - o0;
+#pragma unroll
+    for (int m = 0; m < MC; m++) {
+      if (m > olim) continue;
+      float4 r = make_float4(acc[m][0].x, acc[m][0].y, acc[m][1].x, acc[m][1].y);
+      if (bias) {
+        const float b = bias[o0 + m];
+        r.x = __fadd_rn(r.x, b);
+        r.y = __fadd_rn(r.y, b);
+        r.z = __fadd_rn(r.z, b);
+        r.w = __fadd_rn(r.w, b);
+      }
+      if (rq) {
+        const float4 q = *(const float4*)(rq + (int64_t)m * OP);
+        r.x = __fadd_rn(r.x, q.x);
+        r.y = __fadd_rn(r.y, q.y);
+        r.z = __fadd_rn(r.z, q.z);
+        r.w = __fadd_rn(r.w, q.w);
+      }
+      r.x = pw_act(r.x, d.act, d.lo, d.hi);
+      r.y = pw_act(r.y, d.act, d.lo, d.hi);
+      r.z = pw_act(r.z, d.act, d.lo, d.hi);
+      r.w = pw_act(r.w, d.act, d.lo, d.hi);
+      if (RTENHIP_PW_EXPERIMENT != 1 || r.x == 1234.5f) *(float4*)(yp + (int64_t)m * OP) = r;
+    }
+  }
+}
+
+// Rows per block of the LDS-staged direct conv (0: not eligible).
+static DirLdsDesc dir_lds_plan(int64_t C, int64_t kh, int64_t sh, int64_t oh, int64_t ow, int64_t M) {
+  DirLdsDesc e{};
+  const int64_t ow4 = ow / 4;
+  (void)M;
+  if (ow4 < 1 || ow4 > 256) return e;
+  const int64_t lrow = sh * 4 * ow4 + 12;
+  int64_t tr = std::min<int64_t>(oh, 256 / ow4);
+  auto rows = [&](int64_t t) { return C * ((t - 1) * sh + kh) * lrow; };
+  while (tr >= 1 && rows(tr) > 256 * kDirLdsQ) tr--;
+  if (tr < 1) return e;
+  e.TR = (int)tr;
+  e.R = (int)((tr - 1) * sh + kh);
+  e.LROW = (int)lrow;
+  e.tiles_y = (int)((oh + tr - 1) / tr);
+  e.fdLROW = make_fastdiv((uint32_t)lrow);
+  e.fdR = make_fastdiv((uint32_t)e.R);
+  return e;
+}
+
+bool conv_direct_lds_eligible(const ConvPlan& g, bool padded_out) {
+  return conv_direct_valu_eligible(g, padded_out) && g.kh <= 3 && g.dh == 1 && g.sh == g.sw &&
+         (g.pads[1] == 0 || g.pads[1] == 1) && dir_lds_plan(g.C, g.kh, g.sh, g.oh, g.ow, g.O).TR > 0;
+}
+
 // w [M][K] -> wt [K][Mpad], zero columns M..Mpad-1
 __global__ void transpose_weights_kernel(const float* __restrict__ w, float* __restrict__ wt, int M,
                                          int Mpad, int K) {
@@ -310,10 +458,18 @@ bool pw_variant_ok(int variant, int64_t K) {
 }
 
 rtenhip_status conv_direct_valu(const ConvDmaArgs& a, int mc, hipStream_t s) {
+  const bool lds = mc >= 100;
+  if (lds) mc -= 100;
   if (a.groups != 1 || a.kw != 3 || a.dw != 1 || (a.sw != 1 && a.sw != 2) || a.ow % 4 ||
       a.C * a.kh * a.kw > 64 || (uintptr_t)a.y % 16 || (a.residual && (uintptr_t)a.residual % 16) ||
       !a.x_unpadded || (mc != 16 && mc != 32))
     return fail(RTENHIP_INVALID_VALUE, "direct VALU conv: unsupported layout");
+  DirLdsDesc e{};
+  if (lds) {
+    e = dir_lds_plan(a.C, a.kh, a.sh, a.oh, a.ow, a.O);
+    if (e.TR == 0 || a.kh > 3 || a.dh != 1 || a.sh != a.sw || (a.pad_l != 0 && a.pad_l != 1))
+      return fail(RTENHIP_INVALID_VALUE, "direct VALU conv (LDS rows): unsupported layout");
+  }
   DirDesc d{};
   d.C = (int)a.C;
   d.x_elems = a.N * a.C * a.H * a.W;
@@ -332,6 +488,27 @@ rtenhip_status conv_direct_valu(const ConvDmaArgs& a, int mc, hipStream_t s) {
   d.act = a.act;
   d.lo = a.lo;
   d.hi = a.hi;
+  if (lds) {
+    const unsigned blocks = (unsigned)(a.N * e.tiles_y);
+    const size_t bytes = (size_t)a.C * e.R * e.LROW * 4;
+#define DIR_LDS_LAUNCH(MC, SW, PL)                                                                      \
+  conv_direct_lds_kernel<MC, SW, PL><<<blocks, 256, bytes, s>>>(a.x_unpadded, a.packed_w, a.bias, a.residual, \
+                                                                a.y, d, e)
+#define DIR_LDS_PL(MC, SW) \
+  if (a.pad_l == 1) { DIR_LDS_LAUNCH(MC, SW, 1); } else { DIR_LDS_LAUNCH(MC, SW, 0); }
+#define DIR_LDS_SW(MC) \
+  if (a.sw == 2) { DIR_LDS_PL(MC, 2); } else { DIR_LDS_PL(MC, 1); }
+    if (mc == 32) {
+      DIR_LDS_SW(32);
+    } else {
+      DIR_LDS_SW(16);
+    }
+#undef DIR_LDS_SW
+#undef DIR_LDS_PL
+#undef DIR_LDS_LAUNCH
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   const int64_t gx = (d.groups4 + 255) / 256;
   const int nchunk = (d.M + mc - 1) / mc;
   int gy = 1;

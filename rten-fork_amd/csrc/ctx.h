@@ -108,8 +108,10 @@ rtenhip_status pack_pw_weights(const float* w, int64_t M, int64_t K, float* wt, 
 // KX = 0 streams x per pass, KX = 16 / 32 holds a K <= KX column in VGPRs.
 bool pw_variant_ok(int variant, int64_t K);
 // Direct VALU conv (3-wide kernels, stride 1 or 2, K = C*kh*kw <= 64, OW % 4 == 0,
-// unpadded output), variant kPwDirect + mc, mc in {16, 32}.
+// unpadded output), variant kPwDirect + mc, mc in {16, 32}; mc + 100 stages
+// the block's input rows in LDS (kh <= 3, dh = 1, sh = sw, pad_l <= 1).
 bool conv_direct_valu_eligible(const ConvPlan& g, bool padded_out);
+bool conv_direct_lds_eligible(const ConvPlan& g, bool padded_out);
 rtenhip_status conv_direct_valu(const ConvDmaArgs& a, int mc, hipStream_t s);
 constexpr int kPwDirect = 300;
 rtenhip_status conv_pw_valu(const ConvDmaArgs& a, int variant, hipStream_t s);

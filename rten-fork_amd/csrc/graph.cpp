@@ -2058,6 +2058,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
                      ((uintptr_t)a.xin | (uintptr_t)a.y) % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
   const bool direct_ok = pin == p.padded.end() && conv_direct_valu_eligible(g, pout != p.padded.end()) &&
                          (uintptr_t)a.y % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
+  const bool direct_lds_ok = direct_ok && conv_direct_lds_eligible(g, pout != p.padded.end());
   auto launch = [&]() -> rtenhip_status {
     if (a.cfg >= kPwCfgBase + kPwDirect) return conv_direct_valu(a, a.cfg - kPwCfgBase - kPwDirect, s);
     return a.cfg >= kPwCfgBase ? conv_pw_valu(a, a.cfg - kPwCfgBase, s) : conv_dma(ctx, a);
@@ -2107,7 +2108,8 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
     const bool pw_forced = (pw_ok && pw_valu_mode > 0 && pw_valu_mode < kPwDirect && pw_variant_ok(pw_valu_mode, K)) ||
-                           (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32));
+                           (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32)) ||
+                           (direct_lds_ok && (pw_valu_mode == kPwDirect + 116 || pw_valu_mode == kPwDirect + 132));
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
     const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode);
     if (lat_forced) {
@@ -2244,7 +2246,8 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           for (Cand& c : cands)
             if (c.cfg < kPwCfgBase) c.ms += pad_ms;
         }
-        for (int mc : {16, 32}) {
+        for (int mc : {16, 32, 116, 132}) {
+          if (mc >= 100 && !direct_lds_ok) continue;
           const int cfg = kPwCfgBase + kPwDirect + mc;
           float* pk = nullptr;
           RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));

@@ -129,10 +129,20 @@ DIRECT_CASES = [
     (1, 4, 12, 12, 40, 3, 1, [1, 1, 1, 1], "none"),  # stride 1, partial chunk
     (2, 2, 9, 12, 16, 1, 1, [0, 1, 0, 1], "add"),   # 1x3 kernel, residual
     (1, 7, 10, 14, 8, 3, 2, [0, 2, 1, 1], "clip"),  # asymmetric pads, K = 63
+    (2, 3, 224, 224, 32, 3, 2, [1, 1, 1, 1], "clip"),  # MobileNetV2 stem, full width (LDS rows: 8-row tiles)
+    (1, 3, 62, 40, 24, 2, 2, [0, 0, 1, 1], "relu"),  # no left pad, stride 2, partial last row tile
+    (1, 5, 20, 24, 20, 3, 1, [1, 0, 1, 2], "add"),   # no left pad, stride 1
 ]
 
 
-@pytest.mark.parametrize("mode", ["316", "332"])
+def _direct_lds_eligible(case):
+    N, C, H, W, O, kh, st, pads, tail = case
+    return kh <= 3 and pads[1] <= 1
+
+
+# 316 / 332: one lane per 4 outputs reading x directly; 416 / 432: the same
+# with the block's input rows staged in LDS (conv_direct_lds_kernel).
+@pytest.mark.parametrize("mode", ["316", "332", "416", "432"])
 @pytest.mark.parametrize("case", DIRECT_CASES, ids=lambda c: "x".join(map(str, c[:6])) + f"s{c[6]}-{c[8]}")
 def test_direct_valu_bitexact(rh, monkeypatch, mode, case):
     import torch
@@ -140,6 +150,8 @@ def test_direct_valu_bitexact(rh, monkeypatch, mode, case):
     from rten_hip.graph import ModelSpec
 
     N, C, H, W, O, kh, st, pads, tail = case
+    if mode.startswith("4") and not _direct_lds_eligible(case):
+        pytest.skip("LDS-row variant needs kh <= 3 and a left pad <= 1")
     monkeypatch.setenv("RTENHIP_PW_VALU", mode)
     rng = np.random.default_rng(C * 17 + O + kh)
     m = ModelSpec("direct")
