@@ -192,6 +192,18 @@ rtenhip_status rtenhip_layer_norm_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x,
 rtenhip_status rtenhip_softmax_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, int64_t axis,
                                    rtenhip_tensor* y);
 
+/* LogSoftmax (src/ops/norm.rs:381-430, log_softmax_in_place); y may alias x.
+ * exp / ln are libm's (Rust f32::exp / f32::ln): computed in f64 and rounded. */
+rtenhip_status rtenhip_log_softmax_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, int64_t axis,
+                                       rtenhip_tensor* y);
+
+/* InstanceNormalization (src/ops/norm.rs:131-241): x is [N, C, ...]; scale and
+ * bias are device arrays of n_channels (must equal C) floats; y may alias x.
+ * The reference's default epsilon is 1e-5. */
+rtenhip_status rtenhip_instance_norm_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, const float* scale,
+                                         const float* bias, int64_t n_channels, float epsilon,
+                                         rtenhip_tensor* y);
+
 /* Unary float ops (src/ops/unary_elementwise.rs; numerics of rten-vecmath). */
 typedef enum {
   RTENHIP_UNARY_RELU = 0,

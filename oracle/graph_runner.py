@@ -86,6 +86,10 @@ def run_op(node, ins):
                             a.get("epsilon", 1e-5))
     if t == "Softmax":
         return O.softmax(x, a.get("axis", -1))
+    if t == "LogSoftmax":
+        return O.log_softmax(x, a.get("axis", -1))
+    if t == "InstanceNormalization":
+        return O.instance_norm(x, ins[1], ins[2], a.get("epsilon", 1e-5))
     if t == "Transpose":
         return np.ascontiguousarray(np.transpose(x, a.get("perm")))
     if t == "Reshape":

@@ -132,6 +132,11 @@ int orc_unary(int op, const float* x, int64_t n, float* out, float p0, float p1)
 
 /* Softmax over `axis` (src/ops/norm.rs:332-448, rten-vecmath softmax.rs). */
 int orc_softmax(const float* x, const int64_t* shape, int ndim, int64_t axis, float* out);
+/* LogSoftmax over `axis` (src/ops/norm.rs:381-430; libm expf / logf). */
+int orc_log_softmax(const float* x, const int64_t* shape, int ndim, int64_t axis, float* out);
+/* InstanceNormalization (src/ops/norm.rs:131-241). */
+int orc_instance_norm(const float* x, const int64_t* shape, int ndim, const float* scale, int64_t n_scale,
+                      const float* bias, int64_t n_bias, float epsilon, float* out);
 
 /* LayerNormalization (src/ops/norm.rs:245-299) for scale/bias of the
  * normalized shape (same trailing dims). bias may be NULL. */

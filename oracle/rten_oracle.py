@@ -290,6 +290,21 @@ def softmax(x, axis=-1):
     return out
 
 
+def log_softmax(x, axis=-1):
+    x = _c(x)
+    out = np.empty_like(x)
+    _check(lib().orc_log_softmax(_f(x), _shape(x.shape), C.c_int(x.ndim), C.c_int64(axis), _f(out)))
+    return out
+
+
+def instance_norm(x, scale, bias, epsilon=1e-5):
+    x, scale, bias = _c(x), _c(scale), _c(bias)
+    out = np.empty_like(x)
+    _check(lib().orc_instance_norm(_f(x), _shape(x.shape), C.c_int(x.ndim), _f(scale), C.c_int64(scale.size),
+                                   _f(bias), C.c_int64(bias.size), C.c_float(epsilon), _f(out)))
+    return out
+
+
 def layer_norm(x, scale, bias=None, axis=-1, epsilon=1e-5):
     x = _c(x)
     out = np.empty_like(x)

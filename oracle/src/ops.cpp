@@ -337,6 +337,56 @@ int orc_batch_norm(const float* x, const int64_t* shape, int ndim, const float* 
   return ORC_OK;
 }
 
+// log_softmax_in_place (src/ops/norm.rs:381-406) over lanes along `axis`
+// (softmax_lanes moves the axis last; the per-lane arithmetic does not depend
+// on where the elements sit).  exp / ln are Rust's f32::exp / f32::ln, i.e.
+// libm expf / logf -- the same functions std::exp / std::log call here.
+int orc_log_softmax(const float* x, const int64_t* shape, int ndim, int64_t axis, float* out) {
+  if (axis < 0) axis += ndim;
+  if (axis < 0 || axis >= ndim) return fail(ORC_INVALID_VALUE, "Axis is invalid");
+  const int64_t len = shape[axis];
+  const int64_t outer = numel(shape, (int)axis), inner = numel(shape + axis + 1, ndim - (int)axis - 1);
+#pragma omp parallel for collapse(2) if (outer * inner > 64)
+  for (int64_t o = 0; o < outer; o++)
+    for (int64_t i = 0; i < inner; i++) {
+      const float* p = x + o * len * inner + i;
+      float* q = out + o * len * inner + i;
+      // slice_max (slice_reductions.rs:16-36): f32::max from f32::MIN
+      float m = -FLT_MAX;
+      for (int64_t k = 0; k < len; k++) m = rust_max(m, p[k * inner]);
+      float s = 0.f;
+      for (int64_t k = 0; k < len; k++) s = s + std::exp(p[k * inner] - m);
+      const float lse = std::log(s);
+      for (int64_t k = 0; k < len; k++) q[k * inner] = (p[k * inner] - m) - lse;
+    }
+  return ORC_OK;
+}
+
+// instance_normalization_in_place (src/ops/norm.rs:144-198).
+int orc_instance_norm(const float* x, const int64_t* shape, int ndim, const float* scale, int64_t n_scale,
+                      const float* bias, int64_t n_bias, float epsilon, float* out) {
+  if (ndim < 2) return fail(ORC_INVALID_VALUE, "expected input with >= 2 dims");
+  const int64_t N = shape[0], C = shape[1], len = numel(shape + 2, ndim - 2);
+  if (n_scale != C) return fail(ORC_INVALID_VALUE, "scale length should match channel count");
+  if (n_bias != C) return fail(ORC_INVALID_VALUE, "bias length should match channel count");
+#pragma omp parallel for collapse(2)
+  for (int64_t n = 0; n < N; n++)
+    for (int64_t c = 0; c < C; c++) {
+      const float* p = x + (n * C + c) * len;
+      float* q = out + (n * C + c) * len;
+      const float mean = slice_sum(p, len) / (float)len;
+      float var = 0.f;  // Iterator::sum: one chain in index order
+      for (int64_t i = 0; i < len; i++) {
+        const float d = p[i] - mean;
+        var = var + d * d;
+      }
+      var = var / (float)len;
+      const float r = scale[c] / std::sqrt(var + epsilon);
+      for (int64_t i = 0; i < len; i++) q[i] = (p[i] - mean) * r + bias[c];
+    }
+  return ORC_OK;
+}
+
 int orc_softmax(const float* x, const int64_t* shape, int ndim, int64_t axis, float* out) {
   if (axis < 0) axis += ndim;
   if (axis < 0 || axis >= ndim) return fail(ORC_INVALID_VALUE, "Axis is invalid");

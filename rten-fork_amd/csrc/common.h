@@ -143,6 +143,12 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
                                 hipStream_t s);
 rtenhip_status launch_softmax(const float* x, float* y, int64_t rows, int64_t len,
                               hipStream_t s);
+// LogSoftmax over the middle axis of [outer, len, inner]; InstanceNorm over the
+// contiguous planes of [N, C, len] (norm.hip).
+rtenhip_status launch_log_softmax(const float* x, float* y, int64_t outer, int64_t len, int64_t inner,
+                                  hipStream_t s);
+rtenhip_status launch_instance_norm(const float* x, float* y, int64_t N, int64_t C, int64_t len,
+                                    const float* scale, const float* bias, float eps, hipStream_t s);
 struct PackedOut;
 // pk: also store y as a MatMul's packed A (packed_a.h); only the rows kernel
 // does (layer_norm_rows_ok), the call fails otherwise.

@@ -514,10 +514,11 @@ rtenhip_status Graph::infer_shapes(int op_id, const std::vector<const Shape*>& i
     outs[0].assign(os, os + on);
   } else {
     // Shape-preserving ops: unary activations, BatchNormalization,
-    // LayerNormalization, Softmax, Identity, Cast.
+    // LayerNormalization, Softmax, Identity, Cast, LogSoftmax,
+    // InstanceNormalization.
     static const std::set<std::string> same = {
         "Relu", "Clip", "Gelu", "Erf", "Sigmoid", "Tanh", "Exp", "Silu", "Sqrt", "BatchNormalization",
-        "LayerNormalization", "Softmax", "Identity", "Cast"};
+        "LayerNormalization", "Softmax", "Identity", "Cast", "LogSoftmax", "InstanceNormalization"};
     if (!same.count(t)) {
       std::string msg = "Unsupported operator type: " + t;
       set_error(RTENHIP_UNSUPPORTED_VALUE, msg);
@@ -1493,6 +1494,16 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
                                   (float)n.attrs.num("epsilon", 1e-5), &y);
   }
   if (t == "Softmax") return rtenhip_softmax_f32(c, &x, (int64_t)n.attrs.num("axis", -1), &y);
+  if (t == "LogSoftmax") return rtenhip_log_softmax_f32(c, &x, (int64_t)n.attrs.num("axis", -1), &y);
+  if (t == "InstanceNormalization") {
+    // instance_normalization_in_place (norm.rs:144-198): rank, then the
+    // scale and bias lengths, then epsilon (None -> 1e-5).
+    if (x.ndim < 2) return fail(RTENHIP_INVALID_VALUE, "expected input with >= 2 dims");
+    const rtenhip_tensor sc = T(n.inputs[1]), bi = T(n.inputs[2]);
+    if (numel(sc) != x.shape[1]) return fail(RTENHIP_INVALID_VALUE, "scale length should match channel count");
+    if (numel(bi) != x.shape[1]) return fail(RTENHIP_INVALID_VALUE, "bias length should match channel count");
+    return rtenhip_instance_norm_f32(c, &x, sc.data, bi.data, x.shape[1], (float)n.attrs.num("epsilon", 1e-5), &y);
+  }
   if (t == "Transpose") {
     auto perm = n.attrs.ints("perm", {});
     if (perm.empty())
@@ -2435,8 +2446,9 @@ rtenhip_status Graph::exec_conv_dual(Plan& p, int op_id, bool& handled) {
     }
     std::sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) { return x.ms < y.ms; });
     // RTENHIP_DUAL=1 (tests): the fastest dual candidate even when the pair
-    // unfused is faster.
-    static const bool force = getenv("RTENHIP_DUAL") && atoi(getenv("RTENHIP_DUAL")) > 0;
+    // unfused is faster.  (Read per decision, not cached per process: tests
+    // flip it between graphs.)
+    const bool force = getenv("RTENHIP_DUAL") && atoi(getenv("RTENHIP_DUAL")) > 0;
     float best = force ? 1e30f : unfused;
     int pick = -1;
     for (size_t i = 0; i < cands.size() && i < 3; i++) {

@@ -216,7 +216,8 @@ void read_op(const std::string& type, uint8_t attrs_type, const Table& a, Attrs&
       out.nums["strides"] = {1, 1};
     }
     if (type == "AveragePool") out.nums["count_include_pad"] = {(double)a.scalar<uint8_t>(4, 0)};
-  } else if (type == "BatchNormalization") {
+  } else if (type == "BatchNormalization" || type == "InstanceNormalization") {
+    // (InstanceNormalization reads BatchNormalizationAttrs, op_registry.rs:556-564)
     need(kBatchNormalizationAttrs);
     out.nums["epsilon"] = {(double)a.scalar<float>(0, 0.f)};
   } else if (type == "Gemm") {
@@ -228,7 +229,8 @@ void read_op(const std::string& type, uint8_t attrs_type, const Table& a, Attrs&
   } else if (type == "Flatten") {
     need(kFlattenAttrs);
     out.nums["axis"] = {(double)a.scalar<int32_t>(0, 0)};
-  } else if (type == "Softmax") {
+  } else if (type == "Softmax" || type == "LogSoftmax") {
+    // (LogSoftmax reads SoftmaxAttrs, op_registry.rs:587)
     need(kSoftmaxAttrs);
     out.nums["axis"] = {(double)a.scalar<int32_t>(0, 0)};
   } else if (type == "LayerNormalization") {

@@ -447,4 +447,130 @@ rtenhip_status launch_reduce_mean_iter(const float* x, float* y, const ReduceDes
   return RTENHIP_OK;
 }
 
+// ---------------------------------------------------------------------------
+// LogSoftmax (log_softmax_in_place, src/ops/norm.rs:381-406) and
+// InstanceNormalization (instance_normalization_in_place, norm.rs:144-198):
+// one wave per lane / plane.  Their folds are serial in index order in the
+// reference (Iterator::fold / sum, slice_sum's chunk fold), so the wave forms
+// 64 terms at a time in parallel and every lane runs the same serial chain
+// over them through v_readlane (no LDS, any length, in place safe).
+// exp / ln are Rust's f32::exp / f32::ln (libm expf / logf, not rten-vecmath):
+// evaluated here in f64 and rounded once, i.e. the correctly rounded value,
+// which libm's expf / logf (< 0.51 ULP) return in all but rare ties.
+
+__device__ __forceinline__ float lane_f(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// acc + t_0 + t_1 + ... + t_{n-1}, t_j held by lane j (n <= 64).
+__device__ __forceinline__ float wave_serial_fold(float acc, float t, int n) {
+  if (n == 64) {
+#pragma unroll
+    for (int j = 0; j < 64; j++) acc = __fadd_rn(acc, lane_f(t, j));
+  } else {
+    for (int j = 0; j < n; j++) acc = __fadd_rn(acc, lane_f(t, j));
+  }
+  return acc;
+}
+
+// Rows: row r = (o, i) with o = r / inner, i = r % inner; element k of the row
+// at o * len * inner + i + k * inner (the axis need not be last: each lane's
+// arithmetic is independent of where its elements sit).
+__global__ __launch_bounds__(256) void log_softmax_kernel(const float* x, float* y, int64_t rows, int len,
+                                                          int64_t inner) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const int64_t o = row / inner, i = row - o * inner;
+  const float* xr = x + o * len * inner + i;
+  float* yr = y + o * len * inner + i;
+  // slice_max: max is exact and order-free on the values it sees (f32::max
+  // ignores NaN like fmaxf), from f32::MIN.
+  float m = -FLT_MAX;
+  for (int k = lane; k < len; k += 64) m = rust_max(m, xr[(int64_t)k * inner]);
+  for (int off = 32; off > 0; off >>= 1) m = rust_max(m, __shfl_xor(m, off));
+  // fold(0., |s, x| s + (x - max).exp())
+  float s = 0.f;
+  for (int k0 = 0; k0 < len; k0 += 64) {
+    const int k = k0 + lane;
+    const float e = k < len ? (float)exp((double)__fsub_rn(xr[(int64_t)k * inner], m)) : 0.f;
+    s = wave_serial_fold(s, e, min(64, len - k0));
+  }
+  const float lse = (float)log((double)s);
+  for (int k = lane; k < len; k += 64) {
+    const int64_t at = (int64_t)k * inner;
+    yr[at] = __fsub_rn(__fsub_rn(xr[at], m), lse);
+  }
+}
+
+rtenhip_status launch_log_softmax(const float* x, float* y, int64_t outer, int64_t len, int64_t inner,
+                                  hipStream_t s) {
+  const int64_t rows = outer * inner;
+  if (rows == 0 || len == 0) return RTENHIP_OK;
+  if (len > INT32_MAX) return fail(RTENHIP_INVALID_VALUE, "LogSoftmax: axis too long");
+  hipLaunchKernelGGL(log_softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, y, rows, (int)len,
+                     inner);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
+// Plane p = (n, c) of len contiguous floats, channel c = p % C.
+__global__ __launch_bounds__(256) void instance_norm_kernel(const float* x, float* y, int64_t planes, int C,
+                                                            int64_t len, const float* __restrict__ scale,
+                                                            const float* __restrict__ bias, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * 4 + wave;
+  if (p >= planes) return;
+  const float* xr = x + p * len;
+  float* yr = y + p * len;
+  const int c = (int)(p % C);
+  // slice_sum (slice_reductions.rs:37-53): 8-element chunks
+  // ((x0+x4)+(x1+x5))+(x2+x6))+(x3+x7), folded in order from 0, then the
+  // tail chunk's own fold from 0.
+  const int64_t nchunks = len / 8;
+  float total = 0.f;
+  for (int64_t c0 = 0; c0 < nchunks; c0 += 64) {
+    const int64_t ck = c0 + lane;
+    float cs = 0.f;
+    if (ck < nchunks) {
+      const float* q = xr + 8 * ck;
+      const float z0 = __fadd_rn(q[0], q[4]), z1 = __fadd_rn(q[1], q[5]);
+      const float z2 = __fadd_rn(q[2], q[6]), z3 = __fadd_rn(q[3], q[7]);
+      cs = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
+    }
+    total = wave_serial_fold(total, cs, (int)min<int64_t>(64, nchunks - c0));
+  }
+  if (nchunks * 8 < len) {
+    const int64_t k = nchunks * 8 + lane;
+    const float t = k < len ? xr[k] : 0.f;
+    total = __fadd_rn(total, wave_serial_fold(0.f, t, (int)(len - nchunks * 8)));
+  }
+  const float mean = __fdiv_rn(total, (float)len);
+  // slice.iter().map(|x| (x - mean)^2).sum() / len: one serial chain.
+  float var = 0.f;
+  for (int64_t k0 = 0; k0 < len; k0 += 64) {
+    const int64_t k = k0 + lane;
+    float d2 = 0.f;
+    if (k < len) {
+      const float d = __fsub_rn(xr[k], mean);
+      d2 = __fmul_rn(d, d);
+    }
+    var = wave_serial_fold(var, d2, (int)min<int64_t>(64, len - k0));
+  }
+  var = __fdiv_rn(var, (float)len);
+  const float r = __fdiv_rn(scale[c], sqrt_rn(__fadd_rn(var, eps)));
+  const float b = bias[c];
+  for (int64_t k = lane; k < len; k += 64) yr[k] = __fadd_rn(__fmul_rn(__fsub_rn(xr[k], mean), r), b);
+}
+
+rtenhip_status launch_instance_norm(const float* x, float* y, int64_t N, int64_t C, int64_t len,
+                                    const float* scale, const float* bias, float eps, hipStream_t s) {
+  const int64_t planes = N * C;
+  if (planes == 0 || len == 0) return RTENHIP_OK;
+  hipLaunchKernelGGL(instance_norm_kernel, dim3((unsigned)((planes + 3) / 4)), dim3(256), 0, s, x, y, planes,
+                     (int)C, len, scale, bias, eps);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 }  // namespace rtenhip

@@ -349,6 +349,43 @@ static int64_t resolve_axis(int64_t axis, int ndim, bool* ok) {
   return axis;
 }
 
+rtenhip_status rtenhip_log_softmax_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, int64_t axis,
+                                       rtenhip_tensor* y) {
+  // LogSoftmax (src/ops/norm.rs:381-430): softmax_lanes' axis move is a
+  // layout change only, so the kernel walks the axis in place with stride
+  // `inner`.
+  Ctx* cx = C_(ctx);
+  if (!x) return fail(RTENHIP_MISSING_INPUTS, "Missing inputs");
+  bool ok;
+  const int64_t ax = resolve_axis(axis, x->ndim, &ok);
+  if (!ok) return fail(RTENHIP_INVALID_VALUE, "Axis is invalid");
+  rtenhip_status st = check_out_shape(y, x->shape, x->ndim);
+  if (st) return st;
+  const float* xd = contiguous(cx, *x, 0, &st);
+  if (st) return st;
+  int64_t outer = 1, inner = 1;
+  for (int i = 0; i < ax; i++) outer *= x->shape[i];
+  for (int i = (int)ax + 1; i < x->ndim; i++) inner *= x->shape[i];
+  return launch_log_softmax(xd, y->data, outer, x->shape[ax], inner, cx->stream);
+}
+
+rtenhip_status rtenhip_instance_norm_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, const float* scale,
+                                         const float* bias, int64_t n_channels, float epsilon,
+                                         rtenhip_tensor* y) {
+  // InstanceNormalization (src/ops/norm.rs:131-198).
+  Ctx* cx = C_(ctx);
+  if (!x || !scale || !bias) return fail(RTENHIP_MISSING_INPUTS, "Missing inputs");
+  if (x->ndim < 2) return fail(RTENHIP_INVALID_VALUE, "expected input with >= 2 dims");
+  if (n_channels != x->shape[1]) return fail(RTENHIP_INVALID_VALUE, "scale length should match channel count");
+  rtenhip_status st = check_out_shape(y, x->shape, x->ndim);
+  if (st) return st;
+  const float* xd = contiguous(cx, *x, 0, &st);
+  if (st) return st;
+  int64_t len = 1;
+  for (int i = 2; i < x->ndim; i++) len *= x->shape[i];
+  return launch_instance_norm(xd, y->data, x->shape[0], x->shape[1], len, scale, bias, epsilon, cx->stream);
+}
+
 rtenhip_status rtenhip_reduce_mean_f32(rtenhip_ctx* ctx, const rtenhip_tensor* x, const int32_t* axes,
                                        int32_t n_axes, int keep_dims, rtenhip_tensor* y) {
   // reduce (src/ops/reduce.rs:225-330) with the MeanReducer (334-353).

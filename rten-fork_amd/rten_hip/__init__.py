@@ -119,7 +119,7 @@ EXPORTED_SYMBOLS = [
     "rtenhip_where_output_shape", "rtenhip_where_f32", "rtenhip_cast_f32_to_i32",
     "rtenhip_cast_i32_to_f32", "rtenhip_graph_add_constant_i32", "rtenhip_graph_run_typed",
     "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts", "rtenhip_reduce_mean_f32",
-    "rtenhip_graph_describe",
+    "rtenhip_graph_describe", "rtenhip_log_softmax_f32", "rtenhip_instance_norm_f32",
 ]
 
 # rtenhip_dtype (sg::DataType order, include/rten_hip.h)
@@ -499,6 +499,29 @@ def softmax(x, axis=-1, out=None, ctx=None):
     xd, yd = describe(x), describe(y)
     check(lib().rtenhip_softmax_f32(C.c_void_p(ctx.ptr), C.byref(xd), C.c_int64(axis),
                                     C.byref(yd)))
+    return y
+
+
+def log_softmax(x, axis=-1, out=None, ctx=None):
+    """LogSoftmax (src/ops/norm.rs:381-430)."""
+    ctx = ctx or default_context()
+    y = out if out is not None else _empty(x.shape, x)
+    xd, yd = describe(x), describe(y)
+    check(lib().rtenhip_log_softmax_f32(C.c_void_p(ctx.ptr), C.byref(xd), C.c_int64(axis), C.byref(yd)))
+    return y
+
+
+def instance_normalization(x, scale, bias, epsilon=None, out=None, ctx=None):
+    """InstanceNormalization (src/ops/norm.rs:131-241); epsilon defaults to 1e-5.
+    scale / bias: contiguous device float tensors of C elements."""
+    ctx = ctx or default_context()
+    y = out if out is not None else _empty(x.shape, x)
+    xd, yd = describe(x), describe(y)
+    if x.dim() >= 2 and scale.numel() == x.shape[1] and bias.numel() != scale.numel():
+        raise OpError(5, "bias length should match channel count")
+    check(lib().rtenhip_instance_norm_f32(C.c_void_p(ctx.ptr), C.byref(xd), C.c_void_p(scale.data_ptr()),
+                                          C.c_void_p(bias.data_ptr()), C.c_int64(scale.numel()),
+                                          C.c_float(1e-5 if epsilon is None else epsilon), C.byref(yd)))
     return y
 
 

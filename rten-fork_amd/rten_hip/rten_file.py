@@ -218,7 +218,7 @@ def _op_attrs(op_type: str, a: dict):
             f.append(("count_include_pad", "bool", int(bool(a.get("count_include_pad", 0)))))
             return ATTRS_AVERAGE_POOL, _T("AveragePoolAttrs", *f)
         return ATTRS_MAX_POOL, _T("MaxPoolAttrs", *f)
-    if op_type == "BatchNormalization":
+    if op_type in ("BatchNormalization", "InstanceNormalization"):
         return ATTRS_BATCH_NORM, _T("BatchNormalizationAttrs", ("epsilon", "f32", float(a.get("epsilon", 1e-5))))
     if op_type == "Gemm":
         return ATTRS_GEMM, _T("GemmAttrs", ("alpha", "f32", float(a.get("alpha", 1.0))),
@@ -227,7 +227,7 @@ def _op_attrs(op_type: str, a: dict):
                               ("transpose_b", "bool", int(bool(a.get("transB", 0)))))
     if op_type == "Flatten":
         return ATTRS_FLATTEN, _T("FlattenAttrs", ("axis", "i32", int(a.get("axis", 1))))
-    if op_type == "Softmax":
+    if op_type in ("Softmax", "LogSoftmax"):
         return ATTRS_SOFTMAX, _T("SoftmaxAttrs", ("axis", "i32", int(a.get("axis", -1))))
     if op_type == "LayerNormalization":
         return ATTRS_LAYER_NORM, _T("LayerNormalizationAttrs", ("axis", "i32", int(a.get("axis", -1))),

@@ -333,6 +333,78 @@ def test_layer_norm_bitexact(rh, oracle, shape):
                 oracle.layer_norm(x, sc, bi, -1, 1e-12), f"layernorm {shape}")
 
 
+@pytest.mark.parametrize("shape,axis", [((6,), 0), ((2, 3), 1), ((2, 3), 0), ((64, 1000), -1), ((3, 4097), 1),
+                                        ((4, 37, 5), 1), ((2, 3, 130), 0), ((1, 1), 0)])
+def test_log_softmax(rh, oracle, shape, axis):
+    """LogSoftmax vs the oracle (libm expf / logf, as Rust's f32::exp / ln).
+    The GPU forms exp and ln in f64 rounded once (the correctly rounded
+    values); libm's expf / logf differ from those in ~0.05% of arguments by
+    1 ULP, so this is a tolerance check (well inside north_star's 1e-4 rel):
+    |d| <= 4 ULP of the output scale.  (A 1-ULP change of a row's ln(sum)
+    moves every element of the row, so no bit-equal fraction is asserted.)"""
+    x = rnd(oracle, 95, *shape, scale=8.0)
+    got = host(rh.log_softmax(dev(x), axis))
+    exp = oracle.log_softmax(x, axis)
+    tol = 4 * np.spacing(np.maximum(np.abs(exp), 1.0).astype(np.float32))
+    assert np.all(np.abs(got - exp) <= tol), np.abs(got - exp).max()
+
+
+def test_log_softmax_reference_kats(rh):
+    for c in KATS["log_softmax"]:
+        x = np.array(c["x"], np.float32).reshape(c["x_shape"])
+        np.testing.assert_allclose(host(rh.log_softmax(dev(x), c["axis"])), np.array(c["y"]).reshape(x.shape),
+                                   atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("shape", [(1, 5, 2), (2, 3, 7, 9), (2, 64, 56, 56), (3, 4, 1027), (4, 6), (1, 2, 3, 4, 5)])
+def test_instance_norm_bitexact(rh, oracle, shape):
+    x = rnd(oracle, 96, *shape, scale=3.0)
+    sc = rnd(oracle, 97, shape[1]) + np.float32(1.0)
+    bi = rnd(oracle, 98, shape[1])
+    assert_bits(host(rh.instance_normalization(dev(x), dev(sc), dev(bi))), oracle.instance_norm(x, sc, bi),
+                f"instancenorm {shape}")
+
+
+def test_instance_norm_reference_kat_and_errors(rh):
+    c = KATS["instance_norm"]
+    x = np.array(c["x"], np.float32).reshape(c["x_shape"])
+    sc, bi = np.array(c["scale"], np.float32), np.array(c["bias"], np.float32)
+    np.testing.assert_allclose(host(rh.instance_normalization(dev(x), dev(sc), dev(bi))),
+                               np.array(c["y"]).reshape(x.shape), atol=1e-4, rtol=0)
+    for args, msg in [((x[0, 0], sc, bi), "expected input with >= 2 dims"),
+                      ((x, sc[:4], bi[:4]), "scale length should match channel count"),
+                      ((x, sc, bi[:4]), "bias length should match channel count")]:
+        with pytest.raises(rh.OpError) as e:
+            rh.instance_normalization(*(dev(a) for a in args))
+        assert str(e.value) == msg
+
+
+def test_log_softmax_instance_norm_graph(rh, oracle):
+    """Both ops as graph nodes: eager, captured, replayed."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    m = ModelSpec("norms")
+    x = m.value("x")
+    m.inputs = ["x"]
+    sc = m.const("sc", rnd(oracle, 99, 8) + np.float32(1.0))
+    bi = m.const("bi", rnd(oracle, 100, 8))
+    h = m.op("InstanceNormalization", [x, sc, bi], {"epsilon": 1e-3})
+    y = m.op("LogSoftmax", [h], {"axis": 1})
+    m.outputs = [y]
+    ins = {"x": rnd(oracle, 101, 2, 8, 5, 6, scale=2.0)}
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    xd = torch.from_numpy(ins["x"]).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        got = out[0].cpu().numpy()
+        assert np.all(np.abs(got - exp) <= 4 * np.spacing(np.maximum(np.abs(exp), 1.0))), np.abs(got - exp).max()
+
+
 # --------------------------------------------------------------------------
 # ConvTranspose (src/ops/conv.rs:329-577)
 # --------------------------------------------------------------------------

@@ -162,6 +162,26 @@ def test_kat_softmax(oracle, case):
     check(case["tol"], oracle.softmax(x, case["axis"]), case["y"])
 
 
+@pytest.mark.parametrize("case", KATS["log_softmax"], ids=lambda c: c["source"])
+def test_kat_log_softmax(oracle, case):
+    x = np.array(case["x"], np.float32).reshape(case["x_shape"])
+    check(case["tol"], oracle.log_softmax(x, case["axis"]), case["y"])
+
+
+def test_kat_instance_norm(oracle):
+    c = KATS["instance_norm"]
+    x = np.array(c["x"], np.float32).reshape(c["x_shape"])
+    sc, b = np.array(c["scale"], np.float32), np.array(c["bias"], np.float32)
+    check(c["tol"], oracle.instance_norm(x, sc, b), c["y"])
+    # the reference's error order (norm.rs:161-177)
+    for args, msg in [((x[0, 0], sc, b), "expected input with >= 2 dims"),
+                      ((x, sc[:4], b), "scale length should match channel count"),
+                      ((x, sc, b[:4]), "bias length should match channel count")]:
+        with pytest.raises(oracle.OpError) as e:
+            oracle.instance_norm(*args)
+        assert str(e.value) == msg
+
+
 @pytest.mark.parametrize("case", KATS["unary"], ids=lambda c: c["source"])
 def test_kat_unary(oracle, case):
     x = _arr(case["x"])

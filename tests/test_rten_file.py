@@ -121,6 +121,22 @@ def test_export_op_attrs_round_trip():
     assert "value=0.25" in ops["cos_f"] and "dtype=float" in ops["cos_f"]
 
 
+def test_norm_op_attrs_round_trip():
+    """LogSoftmax reads SoftmaxAttrs and InstanceNormalization reads
+    BatchNormalizationAttrs (op_registry.rs:556-564, 587)."""
+    m = ModelSpec("norm_ops")
+    x = m.value("x")
+    m.inputs = ["x"]
+    sc = m.const("sc", np.ones(4, np.float32))
+    bi = m.const("bi", np.zeros(4, np.float32))
+    h = m.op("InstanceNormalization", [x, sc, bi], {"epsilon": 0.5}, name="inorm")
+    m.outputs = [m.op("LogSoftmax", [h], {"axis": 1}, name="lsm")]
+    _, _, nodes = _parse(rten_file.describe_model(_model_bytes(m)))
+    ops = {rest.split(" ")[0]: rest for kind, rest in nodes.values() if kind == "op"}
+    assert "InstanceNormalization" in ops["inorm"] and "epsilon=0.5" in ops["inorm"]
+    assert "LogSoftmax" in ops["lsm"] and "axis=1" in ops["lsm"]
+
+
 def test_inline_and_external_constants_agree():
     spec = _tiny_spec()
     a = rten_file.describe_model(_model_bytes(spec, inline_max=0))
