@@ -78,6 +78,8 @@ Plan::~Plan() {
   }
   for (auto& kv : padded)
     if (kv.second.base) (void)hipFree(kv.second.base);
+  for (auto& kv : dwpw_wt)
+    if (kv.second) (void)hipFree(kv.second);
   for (auto& kv : matmuls) {
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
@@ -782,6 +784,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (nodes[op].fused_residual >= 0) uses[nodes[op].fused_residual]++;
     auto ef = p.expand_fused.find(op);
     if (ef != p.expand_fused.end()) uses[ef->second]++;
+    auto dpf = p.dwpw_fused.find(op);
+    if (dpf != p.dwpw_fused.end()) uses[dpf->second]++;
   }
   std::set<int> outset(out_ids.begin(), out_ids.end());
 
@@ -823,6 +827,31 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.expand_fused[op] = e.inputs[0];
       drop.push_back(n.fe_op);
     }
+    // Depthwise -> project pairs (Node::dp_op): opt-in, RTENHIP_DWPW=1 (the
+    // fused kernel measured slower, see dwpw.hip).
+    const char* dpe = getenv("RTENHIP_DWPW");
+    for (int op : p.ops) {
+      const Node& n = nodes[op];
+      if (!dpe || atoi(dpe) <= 0) break;
+      if (n.op_type != "Conv" || n.dp_op < 0 || !in_plan.count(n.dp_op) || p.expand_fused.count(n.dp_op) ||
+          std::find(drop.begin(), drop.end(), n.dp_op) != drop.end())
+        continue;
+      const Node& dn = nodes[n.dp_op];
+      if (dn.outputs.size() != 1 || n.inputs[0] != dn.outputs[0] || outset0.count(dn.outputs[0]) ||
+          uses_of_value(p.ops, dn.outputs[0]) != 1)
+        continue;
+      const Shape* xs = shape_of(dn.inputs[0]);
+      const Shape& ys = shapes[n.outputs[0]];
+      if (!xs || xs->size() != 4 || ys.size() != 4 || p.dtypes[dn.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
+      ConvAttrs da = conv_attrs(dn, false);
+      if (da.mode != 0 || da.dil != std::vector<int64_t>{1, 1} || da.strides != std::vector<int64_t>{1, 1} ||
+          da.pads.size() != 4 || ys[2] != (*xs)[2] || ys[3] != (*xs)[3] || ys[0] != (*xs)[0] ||
+          !dw_pw_eligible((int)(*xs)[1], (int)(*xs)[2], (int)(*xs)[3], (int)ys[1], (int)da.pads[0], (int)da.pads[1],
+                          (int)da.pads[2], (int)da.pads[3]))
+        continue;
+      p.dwpw_fused[op] = dn.inputs[0];
+      drop.push_back(n.dp_op);
+    }
     if (!drop.empty()) {
       std::vector<int> kept;
       for (int op : p.ops)
@@ -832,7 +861,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   }
   for (int op : p.ops) {
     const Node& n = nodes[op];
-    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op)) continue;
+    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op) || p.dwpw_fused.count(op)) continue;
     const Shape* xs = shape_of(n.inputs[0]);
     const Shape* ws = shape_of(n.inputs[1]);
     if (!xs || !ws || nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
@@ -1203,6 +1232,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       if (n.fused_residual >= 0) drop_use(n.fused_residual);
       auto ef = p.expand_fused.find(op);
       if (ef != p.expand_fused.end()) drop_use(ef->second);
+      auto dpf = p.dwpw_fused.find(op);
+      if (dpf != p.dwpw_fused.end()) drop_use(dpf->second);
       auto cdu = p.conv_dual.find(op);
       if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
     }
@@ -1307,6 +1338,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
+  if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_pw(p, op_id);
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
   if (t == "Conv" && p.conv_dual.count(op_id)) {
     bool handled = false;
@@ -1544,6 +1576,33 @@ rtenhip_status Graph::exec_expand_dw(Plan& p, int op_id) {
                           ptr_of(p, n.outputs[0]), (int)xs[0], (int)xs[1], (int)ys[1], (int)xs[2], (int)xs[3],
                           (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0], (int)fp[1], e.fused_act, e.act_lo,
                           e.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
+}
+
+// Depthwise (3x3) -> project (1x1) pair (Node::dp_op) the plan runs as one
+// dwpw.hip launch, reading the depthwise conv's input.
+rtenhip_status Graph::exec_dw_pw(Plan& p, int op_id) {
+  const Node& n = nodes[op_id];
+  const Node& dn = nodes[n.dp_op];
+  const int xv = p.dwpw_fused[op_id];
+  const Shape* xsp = plan_shape(*this, p, xv);
+  const Shape* ysp = plan_shape(*this, p, n.outputs[0]);
+  if (!xsp || !ysp) return fail(RTENHIP_HIP_ERROR, "depthwise+pointwise: missing shapes");
+  const Shape& xs = *xsp;
+  const Shape& ys = *ysp;
+  const int64_t C = xs[1], M = ys[1];
+  float*& wt = p.dwpw_wt[op_id];
+  if (!wt) {  // first (eager) run: the project weights transposed to [C][Mpad]
+    RTENHIP_HIP_CHECK(hipMalloc(&wt, (size_t)pw_weight_floats(M, C) * 4));
+    rtenhip_status st = pack_pw_weights(ptr_of(p, n.inputs[1]), M, C, wt, ctx->stream);
+    if (st) return st;
+  }
+  const float* bd = dn.inputs.size() > 2 && dn.inputs[2] >= 0 ? ptr_of(p, dn.inputs[2]) : nullptr;
+  const float* bp = n.inputs.size() > 2 && n.inputs[2] >= 0 ? ptr_of(p, n.inputs[2]) : nullptr;
+  const float* res = n.fused_residual >= 0 ? ptr_of(p, n.fused_residual) : nullptr;
+  ConvAttrs da = conv_attrs(dn, false);
+  return launch_dw_pw(ptr_of(p, xv), ptr_of(p, dn.inputs[1]), bd, wt, bp, res, ptr_of(p, n.outputs[0]), (int)xs[0],
+                      (int)C, (int)xs[2], (int)xs[3], (int)M, (int)da.pads[0], (int)da.pads[1], dn.fused_act, dn.act_lo,
+                      dn.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -2783,6 +2842,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           key = plan->chains[ci->second].ops[0] == plan->ops[i] ? "ConvChain" : "Conv(chained)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
+        if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+pw)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -3027,6 +3087,40 @@ rtenhip_status Graph::optimize() {
                                                          nodes[dn.inputs[2]].kind != NodeKind::Constant))
       continue;
     dn.fe_op = i;
+    fused++;
+  }
+  // MobileNetV2 inverted residual, back half: depthwise 3x3 Conv (+ its fused
+  // activation) whose only consumer is a 1x1 Conv (the project conv, with its
+  // fused residual / activation) -> the 1x1 node runs both (dwpw.hip).  The
+  // plan decides on shapes; a depthwise conv the plan runs with its expand
+  // conv (Node::fe_op) stays apart from its project conv.
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& dn = nodes[i];
+    if (dn.kind != NodeKind::Operator || dn.removed || dn.op_type != "Conv" || dn.fused_residual >= 0 ||
+        dn.outputs.size() != 1 || dn.inputs.size() < 2 || !dn.input_perm.empty())
+      continue;
+    const int dw = dn.inputs[1];
+    if (dw < 0 || nodes[dw].kind != NodeKind::Constant || nodes[dw].shape.size() != 4) continue;
+    const int64_t C = nodes[dw].shape[0];
+    if (nodes[dw].shape != Shape{C, 1, 3, 3} || (int64_t)dn.attrs.num("groups", 1) != C ||
+        (dn.inputs.size() > 2 && dn.inputs[2] >= 0 && nodes[dn.inputs[2]].kind != NodeKind::Constant))
+      continue;
+    const int p_op = sole(dn.outputs[0]);
+    if (p_op < 0) continue;
+    Node& pn = nodes[p_op];
+    if (pn.removed || pn.op_type != "Conv" || pn.dp_op >= 0 || pn.inputs.size() < 2 || pn.inputs[0] != dn.outputs[0] ||
+        !pn.input_perm.empty())
+      continue;
+    const int pw = pn.inputs[1];
+    if (pw < 0 || nodes[pw].kind != NodeKind::Constant || nodes[pw].shape.size() != 4 || nodes[pw].shape[1] != C ||
+        nodes[pw].shape[2] != 1 || nodes[pw].shape[3] != 1 ||
+        (pn.inputs.size() > 2 && pn.inputs[2] >= 0 && nodes[pn.inputs[2]].kind != NodeKind::Constant))
+      continue;
+    ConvAttrs pa = conv_attrs(pn, false);
+    if (pa.mode != 0 || pa.groups != 1 || pa.pads != std::vector<int64_t>{0, 0, 0, 0} ||
+        pa.strides != std::vector<int64_t>{1, 1} || pa.dil != std::vector<int64_t>{1, 1})
+      continue;
+    pn.dp_op = i;
     fused++;
   }
   // FusedTranspose (optimize.rs:329-378): a MatMul reads a Transpose's input

@@ -105,6 +105,11 @@ struct Node {
   // fused kernel takes (mbconv.hip) drops that op and runs both here, reading
   // the expand's input; otherwise both run as they are.
   int fe_op = -1;
+  // MobileNetV2's depthwise -> project pair (Graph::optimize): the 3x3
+  // depthwise Conv (+ its fused activation) whose only consumer is this 1x1
+  // Conv.  A plan whose shapes the fused kernel takes (dwpw.hip) drops that op
+  // and runs both here, reading the depthwise conv's input.
+  int dp_op = -1;
   // MatMul epilogue: constant [N] added per column after the K fold
   // (MatMul -> Add(bias)), before the residual and the activation.
   int fused_colbias = -1;
@@ -195,6 +200,10 @@ struct Plan {
   // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
   // the expand's input value, which the depthwise op then reads.
   std::map<int, int> expand_fused;
+  // Pointwise convs running their depthwise producer too (Node::dp_op): op id
+  // -> the depthwise input value; and their transposed weights (plan-owned).
+  std::map<int, int> dwpw_fused;
+  std::map<int, float*> dwpw_wt;
   // ResNet's conv3 + downsample pairs: conv3 op -> downsample op (its fused
   // residual's producer, read by nothing else).  On the first run conv3 times
   // the dual GEMM (gemm_dma_kernel DUAL, both convs in one launch) against
@@ -333,6 +342,7 @@ struct Graph {
   rtenhip_status build_chains(Plan& p);
   rtenhip_status exec_chain(Plan& p, ConvChain& c);
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
+  rtenhip_status exec_dw_pw(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   // The packed-A store a producer of value v makes this run, or false.
