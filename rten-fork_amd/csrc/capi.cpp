@@ -666,15 +666,21 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
   d.K = (int)a.K;
   d.tile = tile;
   d.apk = pk;
+  // Segments (DenseDmaArgs::n_seg) are the GEMM's "images": B, the output
+  // and the residual step by one segment per image.
+  const int64_t nseg = a.n_seg > 1 ? a.n_seg : 1;
+  if (a.N % nseg || (nseg > 1 && (a.residual || a.pk_out)))
+    return fail(RTENHIP_INVALID_VALUE, "segmented dense GEMM: unsupported operands");
+  const int64_t segn = a.N / nseg;
   d.x = a.b;
-  d.x_bytes = (uint32_t)(a.K * a.b_rs * 4);
+  d.x_bytes = (uint32_t)(nseg * a.K * a.b_rs * 4);
   d.x_img = a.K * a.b_rs;
   d.ystride = 0;
   d.xstride = 1;
-  d.OW = (int)a.N;
-  d.P = (int)a.N;
-  d.fdOW = make_fastdiv((uint32_t)a.N);
-  d.fdP = make_fastdiv((uint32_t)a.N);
+  d.OW = (int)segn;
+  d.P = (int)segn;
+  d.fdOW = make_fastdiv((uint32_t)segn);
+  d.fdP = make_fastdiv((uint32_t)segn);
   d.ktab4 = tab;
   d.out = a.out;
   d.out_img = a.M * a.out_rs;

@@ -186,6 +186,9 @@ struct DenseDmaArgs {
   float* pk_out;   // store C as the next MatMul's packed A (DmaDesc::pk_out) ...
   DmaTile pk_tile; // ... for this tile shape,
   int64_t pk_K;    // ... whose K is this GEMM's N
+  // n_seg > 1: N = n_seg segments of N / n_seg columns, segment s reading B
+  // at b + s * K * b_rs, writing out + s * M * out_rs, colbias[n] over all N.
+  int64_t n_seg;
 };
 // Whether gemm_dense_dma with these operands and cfg can store its output as
 // a packed A (DenseDmaArgs::pk_out): the vectorised epilogue runs.

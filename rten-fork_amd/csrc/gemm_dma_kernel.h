@@ -713,7 +713,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
             bl[i] = RES_PRE ? bpre[i] : d.bias[min(tm + wm + mi * 32 + i * 8 + rr, M - 1)];
         }
         float4 cb = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (d.colbias) cb = *(const float4*)(d.colbias + p);
+        if (d.colbias) cb = *(const float4*)(d.colbias + nn);  // (colbias over all N columns)
         float4 rl[RES_PRE ? 1 : 4];
         if constexpr (!RES_PRE) {
           if (d.residual) {
@@ -809,7 +809,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     // bias, the residual) are issued together before its stores -- vmcnt
     // retires in order, so a load behind a store would wait for the store.
     const bool bias_late = !MULTI_KB && d.bias && !d.cin;
-    const float cbv = d.colbias ? d.colbias[p] : 0.f;
+    const float cbv = d.colbias ? d.colbias[n] : 0.f;
 #pragma unroll
     for (int mi = 0; mi < MI; mi++) {
       float bv[16], rv[16];

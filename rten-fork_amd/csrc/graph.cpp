@@ -80,6 +80,8 @@ Plan::~Plan() {
     if (kv.second.base) (void)hipFree(kv.second.base);
   for (auto& kv : dwpw_wt)
     if (kv.second) (void)hipFree(kv.second);
+  for (float* b : grouped_bufs)
+    if (b) (void)hipFree(b);
   for (auto& kv : matmuls) {
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
@@ -980,6 +982,75 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.pk_cons[v] = op;
     }
   }
+  // MatMuls sharing A with constant [K, N] weights, the same shapes and the
+  // same epilogue kind (column bias or none; no residual / activation) run as
+  // one GEMM over N = nseg * N (each output element keeps its own K chain, so
+  // the bits do not change): the first in plan order leads, its B segments,
+  // biases and outputs stacked in plan-owned buffers.  RTENHIP_MM_GROUP=0
+  // keeps them apart.
+  if (!(getenv("RTENHIP_MM_GROUP") && atoi(getenv("RTENHIP_MM_GROUP")) == 0)) {
+    std::set<int> grouped;
+    for (int lead : p.ops) {
+      auto lit = p.matmuls.find(lead);
+      if (lit == p.matmuls.end() || grouped.count(lead)) continue;
+      const MatMulExec& le = lit->second;
+      auto ok = [&](int op) {
+        const Node& n = nodes[op];
+        const int b = n.inputs[1];
+        const Shape* bs = shape_of(b);
+        const bool cb_ok = n.fused_colbias < 0 ||
+                           (nodes[n.fused_colbias].kind == NodeKind::Constant && nodes[n.fused_colbias].dev &&
+                            prod(nodes[n.fused_colbias].shape) == le.N);
+        return !n.input_perm.count(1) && nodes[b].kind == NodeKind::Constant && nodes[b].dev && bs &&
+               bs->size() == 2 && n.fused_residual < 0 && !n.fused_act && cb_ok && !outset.count(n.outputs[0]) &&
+               n.outputs.size() == 1 && !p.pk_only.count(n.outputs[0]) && !p.pk_cons.count(n.outputs[0]);
+      };
+      if (!ok(lead) || le.b_rs != le.N) continue;
+      std::vector<int> members{lead};
+      for (int op : p.ops) {
+        if (op == lead || grouped.count(op) || members.size() >= 4) continue;
+        auto it = p.matmuls.find(op);
+        if (it == p.matmuls.end() || nodes[op].inputs[0] != nodes[lead].inputs[0] || !ok(op)) continue;
+        const MatMulExec& e = it->second;
+        if (e.M != le.M || e.N != le.N || e.K != le.K || e.b_rs != le.b_rs ||
+            (nodes[op].fused_colbias >= 0) != (nodes[lead].fused_colbias >= 0))
+          continue;
+        members.push_back(op);
+      }
+      if (members.size() < 2) continue;
+      const int nseg = (int)members.size();
+      const int64_t M = le.M, N = le.N, K = le.K;
+      float *out = nullptr, *bcat = nullptr, *cbcat = nullptr;
+      const bool has_cb = nodes[lead].fused_colbias >= 0;
+      if (hipMalloc(&out, (size_t)nseg * M * N * 4) != hipSuccess ||
+          hipMalloc(&bcat, (size_t)nseg * K * N * 4) != hipSuccess ||
+          (has_cb && hipMalloc(&cbcat, (size_t)nseg * N * 4) != hipSuccess)) {
+        if (out) (void)hipFree(out);
+        if (bcat) (void)hipFree(bcat);
+        return fail(RTENHIP_HIP_ERROR, "hipMalloc failed");
+      }
+      p.grouped_bufs.push_back(out);
+      p.grouped_bufs.push_back(bcat);
+      if (cbcat) p.grouped_bufs.push_back(cbcat);
+      for (int i = 0; i < nseg; i++) {
+        const Node& n = nodes[members[i]];
+        RTENHIP_HIP_CHECK(hipMemcpy(bcat + (int64_t)i * K * N, nodes[n.inputs[1]].dev, (size_t)K * N * 4,
+                                    hipMemcpyDeviceToDevice));
+        if (cbcat)
+          RTENHIP_HIP_CHECK(hipMemcpy(cbcat + (int64_t)i * N, nodes[n.fused_colbias].dev, (size_t)N * 4,
+                                      hipMemcpyDeviceToDevice));
+        p.grouped_val[n.outputs[0]] = out + (int64_t)i * M * N;
+        grouped.insert(members[i]);
+        if (i > 0) p.mm_group_skip.insert(members[i]);
+      }
+      MatMulExec& me = p.matmuls[lead];
+      me.nseg = nseg;
+      me.seg_n = N;
+      me.N = (int64_t)nseg * N;
+      me.b_cat = bcat;
+      me.cb_cat = cbcat;
+    }
+  }
   // Values produced by a DMA conv and read only (as input 0) by padded DMA
   // convs that agree on the padding get a persistent zero-bordered buffer.
   {
@@ -1185,8 +1256,9 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
                  n.op_type == "Unsqueeze" || n.op_type == "Squeeze";
     n.alias_input0 = alias;
     int in0 = n.inputs.empty() ? -1 : n.inputs[0];
-    if (p.padded.count(out)) {
-      // Persistent zero-bordered storage (PaddedValue), not in the arena.
+    if (p.padded.count(out) || p.grouped_val.count(out)) {
+      // Persistent zero-bordered storage (PaddedValue) or a grouped MatMul's
+      // output segment: plan-owned, not in the arena.
       s.offset = SIZE_MAX - 1;
       p.slots[out] = s;
     } else if (outset.count(out)) {
@@ -1268,6 +1340,8 @@ float* Graph::ptr_of(Plan& p, int v) {
   // copy (the caller's buffer receives it only at the end of the run).
   auto hit = p.host_dev.find(v);
   if (hit != p.host_dev.end()) return hit->second;
+  auto git = p.grouped_val.find(v);
+  if (git != p.grouped_val.end()) return git->second;
   for (size_t i = 0; i < p.output_ids.size(); i++)
     if (p.output_ids[i] == v) return p.bound_out[i];
   auto pit = p.padded.find(v);
@@ -1340,6 +1414,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_pw(p, op_id);
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
+  if (t == "MatMul" && p.mm_group_skip.count(op_id)) return RTENHIP_OK;  // computed by its group's leader
   if (t == "Conv" && p.conv_dual.count(op_id)) {
     bool handled = false;
     rtenhip_status st = exec_conv_dual(p, op_id, handled);
@@ -1822,11 +1897,12 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
   da.K = me.K;
   da.a = a.data;
   da.a_rs = me.K;
-  da.b = b.data;
+  da.b = me.nseg > 1 ? me.b_cat : b.data;
   da.b_rs = me.b_rs;
   da.out = y.data;
-  da.out_rs = me.N;
-  da.colbias = n.fused_colbias >= 0 ? nodes[n.fused_colbias].dev : nullptr;
+  da.out_rs = me.nseg > 1 ? me.seg_n : me.N;
+  da.n_seg = me.nseg;
+  da.colbias = me.nseg > 1 ? me.cb_cat : n.fused_colbias >= 0 ? nodes[n.fused_colbias].dev : nullptr;
   da.residual = ptr_of(p, n.fused_residual);
   da.res_rs = me.N;
   da.act = n.fused_act;
@@ -2841,6 +2917,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (ci != plan->chain_of.end() && plan->chains[ci->second].use)
           key = plan->chains[ci->second].ops[0] == plan->ops[i] ? "ConvChain" : "Conv(chained)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
+        if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
         if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+pw)";
         tot[key].first += ms;
@@ -2911,12 +2988,14 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           os << buf;
         }
         auto me = plan->matmuls.find(plan->ops[i]);
-        if (me != plan->matmuls.end()) {
+        if (plan->mm_group_skip.count(plan->ops[i])) {
+          os << "  (in its group's GEMM)";
+        } else if (me != plan->matmuls.end()) {
           const MatMulExec& m = me->second;
           const double fl = 2.0 * m.M * (double)m.N * m.K;
-          snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%d%s%s %.1f TF/s", (long long)m.M,
+          snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%d%s%s%s %.1f TF/s", (long long)m.M,
                    (long long)m.N, (long long)m.K, m.cfg, m.split ? " split" : "", pers_tag(m.persist),
-                   ms > 0 ? fl / (ms * 1e9) : 0.0);
+                   m.nseg > 1 ? (" group" + std::to_string(m.nseg)).c_str() : "", ms > 0 ? fl / (ms * 1e9) : 0.0);
           os << buf;
         }
         os << "\n";

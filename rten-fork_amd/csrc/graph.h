@@ -159,6 +159,13 @@ struct MatMulExec {
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
   int persist = 0;       // persistent launch, blocks per CU (0: one block per item); tuned
+  // Grouped MatMuls (Plan::mm_group): this leader runs nseg MatMuls that
+  // share A, as one GEMM with N = nseg * seg_n over stacked B / bias /
+  // output segments (BERT's Q, K and V projections).
+  int nseg = 1;
+  int64_t seg_n = 0;
+  float* b_cat = nullptr;   // [nseg][K][seg_n]
+  float* cb_cat = nullptr;  // [nseg][seg_n] or null
 };
 
 // A value stored with a zero border so the DMA convs reading it need no
@@ -203,6 +210,11 @@ struct Plan {
   // Pointwise convs running their depthwise producer too (Node::dp_op): op id
   // -> the depthwise input value; and their transposed weights (plan-owned).
   std::map<int, int> dwpw_fused;
+  // Grouped MatMuls (MatMulExec::nseg): members run by their leader, and the
+  // members' outputs as segments of one plan-owned [nseg][M][N] buffer.
+  std::set<int> mm_group_skip;
+  std::map<int, float*> grouped_val;
+  std::vector<float*> grouped_bufs;
   std::map<int, float*> dwpw_wt;
   // ResNet's conv3 + downsample pairs: conv3 op -> downsample op (its fused
   // residual's producer, read by nothing else).  On the first run conv3 times

@@ -618,3 +618,42 @@ def test_bottleneck_dual_gemm_bitexact(rh, monkeypatch, case, mode):
     torch.cuda.synchronize()
     rep = g.timing_report()
     assert ("Conv(dual)" in rep) == (mode == "force"), rep
+
+
+@pytest.mark.parametrize("group", ["on", "off"])
+def test_grouped_matmuls_bitexact(rh, monkeypatch, group):
+    """MatMuls sharing A with constant weights (BERT's Q / K / V projections)
+    run as one GEMM over stacked weight / bias / output segments
+    (MatMulExec::nseg; RTENHIP_MM_GROUP=0 keeps them apart): every output
+    element keeps its own K chain, so the bits are the unfused graph's."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    if group == "off":
+        monkeypatch.setenv("RTENHIP_MM_GROUP", "0")
+    else:
+        monkeypatch.delenv("RTENHIP_MM_GROUP", raising=False)
+    rng = np.random.default_rng(77)
+    B, S, K, N = 4, 64, 256, 256
+    m = ModelSpec("qkv")
+    a = m.value("a")
+    m.inputs = ["a"]
+    outs = []
+    for name, bias in (("q", True), ("k", True), ("v", True)):
+        w = m.const(name + ".w", rng.uniform(-0.1, 0.1, (K, N)).astype(np.float32))
+        y = m.op("MatMul", [a, w], name=name)
+        if bias:
+            y = m.op("Add", [y, m.const(name + ".b", rng.uniform(-0.1, 0.1, (N,)).astype(np.float32))])
+        outs.append(y)
+    m.outputs = [m.op("Mul", [m.op("Add", [outs[0], outs[1]]), outs[2]])]
+    ins = {"a": rng.uniform(-1, 1, (B, S, K)).astype(np.float32)}
+    exp = graph_runner.run(m, ins)[m.outputs[0]]
+    g = m.to_graph()
+    ad = torch.from_numpy(ins["a"]).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: ad}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        got = out[0].cpu().numpy()
+        assert _bits_equal(got, exp), np.abs(got - exp).max()
