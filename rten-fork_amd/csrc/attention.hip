@@ -27,6 +27,7 @@
 // Shapes: D = 64, S <= 128 and even (the graph executor checks this and runs
 // the unfused operator sequence otherwise).
 #include "common.h"
+#include "packed_a.h"
 #include "vecmath.h"
 
 #include <cfloat>
@@ -207,6 +208,35 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
       const int r = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
       if (FULL || r < S) dst[(int64_t)r * d.o_s + 32 * n2] = o[n2][e];
     }
+  if (d.pk) {
+    // Packed-A copy for the output projection: a lane quad (4g .. 4g + 3)
+    // holds a 4 x 4 block (rows e & 3 of group e >> 2, one column per lane);
+    // transposed through 4 rotations so lane 4g + c holds row c's 4 columns,
+    // stored as one k-quad (store_packed_a4).  Same values, new places.
+    const int c = l32 & 3, g4 = l32 & ~3;
+#pragma unroll
+    for (int n2 = 0; n2 < 2; n2++)
+#pragma unroll
+      for (int a = 0; a < 4; a++) {
+        float w[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+          const int si = (c - t) & 3;  // element this lane sends in round t
+          const float sv = si == 0 ? o[n2][4 * a] : si == 1 ? o[n2][4 * a + 1] : si == 2 ? o[n2][4 * a + 2] : o[n2][4 * a + 3];
+          const float rv = __shfl(sv, h * 32 + g4 + ((c + t) & 3));
+          const int di = (c + t) & 3;  // column of the received value
+          if (t == 0) w[0] = w[1] = w[2] = w[3] = 0.f;
+          w[0] = di == 0 ? rv : w[0];
+          w[1] = di == 1 ? rv : w[1];
+          w[2] = di == 2 ? rv : w[2];
+          w[3] = di == 3 ? rv : w[3];
+        }
+        const int r = i0 + c + 8 * a + 4 * h;
+        if (FULL || r < S)
+          store_packed_a4(d.pk, d.pk_lbm, d.pk_lbk, d.pk_tiles_k, (int64_t)b * S + r, hd * AT_D + 32 * n2 + g4,
+                          make_float4(w[0], w[1], w[2], w[3]));
+      }
+  }
 }
 
 bool attention_fast_ok(const AttnDesc& d) {

@@ -208,6 +208,10 @@ struct AttnDesc {
   int scale_op;
   float* out;
   int64_t o_b, o_h, o_s;
+  // Also store the output as the next MatMul's packed A (packed_a.h), the
+  // output being row-major [B * S, H * D] (o_s = H * D, o_h = D): null = no.
+  float* pk;
+  int pk_lbm, pk_lbk, pk_tiles_k;
 };
 bool attention_fast_ok(const AttnDesc& d);
 rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s);

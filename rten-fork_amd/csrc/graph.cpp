@@ -970,6 +970,17 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
         if (outset.count(v) || uses[v] != 1 || pit->second.M != cit->second.M || pit->second.N != cit->second.K)
           continue;
         p.pk_only.insert(v);
+      } else if (pn.op_type == "Reshape" && !pn.inputs.empty() && producer.count(pn.inputs[0]) &&
+                 nodes[producer[pn.inputs[0]]].op_type == "FusedAttention" &&
+                 !(getenv("RTENHIP_ATTN_PK") && atoi(getenv("RTENHIP_ATTN_PK")) == 0)) {
+        // The attention output [B, S, H, D] reshaped to the MatMul's A
+        // [B, S, H * D]: the kernel stores the packed copy (exec_attention
+        // checks the layout on every run).
+        const Shape* xs = shape_of(pn.inputs[0]);
+        if (!xs || xs->size() != 4 || (*xs)[2] * (*xs)[3] != cit->second.K ||
+            prod(*xs) != cit->second.M * cit->second.K)
+          continue;
+        p.attn_pk[producer[pn.inputs[0]]] = v;
       } else if (pn.op_type == "LayerNormalization") {
         const Shape* xs = shape_of(pn.inputs[0]);
         const int64_t ax = (int64_t)pn.attrs.num("axis", -1);
@@ -1757,7 +1768,25 @@ rtenhip_status Graph::exec_attention(Plan& p, int op_id, rtenhip_tensor y) {
       fast = attention_fast_ok(d);
     }
   }
-  if (fast) return launch_attention(d, ctx->stream);
+  if (fast) {
+    // Packed-A copy for the output projection (Plan::attn_pk) when the
+    // output is row-major [B * S, H * D].
+    auto ap = p.attn_pk.find(op_id);
+    PackedOut po;
+    DmaTile pt{0, 0, 0};
+    const int64_t M = (int64_t)d.B * d.S, K = (int64_t)d.H * d.D;
+    const bool pk = ap != p.attn_pk.end() && d.o_s == K && d.o_h == d.D && d.o_b == (int64_t)d.S * K &&
+                    packed_out_for(p, ap->second, M, K, po, pt) && pt.bm >= 4;
+    if (pk) {
+      d.pk = po.p;
+      d.pk_lbm = po.lbm;
+      d.pk_lbk = po.lbk;
+      d.pk_tiles_k = po.tiles_k;
+    }
+    rtenhip_status st = launch_attention(d, ctx->stream);
+    if (!st && pk) p.pk_ready[ap->second] = pt;
+    return st;
+  }
 
   // Unfused: s = q @ kT; s = s (/|*) c; s = s + mask; softmax; out = s @ v.
   rtenhip_ctx* c = cptr;

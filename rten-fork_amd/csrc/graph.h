@@ -213,6 +213,9 @@ struct Plan {
   // Grouped MatMuls (MatMulExec::nseg): members run by their leader, and the
   // members' outputs as segments of one plan-owned [nseg][M][N] buffer.
   std::set<int> mm_group_skip;
+  // FusedAttention op -> the value (its output's Reshape) a dense MatMul
+  // reads as A: the attention kernel also stores it packed (Plan::pk_cons).
+  std::map<int, int> attn_pk;
   std::map<int, float*> grouped_val;
   std::vector<float*> grouped_bufs;
   std::map<int, float*> dwpw_wt;
