@@ -2074,17 +2074,10 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
   }
   bind(me, me.cfg);
   const DmaTile tile = dma_cfg_tile(me.cfg);
-  // A stored packed by its producer earlier in this run (Plan::pk_cons).
-  auto pre = p.pk_ready.find(n.inputs[0]);
-  if (pre != p.pk_ready.end() && pre->second == tile) {
-    da.pk = p.pk_buf.at(n.inputs[0]).first;
-    da.pack = false;
-    return gemm_dense_dma(ctx, da);
-  }
-  if (pre != p.pk_ready.end() && p.pk_only.count(n.inputs[0]))
-    return fail(RTENHIP_INVALID_VALUE, "MatMul: A was stored packed for another tile shape");
   // Producer of a MatMul's A: store this output in that MatMul's packed
-  // layout instead of row-major (its only reader).
+  // layout instead of row-major (its only reader).  Set up before the
+  // packed-input branch below, which returns (FFN1 reads a LayerNorm-packed A
+  // and stores FFN2's packed A).
   {
     PackedOut po;
     DmaTile pt{0, 0, 0};
@@ -2100,6 +2093,15 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       }
     }
   }
+  // A stored packed by its producer earlier in this run (Plan::pk_cons).
+  auto pre = p.pk_ready.find(n.inputs[0]);
+  if (pre != p.pk_ready.end() && pre->second == tile) {
+    da.pk = p.pk_buf.at(n.inputs[0]).first;
+    da.pack = false;
+    return gemm_dense_dma(ctx, da);
+  }
+  if (pre != p.pk_ready.end() && p.pk_only.count(n.inputs[0]))
+    return fail(RTENHIP_INVALID_VALUE, "MatMul: A was stored packed for another tile shape");
   da.pack = !(p.mm_pack_value == n.inputs[0] && p.mm_pack_tile == tile);
   p.mm_pack_value = n.inputs[0];
   p.mm_pack_tile = tile;
