@@ -201,13 +201,15 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
       }
     }
   float* dst = d.out + b * d.o_b + hd * d.o_h + l32;
+  if (!d.pk_only) {
 #pragma unroll
-  for (int n2 = 0; n2 < 2; n2++)
+    for (int n2 = 0; n2 < 2; n2++)
 #pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const int r = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (FULL || r < S) dst[(int64_t)r * d.o_s + 32 * n2] = o[n2][e];
-    }
+      for (int e = 0; e < 16; e++) {
+        const int r = i0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (FULL || r < S) dst[(int64_t)r * d.o_s + 32 * n2] = o[n2][e];
+      }
+  }
   if (d.pk) {
     // Packed-A copy for the output projection: a lane quad (4g .. 4g + 3)
     // holds a 4 x 4 block (rows e & 3 of group e >> 2, one column per lane);

@@ -212,6 +212,7 @@ struct AttnDesc {
   // output being row-major [B * S, H * D] (o_s = H * D, o_h = D): null = no.
   float* pk;
   int pk_lbm, pk_lbk, pk_tiles_k;
+  int pk_only;  // with pk: skip the row-major store (nothing else reads it)
 };
 bool attention_fast_ok(const AttnDesc& d);
 rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s);

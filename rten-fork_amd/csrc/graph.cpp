@@ -981,6 +981,11 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
             prod(*xs) != cit->second.M * cit->second.K)
           continue;
         p.attn_pk[producer[pn.inputs[0]]] = v;
+        // Only the MatMul reads it (through the Reshape): the packed copy alone.
+        if (!outset.count(v) && !outset.count(pn.inputs[0]) && uses[v] == 1 && uses[pn.inputs[0]] == 1) {
+          p.attn_pk_only.insert(producer[pn.inputs[0]]);
+          p.pk_only.insert(v);
+        }
       } else if (pn.op_type == "LayerNormalization") {
         const Shape* xs = shape_of(pn.inputs[0]);
         const int64_t ax = (int64_t)pn.attrs.num("axis", -1);
@@ -1782,6 +1787,7 @@ rtenhip_status Graph::exec_attention(Plan& p, int op_id, rtenhip_tensor y) {
       d.pk_lbm = po.lbm;
       d.pk_lbk = po.lbk;
       d.pk_tiles_k = po.tiles_k;
+      d.pk_only = p.attn_pk_only.count(op_id) ? 1 : 0;
     }
     rtenhip_status st = launch_attention(d, ctx->stream);
     if (!st && pk) p.pk_ready[ap->second] = pt;

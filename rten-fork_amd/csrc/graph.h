@@ -216,6 +216,7 @@ struct Plan {
   // FusedAttention op -> the value (its output's Reshape) a dense MatMul
   // reads as A: the attention kernel also stores it packed (Plan::pk_cons).
   std::map<int, int> attn_pk;
+  std::set<int> attn_pk_only;  // ... and nothing reads its row-major output
   std::map<int, float*> grouped_val;
   std::vector<float*> grouped_bufs;
   std::map<int, float*> dwpw_wt;
