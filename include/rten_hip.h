@@ -294,9 +294,11 @@ int32_t rtenhip_graph_add_constant_i32(rtenhip_graph* g, const char* name, const
  * NULL = all float32); the plan infers every value's type (Cast, Gather,
  * Where, shape ops carry int32; the f32 kernels reject int32 inputs with
  * RTENHIP_INCORRECT_INPUT_TYPE).  output_dtypes (may be NULL) receives the
- * outputs' types.  A plan with a Gather on non-constant indices reports an
- * out-of-range index ("Entry in `indices` is out of range") when the run
- * completes, so such runs end with a stream synchronization. */
+ * outputs' types.  A plan with a Gather on non-constant indices checks its
+ * indices on the device (gather.rs:52-60) without a host round trip: an
+ * out-of-range index ("Entry in `indices` is out of range", INVALID_VALUE) is
+ * reported by rtenhip_graph_synchronize, or by the next run of the same plan
+ * (before that run is queued), whichever comes first. */
 rtenhip_status rtenhip_graph_run_typed(rtenhip_graph* g, const int32_t* input_ids,
                                        const rtenhip_tensor* inputs, const int32_t* input_dtypes,
                                        int32_t n_inputs, const int32_t* output_ids,
@@ -306,6 +308,10 @@ rtenhip_status rtenhip_graph_plan_typed(rtenhip_graph* g, const int32_t* input_i
                                         int32_t n_inputs, const int32_t* output_ids,
                                         int32_t n_outputs, int64_t* shapes, int32_t* ndims,
                                         int32_t* output_dtypes);
+/* Wait for every queued run of the graph and report a deferred Gather index
+ * error (see rtenhip_graph_run_typed).  Stands in for the point where RTen's
+ * synchronous Model::run returns (src/model.rs:580-592). */
+rtenhip_status rtenhip_graph_synchronize(rtenhip_graph* g);
 /* Output shape of a value after the last run (or -1). */
 int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape);
 /* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled. */

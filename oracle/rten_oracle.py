@@ -119,6 +119,32 @@ def gemm(a, b, alpha=1.0, beta=0.0, out=None, bias=None):
     return out
 
 
+def gemm_gflops_1t(m: int, n: int, k: int, seconds: float = 0.5) -> float:
+    """Single-thread GFLOP/s of gemm() at one of the reference's bench_gemm
+    shapes (src/gemm.rs:1782-1903 times m = n = k square products): best of
+    the runs made within `seconds`.  The thread count is restored after."""
+    import time
+
+    prev = num_threads()
+    set_num_threads(1)
+    try:
+        a = ((xorshift(11, m * k) - 0.5).reshape(m, k))
+        b = ((xorshift(12, k * n) - 0.5).reshape(k, n))
+        out = np.zeros((m, n), np.float32)
+        gemm(a, b, out=out)
+        best = float("inf")
+        t_end = time.perf_counter() + seconds
+        while True:
+            t0 = time.perf_counter()
+            gemm(a, b, out=out)
+            best = min(best, time.perf_counter() - t0)
+            if time.perf_counter() > t_end:
+                break
+        return 2.0 * m * n * k / best / 1e9
+    finally:
+        set_num_threads(prev)
+
+
 def reference_gemm(a, b, alpha=1.0, beta=0.0, out=None, bias=None):
     a, b = _c(a), _c(b)
     m, k = a.shape

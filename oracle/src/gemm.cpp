@@ -178,23 +178,47 @@ static void pack_b_block(float* out, const Mat& b, int64_t r0, int64_t r1, int64
 }
 
 // simd_gemm::<__m256, 6, 2> (kernels.rs:206-316): one fma chain per output
-// element from +0 over `depth`, then the alpha/beta store variants.
+// element from +0 over `depth`, then the alpha/beta store variants.  The
+// first depth - 1 steps run unrolled x4 with a prefetch of the next step's B
+// row (kernels.rs:226-245, unroll_loop! + S::prefetch); the last step follows
+// a write prefetch of the tile (kernels.rs:247-268).  The fma order per
+// element is the same k-ordered chain either way.
+__attribute__((target("avx2,fma"), always_inline)) static inline void k6x16_step(__m256 (&acc)[MR][2], const float* a,
+                                                                                  const float* b, int64_t k) {
+  const __m256 b0 = _mm256_loadu_ps(b + k * NR);
+  const __m256 b1 = _mm256_loadu_ps(b + k * NR + 8);
+  const float* ak = a + k * MR;
+  for (int i = 0; i < MR; i++) {
+    const __m256 av = _mm256_set1_ps(ak[i]);
+    acc[i][0] = _mm256_fmadd_ps(av, b0, acc[i][0]);
+    acc[i][1] = _mm256_fmadd_ps(av, b1, acc[i][1]);
+  }
+}
+
 __attribute__((target("avx2,fma"))) static void kernel_6x16(float* tile, int64_t tile_rs,
                                                             const float* a, const float* b,
                                                             int64_t depth, float alpha,
                                                             float beta) {
   __m256 acc[MR][2];
   for (int i = 0; i < MR; i++) acc[i][0] = acc[i][1] = _mm256_setzero_ps();
-  for (int64_t k = 0; k < depth; k++) {
-    __m256 b0 = _mm256_loadu_ps(b + k * NR);
-    __m256 b1 = _mm256_loadu_ps(b + k * NR + 8);
-    const float* ak = a + k * MR;
-    for (int i = 0; i < MR; i++) {
-      __m256 av = _mm256_set1_ps(ak[i]);
-      acc[i][0] = _mm256_fmadd_ps(av, b0, acc[i][0]);
-      acc[i][1] = _mm256_fmadd_ps(av, b1, acc[i][1]);
-    }
+  const int64_t body = depth - 1;
+  int64_t k = 0;
+  for (; k + 4 <= body; k += 4) {
+    _mm_prefetch((const char*)(b + (k + 1) * NR), _MM_HINT_T0);
+    k6x16_step(acc, a, b, k);
+    _mm_prefetch((const char*)(b + (k + 2) * NR), _MM_HINT_T0);
+    k6x16_step(acc, a, b, k + 1);
+    _mm_prefetch((const char*)(b + (k + 3) * NR), _MM_HINT_T0);
+    k6x16_step(acc, a, b, k + 2);
+    _mm_prefetch((const char*)(b + (k + 4) * NR), _MM_HINT_T0);
+    k6x16_step(acc, a, b, k + 3);
   }
+  for (; k < body; k++) {
+    _mm_prefetch((const char*)(b + (k + 1) * NR), _MM_HINT_T0);
+    k6x16_step(acc, a, b, k);
+  }
+  for (int i = 0; i < MR; i++) _mm_prefetch((const char*)(tile + i * tile_rs), _MM_HINT_T0);
+  if (depth > 0) k6x16_step(acc, a, b, depth - 1);
   if (beta == 0.f && alpha == 1.f) {
     for (int i = 0; i < MR; i++) {
       _mm256_storeu_ps(tile + i * tile_rs, acc[i][0]);

@@ -672,6 +672,9 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
   if (a.N % nseg || (nseg > 1 && (a.residual || a.pk_out)))
     return fail(RTENHIP_INVALID_VALUE, "segmented dense GEMM: unsupported operands");
   const int64_t segn = a.N / nseg;
+  // The kernel addresses B and the output segments with 32-bit byte offsets.
+  if (nseg > 1 && (uint64_t)nseg * a.K * a.b_rs * 4 >= (1ull << 32))
+    return fail(RTENHIP_UNSUPPORTED_VALUE, "segmented dense GEMM: operands exceed 32-bit offsets");
   d.x = a.b;
   d.x_bytes = (uint32_t)(nseg * a.K * a.b_rs * 4);
   d.x_img = a.K * a.b_rs;

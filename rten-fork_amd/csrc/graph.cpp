@@ -68,6 +68,13 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 
 Plan::~Plan() {
   if (gather_flag) (void)hipFree(gather_flag);
+  for (auto& c : gchk) {
+    if (c.ev) {
+      (void)hipEventSynchronize(c.ev);
+      (void)hipEventDestroy(c.ev);
+    }
+    if (c.host) (void)hipHostFree(c.host);
+  }
   for (auto& kv : host_dev)
     if (kv.second) (void)hipFree(kv.second);
   for (auto& kv : convs) {
@@ -80,8 +87,6 @@ Plan::~Plan() {
     if (kv.second.base) (void)hipFree(kv.second.base);
   for (auto& kv : dwpw_wt)
     if (kv.second) (void)hipFree(kv.second);
-  for (float* b : grouped_bufs)
-    if (b) (void)hipFree(b);
   for (auto& kv : matmuls) {
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
@@ -168,6 +173,10 @@ Graph::~Graph() {
   for (auto& n : nodes)
     if (n.kind == NodeKind::Constant && n.dev && n.owns_dev) (void)hipFree(n.dev);
   if (arena) (void)hipFree(arena);
+  for (auto& kv : mm_cat) {
+    if (kv.second.first) (void)hipFree(kv.second.first);
+    if (kv.second.second) (void)hipFree(kv.second.second);
+  }
   if (exec_stream) (void)hipStreamDestroy(exec_stream);
   if (side_stream) (void)hipStreamDestroy(side_stream);
   if (ev_in) (void)hipEventDestroy(ev_in);
@@ -926,6 +935,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   // M), B 2-D (or with unit batch dims) with unit column stride.
   for (int op : p.ops) {
     const Node& n = nodes[op];
+    if (!p.dma_mm) break;  // exec_matmul would take the general path (see Plan::dma_mm)
     if (n.op_type != "MatMul" || n.inputs.size() < 2 || n.input_perm.count(0)) continue;
     const Shape* as = shape_of(n.inputs[0]);
     const Shape* bs0 = shape_of(n.inputs[1]);
@@ -1036,26 +1046,39 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       if (members.size() < 2) continue;
       const int nseg = (int)members.size();
       const int64_t M = le.M, N = le.N, K = le.K;
-      float *out = nullptr, *bcat = nullptr, *cbcat = nullptr;
+      // The stacked B is addressed with 32-bit byte offsets by the kernel
+      // (the buffer resource of gemm_dma_kernel.h).
+      if ((uint64_t)nseg * K * N * 4 >= (1ull << 32)) continue;
       const bool has_cb = nodes[lead].fused_colbias >= 0;
-      if (hipMalloc(&out, (size_t)nseg * M * N * 4) != hipSuccess ||
-          hipMalloc(&bcat, (size_t)nseg * K * N * 4) != hipSuccess ||
-          (has_cb && hipMalloc(&cbcat, (size_t)nseg * N * 4) != hipSuccess)) {
-        if (out) (void)hipFree(out);
-        if (bcat) (void)hipFree(bcat);
-        return fail(RTENHIP_HIP_ERROR, "hipMalloc failed");
+      // Stacked weights / biases: one copy per graph, keyed by the member
+      // constants (every plan of the graph shares it).
+      std::vector<int> key;
+      for (int m : members) {
+        key.push_back(nodes[m].inputs[1]);
+        key.push_back(nodes[m].fused_colbias);
       }
-      p.grouped_bufs.push_back(out);
-      p.grouped_bufs.push_back(bcat);
-      if (cbcat) p.grouped_bufs.push_back(cbcat);
-      for (int i = 0; i < nseg; i++) {
-        const Node& n = nodes[members[i]];
-        RTENHIP_HIP_CHECK(hipMemcpy(bcat + (int64_t)i * K * N, nodes[n.inputs[1]].dev, (size_t)K * N * 4,
-                                    hipMemcpyDeviceToDevice));
-        if (cbcat)
-          RTENHIP_HIP_CHECK(hipMemcpy(cbcat + (int64_t)i * N, nodes[n.fused_colbias].dev, (size_t)N * 4,
+      auto cat = mm_cat.find(key);
+      if (cat == mm_cat.end()) {
+        float *bcat = nullptr, *cbcat = nullptr;
+        if (hipMalloc(&bcat, (size_t)nseg * K * N * 4) != hipSuccess ||
+            (has_cb && hipMalloc(&cbcat, (size_t)nseg * N * 4) != hipSuccess)) {
+          if (bcat) (void)hipFree(bcat);
+          return fail(RTENHIP_HIP_ERROR, "hipMalloc failed");
+        }
+        for (int i = 0; i < nseg; i++) {
+          const Node& n = nodes[members[i]];
+          RTENHIP_HIP_CHECK(hipMemcpy(bcat + (int64_t)i * K * N, nodes[n.inputs[1]].dev, (size_t)K * N * 4,
                                       hipMemcpyDeviceToDevice));
-        p.grouped_val[n.outputs[0]] = out + (int64_t)i * M * N;
+          if (cbcat)
+            RTENHIP_HIP_CHECK(hipMemcpy(cbcat + (int64_t)i * N, nodes[n.fused_colbias].dev, (size_t)N * 4,
+                                        hipMemcpyDeviceToDevice));
+        }
+        cat = mm_cat.emplace(key, std::make_pair(bcat, cbcat)).first;
+      }
+      // The outputs: one arena block of [nseg][M][N] placed when the leader's
+      // output is allocated, member i's value at segment i (make_plan).
+      p.mm_group[lead] = members;
+      for (int i = 0; i < nseg; i++) {
         grouped.insert(members[i]);
         if (i > 0) p.mm_group_skip.insert(members[i]);
       }
@@ -1063,8 +1086,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       me.nseg = nseg;
       me.seg_n = N;
       me.N = (int64_t)nseg * N;
-      me.b_cat = bcat;
-      me.cb_cat = cbcat;
+      me.b_cat = cat->second.first;
+      me.cb_cat = cat->second.second;
     }
   }
   // Values produced by a DMA conv and read only (as input 0) by padded DMA
@@ -1272,9 +1295,30 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
                  n.op_type == "Unsqueeze" || n.op_type == "Squeeze";
     n.alias_input0 = alias;
     int in0 = n.inputs.empty() ? -1 : n.inputs[0];
-    if (p.padded.count(out) || p.grouped_val.count(out)) {
-      // Persistent zero-bordered storage (PaddedValue) or a grouped MatMul's
-      // output segment: plan-owned, not in the arena.
+    auto grp = p.mm_group.find(op);
+    if (p.mm_group_skip.count(op)) {
+      // A grouped MatMul's member: its output segment was placed with the
+      // leader's (below).
+    } else if (grp != p.mm_group.end()) {
+      // Grouped MatMuls: one block of [nseg][M][N], live while any member's
+      // output is; member i's value is segment i.
+      const std::vector<int>& mem = grp->second;
+      int refs = 0;
+      for (int m : mem) refs += uses[nodes[m].outputs[0]];
+      const size_t seg = bytes;
+      const size_t off = alloc(seg * mem.size());
+      blocks.push_back({off, seg * mem.size(), refs});
+      for (size_t i = 0; i < mem.size(); i++) {
+        const int mo = nodes[mem[i]].outputs[0];
+        block_of[mo] = (int)blocks.size() - 1;
+        Slot ms;
+        ms.shape = shapes[mo];
+        ms.offset = off + i * seg;
+        p.slots[mo] = ms;
+      }
+    } else if (p.padded.count(out)) {
+      // Persistent zero-bordered storage (PaddedValue): plan-owned, not in
+      // the arena.
       s.offset = SIZE_MAX - 1;
       p.slots[out] = s;
     } else if (outset.count(out)) {
@@ -1356,8 +1400,6 @@ float* Graph::ptr_of(Plan& p, int v) {
   // copy (the caller's buffer receives it only at the end of the run).
   auto hit = p.host_dev.find(v);
   if (hit != p.host_dev.end()) return hit->second;
-  auto git = p.grouped_val.find(v);
-  if (git != p.grouped_val.end()) return git->second;
   for (size_t i = 0; i < p.output_ids.size(); i++)
     if (p.output_ids[i] == v) return p.bound_out[i];
   auto pit = p.padded.find(v);
@@ -1839,8 +1881,13 @@ rtenhip_status Graph::exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_
                                   rtenhip_tensor y) {
   const Node& n = nodes[op_id];
   auto mit = p.matmuls.find(op_id);
-  if (mit != p.matmuls.end() && ctx->use_dma && gemm_forced_cfg() < 0)
+  if (mit != p.matmuls.end()) {
+    // Plan-time choices (groups, packed-A producers and consumers) hold only
+    // on the DMA GEMM; find_plan keys plans on the knobs, so this is a guard.
+    if (!(ctx->use_dma && gemm_forced_cfg() < 0))
+      return fail(RTENHIP_HIP_ERROR, "dense MatMul planned for the DMA GEMM, which is now disabled");
     return exec_matmul_dma(p, op_id, a, b, y, mit->second);
+  }
   rtenhip_ctx* c = cptr;
   const bool fused = n.fused_colbias >= 0 || n.fused_residual >= 0 || n.fused_act;
   if (!fused) return rtenhip_matmul_f32(c, &a, &b, &y);
@@ -2672,13 +2719,19 @@ rtenhip_status Graph::find_plan(const int32_t* in_ids, const rtenhip_tensor* ins
   }
   for (int o : ov)
     if (o < 0 || o >= (int)nodes.size()) return fail(RTENHIP_INVALID_VALUE, "Invalid output id");
+  // A plan is specialised to the kernel knobs it was made under (Plan::dma,
+  // Plan::dma_mm): a knob change makes a new plan instead of running one whose
+  // groups / packed-A producers assume the DMA GEMM.
+  const bool dma = ctx->use_dma, dma_mm = ctx->use_dma && gemm_forced_cfg() < 0;
   for (auto& pl : plans)
     if (pl->input_ids == iv && pl->output_ids == ov && pl->input_shapes == ishapes &&
-        pl->input_dtypes == idt) {
+        pl->input_dtypes == idt && pl->dma == dma && pl->dma_mm == dma_mm) {
       *out = pl.get();
       return RTENHIP_OK;
     }
   auto np = std::make_unique<Plan>();
+  np->dma = dma;
+  np->dma_mm = dma_mm;
   rtenhip_status st = make_plan(iv, ishapes, idt, ov, *np);
   if (st) return st;
   plans.push_back(std::move(np));
@@ -2717,6 +2770,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   {
     rtenhip_status st = find_plan(in_ids, ins, n_in, in_dt, out_ids, n_out, &plan);
     if (st) return st;
+    // An index error an earlier run recorded and nobody has read yet is
+    // reported now, before this run is queued.
+    if (plan->gather_flag && (st = collect_gather_checks(*plan, false))) return st;
   }
   std::vector<int> ov(out_ids, out_ids + n_out);
   // Check the caller's output buffers (RunError::OutputMismatch).
@@ -3042,18 +3098,65 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   }
   ctx->stream = caller;
   if (plan->gather_flag) {
-    // Gather's index check (gather.rs:52-60) completes with the run: read the
-    // flag the kernels set on an out-of-range index, and clear it whatever the
-    // run's status, so a failed run cannot leave it set for the next one.
-    int bad = 0;
-    if (!st) RTENHIP_HIP_CHECK(hipMemcpyAsync(&bad, plan->gather_flag, sizeof(int), hipMemcpyDeviceToHost, exec_stream));
+    // Gather's index check (gather.rs:52-60), without a host round trip: the
+    // flag the kernels set on an out-of-range index goes to a pinned word of
+    // the check ring and is cleared whatever the run's status; an event marks
+    // the copy.  A later run or synchronize() reads it (collect_gather_checks).
+    Plan::GatherCheck& c = plan->gchk[plan->gchk_next];
+    if (c.pending) {
+      // The ring is full: this slot's run must have finished before reuse.
+      rtenhip_status cs = RTENHIP_OK;
+      if (hipEventSynchronize(c.ev) != hipSuccess) cs = fail(RTENHIP_HIP_ERROR, "gather check event");
+      else if (*c.host) cs = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+      c.pending = false;
+      if (!st) st = cs;
+    }
+    if (!c.host) {
+      RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.host), sizeof(int), hipHostMallocDefault));
+      RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
+    }
+    *c.host = 0;
+    const hipError_t e0 = hipMemcpyAsync(c.host, plan->gather_flag, sizeof(int), hipMemcpyDeviceToHost, exec_stream);
     const hipError_t e1 = hipMemsetAsync(plan->gather_flag, 0, sizeof(int), exec_stream);
-    const hipError_t e2 = hipStreamSynchronize(exec_stream);
-    if (!st && (e1 != hipSuccess || e2 != hipSuccess)) st = hip_fail(e1 != hipSuccess ? e1 : e2, "gather flag");
-    if (!st && bad) st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+    const hipError_t e2 = hipEventRecord(c.ev, exec_stream);
+    if (e0 != hipSuccess || e1 != hipSuccess || e2 != hipSuccess) {
+      if (!st) st = hip_fail(e0 != hipSuccess ? e0 : e1 != hipSuccess ? e1 : e2, "gather flag");
+    } else {
+      c.pending = true;
+      plan->gchk_next = (plan->gchk_next + 1) % Plan::kGatherChecks;
+    }
   }
   RTENHIP_HIP_CHECK(hipEventRecord(ev_out, exec_stream));
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
+  return st;
+}
+
+rtenhip_status Graph::collect_gather_checks(Plan& p, bool wait) {
+  rtenhip_status st = RTENHIP_OK;
+  // Oldest first, so the error reported is the earliest run's.
+  for (int i = 0; i < Plan::kGatherChecks; i++) {
+    Plan::GatherCheck& c = p.gchk[(p.gchk_next + i) % Plan::kGatherChecks];
+    if (!c.pending) continue;
+    const hipError_t e = wait ? hipEventSynchronize(c.ev) : hipEventQuery(c.ev);
+    if (e == hipErrorNotReady) continue;
+    c.pending = false;
+    if (e != hipSuccess) {
+      if (!st) st = hip_fail(e, "gather check event");
+    } else if (*c.host && !st) {
+      st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+    }
+  }
+  return st;
+}
+
+rtenhip_status Graph::synchronize() {
+  rtenhip_status st = RTENHIP_OK;
+  if (exec_stream && hipStreamSynchronize(exec_stream) != hipSuccess) st = fail(RTENHIP_HIP_ERROR, "hipStreamSynchronize");
+  for (auto& pl : plans)
+    if (pl->gather_flag) {
+      const rtenhip_status s2 = collect_gather_checks(*pl, true);
+      if (!st) st = s2;
+    }
   return st;
 }
 
@@ -3577,6 +3680,8 @@ int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape) 
   }
   return -1;
 }
+
+rtenhip_status rtenhip_graph_synchronize(rtenhip_graph* g) { return G_(g)->synchronize(); }
 
 rtenhip_status rtenhip_graph_set_timing(rtenhip_graph* g, int enabled) {
   G_(g)->timing = enabled != 0;

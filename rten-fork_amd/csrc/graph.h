@@ -196,6 +196,11 @@ struct ConvChain {
 
 struct Plan {
   ~Plan();
+  // Kernel knobs the plan was made under (Graph::find_plan matches them):
+  // Ctx::use_dma, and use_dma with no forced GEMM configuration (dense
+  // MatMuls on the DMA GEMM; only then are Q/K/V groups and packed-A
+  // producers formed, since only that kernel writes them).
+  bool dma = true, dma_mm = true;
   std::vector<int> ops;               // topological order
   std::map<int, ConvExec> convs;      // op id -> DMA conv state
   std::map<int, PaddedValue> padded;  // value id -> zero-bordered storage
@@ -210,15 +215,15 @@ struct Plan {
   // Pointwise convs running their depthwise producer too (Node::dp_op): op id
   // -> the depthwise input value; and their transposed weights (plan-owned).
   std::map<int, int> dwpw_fused;
-  // Grouped MatMuls (MatMulExec::nseg): members run by their leader, and the
-  // members' outputs as segments of one plan-owned [nseg][M][N] buffer.
+  // Grouped MatMuls (MatMulExec::nseg): leader op -> members (leader first),
+  // members run by their leader; the members' outputs are segments of one
+  // arena block of [nseg][M][N].
+  std::map<int, std::vector<int>> mm_group;
   std::set<int> mm_group_skip;
   // FusedAttention op -> the value (its output's Reshape) a dense MatMul
   // reads as A: the attention kernel also stores it packed (Plan::pk_cons).
   std::map<int, int> attn_pk;
   std::set<int> attn_pk_only;  // ... and nothing reads its row-major output
-  std::map<int, float*> grouped_val;
-  std::vector<float*> grouped_bufs;
   std::map<int, float*> dwpw_wt;
   // ResNet's conv3 + downsample pairs: conv3 op -> downsample op (its fused
   // residual's producer, read by nothing else).  On the first run conv3 times
@@ -268,10 +273,20 @@ struct Plan {
   // or a graph output reads (uploaded once, plan-owned).
   std::map<int, HostVal> host;
   std::map<int, float*> host_dev;
-  // Gathers with non-constant indices record an out-of-range index here; the
-  // run reads and clears it when it completes (graph-capturable: no sync
-  // inside the ops).
+  // Gathers with non-constant indices record an out-of-range index here
+  // (graph-capturable: no sync inside the ops).  The end of each run copies
+  // the flag into a pinned host word, clears it and records an event, all
+  // asynchronously (a ring of kGatherChecks, so several runs can be queued);
+  // the check is read at the start of a later run of the plan or by
+  // Graph::synchronize (rtenhip_graph_synchronize).
   int* gather_flag = nullptr;
+  static constexpr int kGatherChecks = 4;
+  struct GatherCheck {
+    int* host = nullptr;       // pinned
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  } gchk[kGatherChecks];
+  int gchk_next = 0;
   // hipGraph replay state: valid for these exact input/output pointers.
   hipGraphExec_t exec = nullptr;
   std::vector<float*> bound_in, bound_out;
@@ -293,6 +308,10 @@ struct Graph {
   std::map<std::string, int> by_name;
   std::vector<int> model_inputs, model_outputs;
   std::vector<std::unique_ptr<Plan>> plans;
+  // Grouped MatMuls' stacked weights and column biases ([nseg][K][N],
+  // [nseg][N]), keyed by the members' (weight, bias) node ids; shared by
+  // every plan of the graph.
+  std::map<std::vector<int>, std::pair<float*, float*>> mm_cat;
   void* arena = nullptr;
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
@@ -321,6 +340,11 @@ struct Graph {
                      const int32_t* out_ids, rtenhip_tensor* outs, int n_out,
                      const int32_t* in_dt = nullptr);
   rtenhip_status optimize();
+  // Waits for the queued runs and reports a Gather index error any of them
+  // recorded (see Plan::gchk).
+  rtenhip_status synchronize();
+  // Reads the completed Gather checks of p (all pending ones when wait).
+  rtenhip_status collect_gather_checks(Plan& p, bool wait);
   // RTen's own passes (src/optimize.rs:286-518, graph_optimize.cpp), run
   // first by optimize(): constant propagation, Silu / Gelu / LayerNorm fusion.
   rtenhip_status rten_optimize();

@@ -167,9 +167,16 @@ class Graph:
     def output_shapes(self, inputs: Dict[int, object], outputs: Sequence[int]):
         return [s for s, _ in self.output_info(inputs, outputs)]
 
+    def synchronize(self):
+        """Wait for the queued runs; raises the deferred Gather index error
+        ("Entry in `indices` is out of range") a run recorded."""
+        check(lib().rtenhip_graph_synchronize(C.c_void_p(self.ptr)))
+
     def run(self, inputs: Dict[int, object], outputs: Sequence[int], out=None):
         """Graph::run: inputs {value id: float32 or int32 device tensor};
-        returns device tensors (int32 where the graph's value is int32)."""
+        returns device tensors (int32 where the graph's value is int32).
+        Queued on the device without a host round trip: a Gather index error
+        is raised by synchronize() or by the next run of the same plan."""
         torch = _torch()
         self.ctx.sync_stream()
         in_ids = list(inputs.keys())

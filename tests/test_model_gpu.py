@@ -207,9 +207,10 @@ def _gather_graph():
 
 def test_graph_gather_index_error_and_types(rh):
     """Gather in the captured plan reports an out-of-range index with the
-    reference's error when the run completes (gather.rs:52-60), and the next
-    valid run succeeds; negative indices count from the end; Cast of an int32
-    value; int32 data into an f32-only operator is IncorrectInputType."""
+    reference's error (gather.rs:52-60) without a host round trip per run:
+    at synchronize(), or at the next run of the plan (before it is queued);
+    later valid runs succeed; negative indices count from the end; Cast of an
+    int32 value; int32 data into an f32-only operator is IncorrectInputType."""
     import torch
     from rten_hip import OpError
     from rten_hip.graph import ModelSpec
@@ -220,13 +221,20 @@ def test_graph_gather_index_error_and_types(rh):
     table = np.arange(12, dtype=np.float32).reshape(4, 3)
     exp = table[np.array([[0, 3], [3, 2]])]
     outs = None
-    for feed in (good, good, good, bad, good, bad, good):  # eager, capture, replays
-        if feed is bad:
+    # eager, capture, replays; "bad+next": the error surfaces at the next run
+    for feed in (good, good, good, "bad", good, "bad+next", good, good):
+        if isinstance(feed, str):
+            g.run({g.input_ids[0]: bad}, g.output_ids, out=outs)
             with pytest.raises(OpError, match="Entry in `indices` is out of range") as e:
-                g.run({g.input_ids[0]: feed}, g.output_ids, out=outs)
+                if feed == "bad":
+                    g.synchronize()
+                else:
+                    torch.cuda.synchronize()
+                    g.run({g.input_ids[0]: good}, g.output_ids, out=outs)
             assert e.value.kind == "InvalidValue"
             continue
         outs = g.run({g.input_ids[0]: feed}, g.output_ids, out=outs)
+        g.synchronize()
         torch.cuda.synchronize()
         assert _bits_equal(outs[0].cpu().numpy(), exp)
         assert outs[1].dtype == torch.float32
@@ -657,3 +665,70 @@ def test_grouped_matmuls_bitexact(rh, monkeypatch, group):
         torch.cuda.synchronize()
         got = out[0].cpu().numpy()
         assert _bits_equal(got, exp), np.abs(got - exp).max()
+    g.set_timing(True)
+    g.run({g.input_ids[0]: ad}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    rep = g.timing_report()
+    g.set_timing(False)
+    # The grouping is actually taken (or not) -- not a pass on the ungrouped path.
+    assert ("MatMul(in_group)" in rep) == (group == "on"), rep
+    assert (" group3" in rep) == (group == "on"), rep
+
+    # Knob change after planning: with the DMA GEMM disabled the graph makes a
+    # new plan (Plan::dma_mm) without groups, and every output is still written.
+    import ctypes
+
+    lib = rh.lib()
+    lib.rtenhip_debug_set_dma.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ctx = rh.default_context()
+    lib.rtenhip_debug_set_dma(ctypes.c_void_p(ctx.ptr), 0)
+    try:
+        for _ in range(3):
+            out = g.run({g.input_ids[0]: ad}, g.output_ids, out=out)
+            torch.cuda.synchronize()
+            got = out[0].cpu().numpy()
+            assert _bits_equal(got, exp), np.abs(got - exp).max()
+    finally:
+        lib.rtenhip_debug_set_dma(ctypes.c_void_p(ctx.ptr), 1)
+
+
+@pytest.mark.parametrize("attn_pk", ["on", "off"])
+@pytest.mark.parametrize("extra_reader", [False, True])
+def test_attention_packed_a_store_bitexact(rh, monkeypatch, attn_pk, extra_reader):
+    """FusedAttention -> Reshape -> MatMul (BERT's output projection): the
+    attention kernel stores the MatMul's packed A (Plan::attn_pk), alone when
+    nothing else reads its output (Plan::attn_pk_only), both layouts when the
+    reshaped output has another reader.  The layout is fixed by the MatMul's
+    tile on the first run, so the eager run, the capture and the replays are
+    all checked; RTENHIP_ATTN_PK=0 turns the packed store off."""
+    import torch
+    import graph_runner
+
+    if attn_pk == "off":
+        monkeypatch.setenv("RTENHIP_ATTN_PK", "0")
+    else:
+        monkeypatch.delenv("RTENHIP_ATTN_PK", raising=False)
+    B, H, S, D, N = 4, 4, 64, 64, 256  # M * N * K = 2^24: the dense DMA GEMM
+    m = _attention_spec(S, D, H, "Div", "b11s", True)
+    o = m.outputs[0]
+    shape_merge = m.const("shape.merge", np.array([0, 0, H * D], np.float32))
+    c = m.op("Reshape", [o, shape_merge], name="ctx.reshape")
+    rng = np.random.default_rng(5)
+    w = m.const("proj.w", rng.uniform(-0.1, 0.1, (H * D, N)).astype(np.float32))
+    b = m.const("proj.b", rng.uniform(-0.1, 0.1, (N,)).astype(np.float32))
+    y = m.op("Add", [m.op("MatMul", [c, w], name="proj"), b], name="proj.add")
+    m.outputs = [y] + ([m.op("Relu", [c], name="other")] if extra_reader else [])
+    ins = {n: (rng.random((B, H, S, D), dtype=np.float32) - np.float32(0.5)) * 2 for n in ("q", "k", "v")}
+    mask = np.zeros((B, 1, 1, S), np.float32)
+    mask[-1, ..., S - S // 4:] = -10000.0
+    ins["mask"] = mask
+    res = graph_runner.run(m, ins)
+    g = m.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[name]).cuda() for i, name in enumerate(m.inputs)}
+    out = None
+    for r in range(4):  # eager (tuning fixes the layout), capture, replays
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        for i, name in enumerate(m.outputs):
+            got = out[i].cpu().numpy()
+            assert _bits_equal(got, res[name]), f"run {r} output {i}: max abs {np.abs(got - res[name]).max():.3g}"
