@@ -1326,10 +1326,11 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       s.ext = nullptr;
       p.slots[out] = s;
     } else if (alias && block_of.count(in0)) {
+      // (the input's own offset: a grouped MatMul's segment lies inside its block)
       Block& b = blocks[block_of[in0]];
       b.refs += uses[out];
       block_of[out] = block_of[in0];
-      s.offset = b.off;
+      s.offset = p.slots[in0].offset;
       p.slots[out] = s;
     } else if (alias) {
       // Alias of an input/constant: share its pointer at run time.
@@ -1341,7 +1342,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       Block& b = blocks[block_of[in0]];
       b.refs += uses[out];
       block_of[out] = block_of[in0];
-      s.offset = b.off;
+      s.offset = p.slots[in0].offset;
       p.slots[out] = s;
     } else {
       size_t off = alloc(bytes);
