@@ -163,12 +163,6 @@ rtenhip_status launch_copy_view(const float* src, const int64_t* shape, const in
 rtenhip_status launch_fill(void* y, int64_t n, uint32_t bits, hipStream_t s);
 // Fused 1x1 expand (+bias, act) -> 3x3 depthwise (+bias, act) (mbconv.hip).
 bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, int pr);
-// Fused 3x3 stride-1 pad-1 depthwise (+bias, act) -> 1x1 project (+bias,
-// residual, act) (dwpw.hip); wt = project weights transposed (pack_pw_weights).
-bool dw_pw_eligible(int C, int H, int W, int M, int pt, int pl, int pb, int pr);
-rtenhip_status launch_dw_pw(const float* x, const float* wd, const float* bd, const float* wt, const float* bp,
-                            const float* residual, float* y, int N, int C, int H, int W, int M, int pt, int pl,
-                            int act_d, float lo_d, float hi_d, int act_p, float lo_p, float hi_p, hipStream_t s);
 rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be, const float* wd, const float* bd,
                                 float* y, int N, int cin, int hidden, int H, int W, int OH, int OW, int S, int pt,
                                 int pl, int act_e, float lo_e, float hi_e, int act_d, float lo_d, float hi_d,

@@ -29,6 +29,12 @@
 
 namespace rtenhip {
 
+// Timing experiments only (rtenhip_debug_set_lat_stamps): each launch writes
+// 8 u64 per wave at the next free records of this buffer.
+static unsigned long long* g_lat_stamps = nullptr;
+static int64_t g_lat_stamps_cap = 0, g_lat_stamps_used = 0;
+static int g_lat_seq = 0;
+
 template <int WMW, int MI>
 __global__ __launch_bounds__(256) void gemm_lat_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
   constexpr int WNW = 4 / WMW;
@@ -48,7 +54,141 @@ __global__ __launch_bounds__(256) void gemm_lat_kernel(DmaDesc d, int wg_m, int 
   const int n0 = (tn * WNW + wn) * 16;
   if (sub0 >= subs || n0 >= d.N) return;  // wave past the matrix edge (no counters touched)
   const int wt = (tm * WMW + wm) * (wg_n * WNW) + (n0 >> 4);
-  lat_unit<MI, false>(d, sub0, n0, kb, nkb, subs, wt, ktl[wave], LatNoWait{}, LatNoDone{});
+  lat_unit<MI>(d, sub0, n0, kb, nkb, subs, wt, ktl[wave]);
+}
+
+// LDS-staged variant (71 / 72 / 74): a workgroup of 4 waves computes RW x CW
+// 16x16 tiles of one KC block, one chain per wave.  The RW packed A panels
+// (16 rows x 256 k each) and the CW B tiles (256 k x 16 columns each) are
+// staged in LDS once per workgroup -- A with 16-byte loads, B gathered by all
+// 256 threads -- so a panel read from L2 / the Infinity Cache serves CW waves
+// and a gathered B element RW waves (the one-wave-per-unit kernel above loads
+// both once per wave).  The chains then read their operands from LDS as
+// 16-byte groups in the same k order, so the bits are those of every other
+// variant; the fold and the epilogue are lat_fold_finish's.
+template <int RW, int CW>
+__global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
+  static_assert(RW * CW == 4, "one chain per wave");
+  __shared__ float4 lds_a[RW][LGROUPS][64];
+  __shared__ float4 lds_b[CW][LGROUPS][64];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
+  const int o = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tn = o % wg_n;
+  const int t2 = o / wg_n;
+  const int tm = t2 % wg_m;
+  const int kb = t2 / wg_m;
+  const int K = d.K;
+  const int k0 = kb * LKC;
+  const int ng = min(LGROUPS, (K - k0 + 15) >> 4);
+  const int wr = wave / CW, wc = wave - (wave / CW) * CW;
+  const int sub0 = tm * RW + wr;
+  const int n0 = (tn * CW + wc) * 16;
+  LatStamps stp = lat_stamps_init(d, kb, sub0, n0);
+
+  // A: RW panels of [16 groups][64 lanes] float4 (launch_pack_lat: zero past
+  // K inside a block); rows past M read past the buffer, which returns 0.
+  // All loads are issued before any LDS store (one memory round trip).
+  const __amdgpu_buffer_rsrc_t ar =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, (int)((int64_t)subs * nkb * LGROUPS * 64 * 16), 0x00020000);
+  typedef unsigned int lat_u32x4 __attribute__((ext_vector_type(4)));
+  lat_u32x4 av[RW * 4];
+#pragma unroll
+  for (int i = 0; i < RW * 4; i++) {
+    const int idx = (int)threadIdx.x + 256 * i;
+    const int r = idx >> 10, gl = idx & 1023;
+    const int sub = tm * RW + r;
+    const uint32_t off = sub < subs ? (uint32_t)(((sub * nkb + kb) * LGROUPS * 64 + gl) * 16) : DMA_OOB;
+    av[i] = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
+  }
+
+  // B: thread (wave w, lane (c, h)) gathers groups 4w..4w+3 of each of the CW
+  // column tiles: k = k0 + 16g + 4j + h for j = 0..3, column n0 + c.
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
+  const int h = lane >> 4;
+  const bool linear = d.kstride > 0;
+  // 3x3 windows: koff(k) for k = 9c + 3ky + kx (see lat_chain); this thread
+  // visits k = k0 + h + 4s for s = 16w .. 16w + 15.
+  uint32_t k3off[9];
+  const uint32_t k3step = 16u * (uint32_t)d.kt_plane;
+  if (!linear) {
+    const uint32_t kh0 = (uint32_t)(k0 + h + 64 * wave);
+    const int c0 = (int)(__umulhi(kh0, 0x38E38E39u) >> 1);
+    const int r0 = (int)kh0 - 9 * c0;
+#pragma unroll
+    for (int s9 = 0; s9 < 9; s9++) {
+      const int kk = r0 + 4 * s9;
+      const int q = (kk * 57) >> 9;
+      const int rr2 = kk - 9 * q;
+      const int ky = (rr2 * 11) >> 5;
+      const int kx = rr2 - 3 * ky;
+      k3off[s9] = (uint32_t)((c0 + q) * d.kt_plane + ky * d.kt_row + kx * d.kt_col) * 4u;
+    }
+  }
+  uint32_t koff[16];
+#pragma unroll
+  for (int st = 0; st < 16; st++) {  // step within this thread's 16
+    const int k = k0 + 64 * wave + 4 * st + h;
+    const uint32_t lin = (uint32_t)k * (uint32_t)d.kstride * 4u;
+    const uint32_t win = k3off[st % 9] + (uint32_t)(st / 9) * k3step;
+    koff[st] = k < K ? (linear ? lin : win) : DMA_OOB;
+  }
+  float bv[CW][4][4];
+#pragma unroll
+  for (int cw = 0; cw < CW; cw++) {
+    const LatCol col = lat_col(d, (tn * CW + cw) * 16);
+#pragma unroll
+    for (int gi = 0; gi < 4; gi++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        bv[cw][gi][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + koff[4 * gi + j], 0, 0));
+  }
+  if (stp.p) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stp.at(9);
+  }
+#pragma unroll
+  for (int i = 0; i < RW * 4; i++) {
+    const int idx = (int)threadIdx.x + 256 * i;
+    lds_a[idx >> 10][(idx >> 6) & 15][idx & 63] =
+        make_float4(__uint_as_float(av[i].x), __uint_as_float(av[i].y), __uint_as_float(av[i].z), __uint_as_float(av[i].w));
+  }
+#pragma unroll
+  for (int cw = 0; cw < CW; cw++)
+#pragma unroll
+    for (int gi = 0; gi < 4; gi++)
+      lds_b[cw][4 * wave + gi][lane] = make_float4(bv[cw][gi][0], bv[cw][gi][1], bv[cw][gi][2], bv[cw][gi][3]);
+
+  // Epilogue operands of this wave's tile, in flight during the chain.
+  const bool live = sub0 < subs && n0 < d.N;
+  const LatCol col = lat_col(d, n0);
+  LatEpi<1> e;
+  if (live) lat_epi_loads<1>(d, sub0, col, e);
+  __syncthreads();
+  if (!live) return;  // (after the barrier: every wave helped stage)
+  stp.at(2);
+
+  lat_f32x4 acc[1];
+  acc[0] = (lat_f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < LGROUPS; g++) {
+    if (g < ng) {
+      const float4 a4 = lds_a[wr][g][lane];
+      const float4 b4 = lds_b[wc][g][lane];
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[0], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[0], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[0], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, acc[0], 0, 0, 0);
+    }
+  }
+  if (stp.p) {
+    asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][3]));
+    stp.at(3);
+  }
+  const int wt = sub0 * (wg_n * CW) + (n0 >> 4);
+  lat_fold_finish<1>(d, sub0, kb, nkb, wt, col, e, acc, stp);
 }
 
 // All K blocks of one tile in one workgroup: W = min(nkb, 8) waves, wave w
@@ -70,15 +210,15 @@ __global__ __launch_bounds__(512) void gemm_lat_wg_kernel(DmaDesc d, int n16, in
   const LatCol col = lat_col(d, nt * 16);
   LatEpi<MI> e;  // wave 0's epilogue operands, loaded along with its first block's operands
   const bool early = !(d.dbg & 4);  // (d.dbg & 4: A/B experiments only, loaded after the chains)
-  if (wave == 0 && early) lat_epi_loads<MI>(d, sub0, col, false, e);
+  if (wave == 0 && early) lat_epi_loads<MI>(d, sub0, col, e);
   for (int kb = wave; kb < nkb; kb += W) {
     lat_f32x4 acc[MI];
-    lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, LatNoWait{}, false, acc);
+    lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, acc);
 #pragma unroll
     for (int mi = 0; mi < MI; mi++)
       part[(kb * MI + mi) * 64 + lane] = make_float4(acc[mi][0], acc[mi][1], acc[mi][2], acc[mi][3]);
   }
-  if (wave == 0 && !early) lat_epi_loads<MI>(d, sub0, col, false, e);
+  if (wave == 0 && !early) lat_epi_loads<MI>(d, sub0, col, e);
   __syncthreads();
   if (wave != 0) return;
   lat_f32x4 sum[MI];
@@ -92,7 +232,7 @@ __global__ __launch_bounds__(512) void gemm_lat_wg_kernel(DmaDesc d, int n16, in
       for (int r = 0; r < 4; r++)
         sum[mi][r] = kb == 0 ? lat_first_block(d, vv[r], e.bias[mi][r]) : __fmaf_rn(vv[r], alpha, sum[mi][r]);
     }
-  lat_finish<MI>(d, sub0, col, e, sum, false);
+  lat_finish<MI>(d, sub0, col, e, sum);
 }
 
 // A[M, K] (row stride lda) -> [ceil(M/16)][nkb][16 groups][64 lanes] float4:
@@ -135,6 +275,7 @@ rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float*
 
 bool lat_variant_ok(int v) {
   if (v == 91 || v == 92) return true;  // workgroup fold
+  if (v == 71 || v == 72 || v == 74) return true;  // LDS-staged, RW = v - 70 rows x CW = 4 / RW columns
   const int wmw = v / 10, mi = v % 10;
   return (wmw == 1 || wmw == 2 || wmw == 4) && (mi == 1 || mi == 2);
 }
@@ -144,7 +285,9 @@ struct LatGrid {
   int64_t wgs, tiles;
 };
 static LatGrid lat_grid(int M, int N, int K, int v) {
-  const int wmw = v / 10, mi = v % 10, wnw = 4 / wmw;
+  // (LDS-staged variants: RW row tiles x CW column tiles per workgroup, one each per wave)
+  const bool lds = v >= 70 && v < 80;
+  const int wmw = lds ? v - 70 : v / 10, mi = lds ? 1 : v % 10, wnw = 4 / wmw;
   LatGrid g;
   g.subs = (M + 15) / 16;
   g.wg_m = (g.subs + wmw * mi - 1) / (wmw * mi);
@@ -162,7 +305,7 @@ DmaSplit lat_split_plan(int M, int N, int K, int v) {
   if (g.nkb < 2) return sp;
   sp.split_tiles = (int)g.tiles;
   sp.nkb = g.nkb;
-  sp.ws_floats = g.tiles * g.nkb * (v % 10) * 256;
+  sp.ws_floats = g.tiles * g.nkb * ((v >= 70 && v < 80) ? 1 : v % 10) * 256;
   sp.counters = g.tiles;
   return sp;
 }
@@ -173,7 +316,17 @@ static void lat_launch(const DmaDesc& d, const LatGrid& g, hipStream_t s) {
                      g.subs);
 }
 
-rtenhip_status launch_gemm_lat(const DmaDesc& d, int v, hipStream_t s) {
+rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
+  DmaDesc d = d0;
+  d.stamps = nullptr;
+  if (g_lat_stamps) {
+    const int64_t waves = v >= 90 ? 0 : lat_grid(d.M, d.N, d.K, v).wgs * 4;
+    if (waves > 0 && g_lat_stamps_used + waves <= g_lat_stamps_cap) {
+      d.stamps = g_lat_stamps + kLatStampWords * g_lat_stamps_used;
+      g_lat_stamps_used += waves;
+      d.dbg = (d.dbg & 0xff) | (++g_lat_seq << 8);
+    }
+  }
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty latency GEMM");
   if (!lat_variant_ok(v)) return fail(RTENHIP_INVALID_VALUE, "unknown latency GEMM variant");
   if (d.cin) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM: beta * C not supported");
@@ -195,6 +348,15 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d, int v, hipStream_t s) {
   const LatGrid g = lat_grid(d.M, d.N, d.K, v);
   if (g.wgs > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM grid too large");
   if (g.nkb > 1 && (!d.ws || !d.counters)) return fail(RTENHIP_INVALID_VALUE, "latency GEMM needs its K-block workspace");
+  if (v >= 70 && v < 80) {
+    if (d.kstride <= 0 && !d.k3x3) return fail(RTENHIP_UNSUPPORTED_VALUE, "LDS latency GEMM: 1x1 or 3x3 windows only");
+    const dim3 grid((unsigned)g.wgs), blk(256);
+    if (v == 71) hipLaunchKernelGGL((gemm_lat2_kernel<1, 4>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+    else if (v == 72) hipLaunchKernelGGL((gemm_lat2_kernel<2, 2>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+    else hipLaunchKernelGGL((gemm_lat2_kernel<4, 1>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   switch (v) {
     case 41: lat_launch<4, 1>(d, g, s); break;
     case 21: lat_launch<2, 1>(d, g, s); break;
@@ -208,3 +370,11 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d, int v, hipStream_t s) {
 }
 
 }  // namespace rtenhip
+
+extern "C" void rtenhip_debug_set_lat_stamps(void* buf, int64_t cap_waves) {
+  rtenhip::g_lat_stamps = static_cast<unsigned long long*>(buf);
+  rtenhip::g_lat_stamps_cap = cap_waves;
+  rtenhip::g_lat_stamps_used = 0;
+  rtenhip::g_lat_seq = 0;
+}
+extern "C" int64_t rtenhip_debug_lat_stamps_used() { return rtenhip::g_lat_stamps_used; }

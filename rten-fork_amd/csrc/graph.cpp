@@ -15,7 +15,6 @@
 //    hipEvent times aggregated by operator type.
 #include "graph.h"
 #include "gemm_dma.h"
-#include "chain.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -85,8 +84,6 @@ Plan::~Plan() {
   }
   for (auto& kv : padded)
     if (kv.second.base) (void)hipFree(kv.second.base);
-  for (auto& kv : dwpw_wt)
-    if (kv.second) (void)hipFree(kv.second);
   for (auto& kv : matmuls) {
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
@@ -100,24 +97,6 @@ Plan::~Plan() {
   }
   for (auto& kv : conv_unfused)
     if (kv.second.first) (void)hipFree(kv.second.first);
-
-  for (auto& kv : side_events) {
-    if (kv.second.first) (void)hipEventDestroy(kv.second.first);
-    if (kv.second.second) (void)hipEventDestroy(kv.second.second);
-  }
-  for (auto& c : chains) c.release();
-}
-
-void ConvChain::release() {
-  if (layers_dev) (void)hipFree(layers_dev);
-  if (ctrl) (void)hipFree(ctrl);
-  if (ws) (void)hipFree(ws);
-  for (float* b : packed) (void)hipFree(b);
-  layers_dev = nullptr;
-  ctrl = nullptr;
-  ws = nullptr;
-  packed.clear();
-  use = false;
 }
 
 // FusedTranspose: the permuted view of an operator input (PermuteSpec::apply,
@@ -178,7 +157,6 @@ Graph::~Graph() {
     if (kv.second.second) (void)hipFree(kv.second.second);
   }
   if (exec_stream) (void)hipStreamDestroy(exec_stream);
-  if (side_stream) (void)hipStreamDestroy(side_stream);
   if (ev_in) (void)hipEventDestroy(ev_in);
   if (ev_out) (void)hipEventDestroy(ev_out);
 }
@@ -795,8 +773,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (nodes[op].fused_residual >= 0) uses[nodes[op].fused_residual]++;
     auto ef = p.expand_fused.find(op);
     if (ef != p.expand_fused.end()) uses[ef->second]++;
-    auto dpf = p.dwpw_fused.find(op);
-    if (dpf != p.dwpw_fused.end()) uses[dpf->second]++;
   }
   std::set<int> outset(out_ids.begin(), out_ids.end());
 
@@ -838,31 +814,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.expand_fused[op] = e.inputs[0];
       drop.push_back(n.fe_op);
     }
-    // Depthwise -> project pairs (Node::dp_op): opt-in, RTENHIP_DWPW=1 (the
-    // fused kernel measured slower, see dwpw.hip).
-    const char* dpe = getenv("RTENHIP_DWPW");
-    for (int op : p.ops) {
-      const Node& n = nodes[op];
-      if (!dpe || atoi(dpe) <= 0) break;
-      if (n.op_type != "Conv" || n.dp_op < 0 || !in_plan.count(n.dp_op) || p.expand_fused.count(n.dp_op) ||
-          std::find(drop.begin(), drop.end(), n.dp_op) != drop.end())
-        continue;
-      const Node& dn = nodes[n.dp_op];
-      if (dn.outputs.size() != 1 || n.inputs[0] != dn.outputs[0] || outset0.count(dn.outputs[0]) ||
-          uses_of_value(p.ops, dn.outputs[0]) != 1)
-        continue;
-      const Shape* xs = shape_of(dn.inputs[0]);
-      const Shape& ys = shapes[n.outputs[0]];
-      if (!xs || xs->size() != 4 || ys.size() != 4 || p.dtypes[dn.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
-      ConvAttrs da = conv_attrs(dn, false);
-      if (da.mode != 0 || da.dil != std::vector<int64_t>{1, 1} || da.strides != std::vector<int64_t>{1, 1} ||
-          da.pads.size() != 4 || ys[2] != (*xs)[2] || ys[3] != (*xs)[3] || ys[0] != (*xs)[0] ||
-          !dw_pw_eligible((int)(*xs)[1], (int)(*xs)[2], (int)(*xs)[3], (int)ys[1], (int)da.pads[0], (int)da.pads[1],
-                          (int)da.pads[2], (int)da.pads[3]))
-        continue;
-      p.dwpw_fused[op] = dn.inputs[0];
-      drop.push_back(n.dp_op);
-    }
     if (!drop.empty()) {
       std::vector<int> kept;
       for (int op : p.ops)
@@ -872,7 +823,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   }
   for (int op : p.ops) {
     const Node& n = nodes[op];
-    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op) || p.dwpw_fused.count(op)) continue;
+    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op)) continue;
     const Shape* xs = shape_of(n.inputs[0]);
     const Shape* ws = shape_of(n.inputs[1]);
     if (!xs || !ws || nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
@@ -1136,68 +1087,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (!p.padded.empty()) RTENHIP_HIP_CHECK(hipDeviceSynchronize());
   }
 
-  // Independent branches: a DMA conv whose inputs were ready two or more ops
-  // before its plan position (the ResNet downsample conv: DFS visits it right
-  // before the conv3 that consumes it) moves up to just after its last
-  // producer and runs on the side stream, concurrently with the main chain;
-  // its first consumer joins it.  Only convs that need no ctx scratch.
-  bool side = side_stream_mode > 0;
-  if (side_stream_mode < 0) {
-    constexpr int64_t kSideStreamMaxBatch = 4;
-    side = !p.convs.empty();
-    for (auto& kv : p.convs) side = side && kv.second.g.N <= kSideStreamMaxBatch;
-  }
-  if (side) {
-    std::map<int, int> producer_op;
-    for (int op : p.ops)
-      for (int o : nodes[op].outputs) producer_op[o] = op;
-    std::vector<int> order = p.ops;
-    for (size_t i = 0; i < order.size(); i++) {
-      const int op = order[i];
-      auto cit = p.convs.find(op);
-      if (cit == p.convs.end() || cit->second.fc) continue;
-      const Node& n = nodes[op];
-      const ConvPlan& g = cit->second.g;
-      const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
-      if (has_pad && !p.padded.count(n.inputs[0])) continue;
-      int last = -1;
-      std::vector<int> deps(n.inputs.begin(), n.inputs.end());
-      if (n.fused_residual >= 0) deps.push_back(n.fused_residual);
-      for (int v : deps) {
-        if (v < 0) continue;
-        auto pit = producer_op.find(v);
-        if (pit == producer_op.end()) continue;
-        for (size_t j = 0; j < i; j++)
-          if (order[j] == pit->second) last = std::max(last, (int)j);
-      }
-      if ((int)i - last < 3) continue;
-      order.erase(order.begin() + i);
-      order.insert(order.begin() + last + 1, op);
-      p.side.insert(op);
-    }
-    p.ops = order;
-    for (int d : p.side) {
-      const int v = nodes[d].outputs[0];
-      bool joined = false;
-      bool after = false;
-      for (int op : p.ops) {
-        if (op == d) {
-          after = true;
-          continue;
-        }
-        if (!after) continue;
-        const Node& n = nodes[op];
-        bool reads = n.fused_residual == v;
-        for (int i : n.inputs) reads = reads || i == v;
-        if (reads) {
-          p.joins[op].push_back(d);
-          joined = true;
-          break;
-        }
-      }
-      if (!joined) p.joins[-1].push_back(d);  // graph output: joined at the end of run
-    }
-  }
   // conv3 + downsample pairs (Plan::conv_dual): a conv whose fused residual is
   // a DMA conv's output that nothing else reads.  The downsample's input then
   // stays allocated until the conv3 (which may read it, dual GEMM).
@@ -1209,14 +1098,14 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       const Node& n = nodes[op];
       auto c3 = p.convs.find(op);
       if (n.op_type != "Conv" || c3 == p.convs.end() || c3->second.fc || c3->second.g.groups != 1 ||
-          n.fused_residual < 0 || p.conv_unfused.count(op) || p.side.count(op) || !producer.count(n.fused_residual))
+          n.fused_residual < 0 || p.conv_unfused.count(op) || !producer.count(n.fused_residual))
         continue;
       const int v = n.fused_residual;
       const int ds = producer[v];
       const Node& dn = nodes[ds];
       auto cd = p.convs.find(ds);
       if (dn.op_type != "Conv" || cd == p.convs.end() || cd->second.fc || cd->second.g.groups != 1 ||
-          dn.fused_residual >= 0 || dn.fused_act || outset.count(v) || uses[v] != 1 || p.side.count(ds) ||
+          dn.fused_residual >= 0 || dn.fused_act || outset.count(v) || uses[v] != 1 ||
           p.conv_unfused.count(ds) || p.expand_fused.count(ds) || p.padded.count(v))
         continue;
       const ConvPlan& gd = cd->second.g;
@@ -1230,8 +1119,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       if (getenv("RTENHIP_DUAL_DEBUG")) fprintf(stderr, "dual pair: %s + %s\n", n.name.c_str(), dn.name.c_str());
     }
   }
-  // Inputs of a side op stay allocated until its join.
-  std::map<int, std::vector<int>> deferred_drops;  // join op -> values
 
   // Storage blocks with best-fit reuse; aliases share their base's block.
   struct Block {
@@ -1351,30 +1238,13 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       s.offset = off;
       p.slots[out] = s;
     }
-    if (p.side.count(op)) {
-      int join = -1;
-      for (auto& kv : p.joins)
-        for (int d : kv.second)
-          if (d == op) join = kv.first;
-      for (int i : n.inputs)
-        if (i >= 0) deferred_drops[join].push_back(i);
-      if (n.fused_residual >= 0) deferred_drops[join].push_back(n.fused_residual);
-    } else {
-      for (int i : n.inputs)
-        if (i >= 0) drop_use(i);
-      if (n.fused_residual >= 0) drop_use(n.fused_residual);
-      auto ef = p.expand_fused.find(op);
-      if (ef != p.expand_fused.end()) drop_use(ef->second);
-      auto dpf = p.dwpw_fused.find(op);
-      if (dpf != p.dwpw_fused.end()) drop_use(dpf->second);
-      auto cdu = p.conv_dual.find(op);
-      if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
-    }
-    auto dd = deferred_drops.find(op);
-    if (dd != deferred_drops.end()) {
-      for (int v : dd->second) drop_use(v);
-      deferred_drops.erase(dd);
-    }
+    for (int i : n.inputs)
+      if (i >= 0) drop_use(i);
+    if (n.fused_residual >= 0) drop_use(n.fused_residual);
+    auto ef = p.expand_fused.find(op);
+    if (ef != p.expand_fused.end()) drop_use(ef->second);
+    auto cdu = p.conv_dual.find(op);
+    if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
     // An output nobody reads is released right after its producer.
     if (block_of.count(out) && blocks[block_of[out]].refs == 0) {
       Block& b = blocks[block_of[out]];
@@ -1471,7 +1341,6 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
-  if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_pw(p, op_id);
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
   if (t == "MatMul" && p.mm_group_skip.count(op_id)) return RTENHIP_OK;  // computed by its group's leader
   if (t == "Conv" && p.conv_dual.count(op_id)) {
@@ -1710,33 +1579,6 @@ rtenhip_status Graph::exec_expand_dw(Plan& p, int op_id) {
                           ptr_of(p, n.outputs[0]), (int)xs[0], (int)xs[1], (int)ys[1], (int)xs[2], (int)xs[3],
                           (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0], (int)fp[1], e.fused_act, e.act_lo,
                           e.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
-}
-
-// Depthwise (3x3) -> project (1x1) pair (Node::dp_op) the plan runs as one
-// dwpw.hip launch, reading the depthwise conv's input.
-rtenhip_status Graph::exec_dw_pw(Plan& p, int op_id) {
-  const Node& n = nodes[op_id];
-  const Node& dn = nodes[n.dp_op];
-  const int xv = p.dwpw_fused[op_id];
-  const Shape* xsp = plan_shape(*this, p, xv);
-  const Shape* ysp = plan_shape(*this, p, n.outputs[0]);
-  if (!xsp || !ysp) return fail(RTENHIP_HIP_ERROR, "depthwise+pointwise: missing shapes");
-  const Shape& xs = *xsp;
-  const Shape& ys = *ysp;
-  const int64_t C = xs[1], M = ys[1];
-  float*& wt = p.dwpw_wt[op_id];
-  if (!wt) {  // first (eager) run: the project weights transposed to [C][Mpad]
-    RTENHIP_HIP_CHECK(hipMalloc(&wt, (size_t)pw_weight_floats(M, C) * 4));
-    rtenhip_status st = pack_pw_weights(ptr_of(p, n.inputs[1]), M, C, wt, ctx->stream);
-    if (st) return st;
-  }
-  const float* bd = dn.inputs.size() > 2 && dn.inputs[2] >= 0 ? ptr_of(p, dn.inputs[2]) : nullptr;
-  const float* bp = n.inputs.size() > 2 && n.inputs[2] >= 0 ? ptr_of(p, n.inputs[2]) : nullptr;
-  const float* res = n.fused_residual >= 0 ? ptr_of(p, n.fused_residual) : nullptr;
-  ConvAttrs da = conv_attrs(dn, false);
-  return launch_dw_pw(ptr_of(p, xv), ptr_of(p, dn.inputs[1]), bd, wt, bp, res, ptr_of(p, n.outputs[0]), (int)xs[0],
-                      (int)C, (int)xs[2], (int)xs[3], (int)M, (int)da.pads[0], (int)da.pads[1], dn.fused_act, dn.act_lo,
-                      dn.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -2052,8 +1894,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       chosen_split = twin->split;
       chosen_persist = twin->persist;
     } else if (autotune && cs == hipStreamCaptureStatusNone && da.residual != da.out) {
-      // Candidates are timed alone: a side-stream branch still running would
-      // share the CUs and skew the choice.
+      // Candidates are timed alone, after the work queued before them.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
       static const int kCandidates[] = {0, 1, 2, 3, 4, 6, 7, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24};
       MatMulExec trial = me;
@@ -2260,8 +2101,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   auto pout = p.padded.find(n.outputs[0]);
   const float* w = ptr_of(p, n.inputs[1]);
   const int64_t opg = g.O / g.groups, K = (g.C / g.groups) * g.kh * g.kw;
-  // KC-split buffers for (cfg, split), plan-owned (no ctx scratch, so side-
-  // stream convs never share them).
+  // KC-split buffers for (cfg, split), plan-owned.
   auto set_split = [&](ConvExec& e, int cfg, bool split) -> rtenhip_status {
     e.split = false;
     if (!split) return RTENHIP_OK;
@@ -2342,14 +2182,16 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
                            (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32)) ||
                            (direct_lds_ok && (pw_valu_mode == kPwDirect + 116 || pw_valu_mode == kPwDirect + 132));
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
-    const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode);
+    // gemm_lat2_kernel (variants 7x) forms 1x1 and 3x3 window offsets only.
+    const bool lds_ok = ((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3)) && !getenv("RTENHIP_LAT_KTAB");
+    const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode) &&
+                            (lds_ok || lat_mode < 70 || lat_mode >= 80);
     if (lat_forced) {
       chosen = kLatCfgBase + lat_mode;
       chosen_split = true;
     }
     if (autotune && cs == hipStreamCaptureStatusNone && !pw_forced && !lat_forced) {
-      // Candidates are timed alone: a side-stream branch still running would
-      // share the CUs and skew the choice.
+      // Candidates are timed alone, after the work queued before them.
       RTENHIP_HIP_CHECK(hipDeviceSynchronize());
       static const int kCandidates[] = {7, 13, 14, 15, 16, 17, 0, 1, 2, 3, 4, 8, 9, 10, 19, 20, 21, 22, 23, 24};
       ConvExec trial;  // split buffers reused across candidates
@@ -2413,8 +2255,9 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Latency GEMM variants (small batches: one wave per 16x16 tile and KC
       // block); their K-block fold is part of the kernel (split always on).
       if (lat_mode != 0) {
-        for (int v : {41, 21, 11, 42, 22, 12, 91, 92}) {
+        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74}) {
           if (lat_mode > 0 && v != lat_mode) continue;
+          if (v >= 70 && v < 80 && !lds_ok) continue;
           const int cfg = kLatCfgBase + v;
           float* pk = nullptr;
           RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
@@ -2787,7 +2630,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   hipStream_t caller = ctx->stream;
   if (!exec_stream) {
     RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&exec_stream, hipStreamNonBlocking));
-    RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
     RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
   }
@@ -2817,7 +2659,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
                   : kv.second * sizeof(float) > ctx->slot_cap[kv.first] || !ctx->slots[kv.first];
     if (grow) {
       RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
-      RTENHIP_HIP_CHECK(hipStreamSynchronize(side_stream));
       if (!ctx->reserve_scratch(plan->scratch_need))
         return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
     }
@@ -2830,65 +2671,11 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   plan->bound_in = bin;
   plan->bound_out = bout;
 
-  for (int d : plan->side) {
-    auto& ev = plan->side_events[d];
-    if (!ev.first) RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev.first, hipEventDisableTiming));
-    if (!ev.second) RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev.second, hipEventDisableTiming));
-  }
   RTENHIP_HIP_CHECK(hipEventRecord(ev_in, caller));
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, ev_in, 0));
   ctx->stream = exec_stream;
   rtenhip_status st = RTENHIP_OK;
-  // Conv chains: formed once the first (tuning) run has chosen each conv's
-  // kernel, and again whenever the arena moved (descriptors hold its pointers).
-  if (plan->eager_runs >= 1 && (!plan->chains_built || plan->chains_arena != arena)) {
-    if (plan->exec) {
-      (void)hipGraphExecDestroy(plan->exec);
-      plan->exec = nullptr;
-      same_binding = false;
-    }
-    st = build_chains(*plan);
-    if (st) {
-      ctx->stream = caller;
-      return st;
-    }
-  }
-  // One op, or the chain it heads (the chain's other members are skipped).
-  auto run_op = [&](int op) -> rtenhip_status {
-    auto ci = plan->chain_of.find(op);
-    if (ci != plan->chain_of.end() && plan->chains[ci->second].use) {
-      ConvChain& c = plan->chains[ci->second];
-      return op == c.ops[0] ? exec_chain(*plan, c) : RTENHIP_OK;
-    }
-    return exec_op(*plan, op);
-  };
-  // Launch one op on its stream: side ops fork from the main stream and
-  // record completion; a join op first waits for the side ops it reads.
-  // Timing runs keep every op on the main stream so per-op times do not
-  // include concurrent work.
-  auto on_side = [&](int op) { return !timing && plan->side.count(op) > 0; };
-  auto stream_of = [&](int op) { return on_side(op) ? side_stream : exec_stream; };
-  auto before_op = [&](int op) -> rtenhip_status {
-    if (on_side(op)) {
-      auto& ev = plan->side_events[op];
-      RTENHIP_HIP_CHECK(hipEventRecord(ev.first, exec_stream));
-      RTENHIP_HIP_CHECK(hipStreamWaitEvent(side_stream, ev.first, 0));
-      ctx->stream = side_stream;
-    } else if (!timing) {
-      auto j = plan->joins.find(op);
-      if (j != plan->joins.end())
-        for (int d : j->second)
-          RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, plan->side_events[d].second, 0));
-    }
-    return RTENHIP_OK;
-  };
-  auto after_op = [&](int op) -> rtenhip_status {
-    if (on_side(op)) {
-      RTENHIP_HIP_CHECK(hipEventRecord(plan->side_events[op].second, side_stream));
-      ctx->stream = exec_stream;
-    }
-    return RTENHIP_OK;
-  };
+  auto run_op = [&](int op) -> rtenhip_status { return exec_op(*plan, op); };
   // Outputs that no operator writes (a constant, e.g. after constant
   // propagation, or a plan-time value) are copied into the caller's buffers
   // at the end of the run.
@@ -2908,14 +2695,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
     return RTENHIP_OK;
   };
-  auto join_all = [&]() -> rtenhip_status {
-    if (timing) return RTENHIP_OK;
-    auto j = plan->joins.find(-1);
-    if (j != plan->joins.end())
-      for (int d : j->second)
-        RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, plan->side_events[d].second, 0));
-    return RTENHIP_OK;
-  };
   plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
   plan->pk_ready.clear();
   if (replay) {
@@ -2927,13 +2706,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       hipGraph_t g = nullptr;
       hipError_t e = hipStreamBeginCapture(exec_stream, hipStreamCaptureModeThreadLocal);
       if (e == hipSuccess) {
-        for (int op : plan->ops) {
-          st = before_op(op);
-          if (!st) st = run_op(op);
-          if (!st) st = after_op(op);
-          if (st) break;
-        }
-        if (!st) st = join_all();
+        for (int op : plan->ops)
+          if ((st = run_op(op))) break;
         if (!st) st = copy_static_outputs();
         ctx->stream = exec_stream;
         hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
@@ -2954,21 +2728,18 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     ctx->scratch_log = &plan->scratch_need;
     for (int op : plan->ops) {
       hipEvent_t a = nullptr, b = nullptr;
-      st = before_op(op);
-      if (st) break;
       // (a downsample computed by its conv3's dual GEMM launches nothing: no events)
       const bool timed = timing && !plan->dual_skip.count(op);
       if (timed) {
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
-        (void)hipEventRecord(a, stream_of(op));
+        (void)hipEventRecord(a, exec_stream);
       }
       st = run_op(op);
       if (timing) {
-        if (timed) (void)hipEventRecord(b, stream_of(op));
+        if (timed) (void)hipEventRecord(b, exec_stream);
         evs.push_back({a, b});
       }
-      if (!st) st = after_op(op);
       if (st) {
         std::string msg = "Operator \"" + nodes[op].name + "\" failed: " + rtenhip_last_error_message();
         set_error(st, msg);
@@ -2977,21 +2748,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
     ctx->scratch_log = nullptr;
     ctx->stream = exec_stream;
-    if (!st) st = join_all();
     if (!st) st = copy_static_outputs();
     plan->eager_runs++;
-    // Eager runs check their chains' error word (a dependency wait that timed
-    // out means the grid was not resident; the outputs are not valid).
-    for (ConvChain& c : plan->chains) {
-      if (st || !c.use) continue;
-      int err = 0;
-      if (hipMemcpyAsync(&err, c.ctrl + chain_error_index((int)c.ops.size()), 4, hipMemcpyDeviceToHost,
-                         exec_stream) != hipSuccess ||
-          hipStreamSynchronize(exec_stream) != hipSuccess)
-        st = fail(RTENHIP_HIP_ERROR, "conv chain check failed");
-      else if (err)
-        st = fail(RTENHIP_HIP_ERROR, "conv chain: a dependency wait timed out");
-    }
     if (timing && !st) {
       (void)hipStreamSynchronize(exec_stream);
       std::map<std::string, std::pair<double, int>> tot;
@@ -3007,13 +2765,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
             (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0))
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
-        auto ci = plan->chain_of.find(plan->ops[i]);
-        if (ci != plan->chain_of.end() && plan->chains[ci->second].use)
-          key = plan->chains[ci->second].ops[0] == plan->ops[i] ? "ConvChain" : "Conv(chained)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
-        if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+pw)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -3036,12 +2790,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         os << buf;
       }
       // Per-op rows (RTEN_TIMING "by-shape" analogue): name, type, output shape.
-      for (const ConvChain& c : plan->chains) {
-        snprintf(buf, sizeof buf, "conv chain %s .. %s (%zu convs, %d units, grid %d): %.4f ms as one launch, %.4f ms one by one%s\n",
-                 nodes[c.ops.front()].name.c_str(), nodes[c.ops.back()].name.c_str(), c.ops.size(), c.items, c.grid,
-                 c.chain_ms, c.ops_ms, c.use ? " (used)" : " (not used)");
-        os << buf;
-      }
       os << "--- per op ---\n";
       for (size_t i = 0; i < evs.size(); i++) {
         const Node& n = nodes[plan->ops[i]];
@@ -3309,40 +3057,6 @@ rtenhip_status Graph::optimize() {
     dn.fe_op = i;
     fused++;
   }
-  // MobileNetV2 inverted residual, back half: depthwise 3x3 Conv (+ its fused
-  // activation) whose only consumer is a 1x1 Conv (the project conv, with its
-  // fused residual / activation) -> the 1x1 node runs both (dwpw.hip).  The
-  // plan decides on shapes; a depthwise conv the plan runs with its expand
-  // conv (Node::fe_op) stays apart from its project conv.
-  for (int i = 0; i < (int)nodes.size(); i++) {
-    Node& dn = nodes[i];
-    if (dn.kind != NodeKind::Operator || dn.removed || dn.op_type != "Conv" || dn.fused_residual >= 0 ||
-        dn.outputs.size() != 1 || dn.inputs.size() < 2 || !dn.input_perm.empty())
-      continue;
-    const int dw = dn.inputs[1];
-    if (dw < 0 || nodes[dw].kind != NodeKind::Constant || nodes[dw].shape.size() != 4) continue;
-    const int64_t C = nodes[dw].shape[0];
-    if (nodes[dw].shape != Shape{C, 1, 3, 3} || (int64_t)dn.attrs.num("groups", 1) != C ||
-        (dn.inputs.size() > 2 && dn.inputs[2] >= 0 && nodes[dn.inputs[2]].kind != NodeKind::Constant))
-      continue;
-    const int p_op = sole(dn.outputs[0]);
-    if (p_op < 0) continue;
-    Node& pn = nodes[p_op];
-    if (pn.removed || pn.op_type != "Conv" || pn.dp_op >= 0 || pn.inputs.size() < 2 || pn.inputs[0] != dn.outputs[0] ||
-        !pn.input_perm.empty())
-      continue;
-    const int pw = pn.inputs[1];
-    if (pw < 0 || nodes[pw].kind != NodeKind::Constant || nodes[pw].shape.size() != 4 || nodes[pw].shape[1] != C ||
-        nodes[pw].shape[2] != 1 || nodes[pw].shape[3] != 1 ||
-        (pn.inputs.size() > 2 && pn.inputs[2] >= 0 && nodes[pn.inputs[2]].kind != NodeKind::Constant))
-      continue;
-    ConvAttrs pa = conv_attrs(pn, false);
-    if (pa.mode != 0 || pa.groups != 1 || pa.pads != std::vector<int64_t>{0, 0, 0, 0} ||
-        pa.strides != std::vector<int64_t>{1, 1} || pa.dil != std::vector<int64_t>{1, 1})
-      continue;
-    pn.dp_op = i;
-    fused++;
-  }
   // FusedTranspose (optimize.rs:329-378): a MatMul reads a Transpose's input
   // as a permuted view instead of the materialised copy.  The Transpose stays
   // in the graph and is only planned if something else still reads it.
@@ -3514,11 +3228,9 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTEN_TIMING")) g->timing = s[0] != 0 && s[0] != '0';
   if (const char* s = getenv("RTENHIP_GRAPH")) g->use_hip_graph = s[0] != '0';
   if (const char* s = getenv("RTENHIP_TUNE")) g->autotune = s[0] != '0';
-  if (const char* s = getenv("RTENHIP_SIDE_STREAM")) g->side_stream_mode = atoi(s) > 0 ? 1 : (atoi(s) < 0 ? -1 : 0);
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   if (const char* s = getenv("RTENHIP_LAT")) g->lat_mode = atoi(s);
-  if (const char* s = getenv("RTENHIP_CHAIN")) g->chain_mode = atoi(s);
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

@@ -105,11 +105,6 @@ struct Node {
   // fused kernel takes (mbconv.hip) drops that op and runs both here, reading
   // the expand's input; otherwise both run as they are.
   int fe_op = -1;
-  // MobileNetV2's depthwise -> project pair (Graph::optimize): the 3x3
-  // depthwise Conv (+ its fused activation) whose only consumer is this 1x1
-  // Conv.  A plan whose shapes the fused kernel takes (dwpw.hip) drops that op
-  // and runs both here, reading the depthwise conv's input.
-  int dp_op = -1;
   // MatMul epilogue: constant [N] added per column after the K fold
   // (MatMul -> Add(bias)), before the residual and the activation.
   int fused_colbias = -1;
@@ -178,22 +173,6 @@ struct PaddedValue {
   Shape phys;
 };
 
-// A run of consecutive convs of a plan executed by one persistent launch of
-// latency-GEMM units (conv_chain.hip).  Built after the plan's first (eager,
-// tuning) run and kept when it times faster than the same convs one by one.
-struct ConvChain {
-  std::vector<int> ops;         // plan ops, in plan order; ops[0] launches the chain
-  void* layers_dev = nullptr;   // ChainLayer[ops.size()]
-  int* ctrl = nullptr;          // control words (chain.h), zeroed per launch
-  size_t ctrl_bytes = 0;
-  float* ws = nullptr;          // split-K workspaces of all layers
-  std::vector<float*> packed;   // chain-owned buffers: lat-packed weights, private activations
-  int items = 0, grid = 0;
-  bool use = false;
-  float chain_ms = 0, ops_ms = 0;  // build-time comparison
-  void release();
-};
-
 struct Plan {
   ~Plan();
   // Kernel knobs the plan was made under (Graph::find_plan matches them):
@@ -212,9 +191,6 @@ struct Plan {
   // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
   // the expand's input value, which the depthwise op then reads.
   std::map<int, int> expand_fused;
-  // Pointwise convs running their depthwise producer too (Node::dp_op): op id
-  // -> the depthwise input value; and their transposed weights (plan-owned).
-  std::map<int, int> dwpw_fused;
   // Grouped MatMuls (MatMulExec::nseg): leader op -> members (leader first),
   // members run by their leader; the members' outputs are segments of one
   // arena block of [nseg][M][N].
@@ -224,7 +200,6 @@ struct Plan {
   // reads as A: the attention kernel also stores it packed (Plan::pk_cons).
   std::map<int, int> attn_pk;
   std::set<int> attn_pk_only;  // ... and nothing reads its row-major output
-  std::map<int, float*> dwpw_wt;
   // ResNet's conv3 + downsample pairs: conv3 op -> downsample op (its fused
   // residual's producer, read by nothing else).  On the first run conv3 times
   // the dual GEMM (gemm_dma_kernel DUAL, both convs in one launch) against
@@ -258,11 +233,6 @@ struct Plan {
   std::set<int> pk_only;
   std::map<int, std::pair<float*, int64_t>> pk_buf;
   std::map<int, DmaTile> pk_ready;
-  // Ops launched on the side stream (independent branches such as the
-  // ResNet downsample conv), and for each op the side ops it must wait for.
-  std::set<int> side;
-  std::map<int, std::vector<int>> joins;
-  std::map<int, std::pair<hipEvent_t, hipEvent_t>> side_events;  // op -> (fork, done)
   std::map<int, Slot> slots;          // value id -> storage
   size_t arena_bytes = 0;
   std::vector<int> input_ids, output_ids;
@@ -293,12 +263,6 @@ struct Plan {
   uint64_t scratch_gen = 0;                // Ctx::scratch_gen when exec was captured
   std::map<size_t, size_t> scratch_need;   // ctx scratch slot -> floats (eager runs)
   int eager_runs = 0;
-  // Conv chains (see ConvChain) and the chain of each member op; built once
-  // per arena (the layer descriptors hold arena pointers).
-  std::vector<ConvChain> chains;
-  std::map<int, int> chain_of;
-  bool chains_built = false;
-  void* chains_arena = nullptr;
 };
 
 struct Graph {
@@ -315,20 +279,12 @@ struct Graph {
   void* arena = nullptr;
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
-  hipStream_t side_stream = nullptr;
-  // Downsample branches on a second stream: 1 always, 0 never (default), -1
-  // for plans whose image batch is at most kSideStreamMaxBatch.  Measured
-  // slower at both ends: 0.5% on ResNet-50 b64 (the concurrent kernels were
-  // tuned alone) and 5% at batch 1 (0.591 -> 0.623 ms, the cross-stream
-  // event waits cost more than the overlap gains).  RTENHIP_SIDE_STREAM.
-  int side_stream_mode = 0;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
   bool use_hip_graph = true;
   bool autotune = true;  // time DMA conv configurations on a plan's first run
   int persist_mode = -1; // DMA GEMM launches: -1 tuned, 0 never persistent, k: always, k blocks/CU
   int lat_mode = -1;     // latency GEMM convs (gemm_lat.hip): -1 tuned, 0 never, v > 0 forced variant
-  int chain_mode = 0;    // conv chains: -1 kept when faster, 0 never (default: measured slower), 1 always (RTENHIP_CHAIN)
   int pw_valu_mode = -1; // pointwise convs on the VALU kernel: -1 tuned, 0 never, v > 0 forced variant (pw_variant_ok)
   std::string timing_report;
   std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
@@ -379,10 +335,7 @@ struct Graph {
   // choice between it and the unfused pair.
   rtenhip_status exec_conv_dual(Plan& p, int op_id, bool& handled);
   void conv_io_args(Plan& p, int op_id, ConvDmaArgs& a);
-  rtenhip_status build_chains(Plan& p);
-  rtenhip_status exec_chain(Plan& p, ConvChain& c);
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
-  rtenhip_status exec_dw_pw(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   // The packed-A store a producer of value v makes this run, or false.

@@ -1,4 +1,4 @@
-// Building blocks of the latency GEMM (gemm_lat.hip, conv_chain.hip): a wave
+// Building blocks of the latency GEMM (gemm_lat.hip): a wave
 // computes the chains of a (16*MI) x 16 output tile for one KC block
 // (lat_chain); the blocks of a tile are folded in K order either by the last
 // block to arrive through a global workspace (lat_unit) or inside one
@@ -18,18 +18,11 @@ namespace rtenhip {
 typedef float lat_f32x4 __attribute__((ext_vector_type(4)));
 constexpr int LKC = 256;           // the reference's KC block
 constexpr int LGROUPS = LKC / 16;  // 16-k groups per block (4 MFMA steps each)
-constexpr int kLoadSc1 = 16;       // buffer-load cache policy: sc1 (L1 bypass, see conv_chain.hip)
 
 __device__ __forceinline__ float lat_f4(const float4& v, int j) {
   return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w;
 }
 
-struct LatNoWait {
-  __device__ void operator()() const {}
-};
-struct LatNoDone {
-  __device__ void operator()() const {}
-};
 
 // The output column of this lane (c = lane % 16) of a tile starting at n0,
 // and its x offset colbase(n) in bytes (DMA_OOB past N).
@@ -53,13 +46,11 @@ __device__ __forceinline__ LatCol lat_col(const DmaDesc& d, int n0) {
 }
 
 // The chains of KC block kb: acc[mi] = fma chains over the block's k, from
-// +0.  ktl: this wave's 256-word LDS slot.  wait() runs once the weight and
-// K-table loads are in flight and before the first load of x.  sc1_ld: x is
-// read with sc1 loads (chain hand-offs).
-template <int MI, typename Wait>
+// +0.  ktl: this wave's 256-word LDS slot.
+template <int MI>
 __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, const int kb, const int nkb, const int subs,
-                                          const LatCol& col, uint32_t* ktl, Wait wait, const bool sc1_ld,
-                                          lat_f32x4 (&acc)[MI]) {
+                                          const LatCol& col, uint32_t* ktl,
+                                          lat_f32x4 (&acc)[MI], const bool drain = false) {
   const int lane = threadIdx.x & 63;
   const int h = lane >> 4;
   const int K = d.K;
@@ -105,55 +96,52 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
     asm volatile("" ::: "memory");
   }
 
-  // A: packed [subtile][kb][group][lane] float4 (launch_pack_lat).
-  const float4* __restrict__ ap = reinterpret_cast<const float4*>(d.apk);
-  float4 av[LGROUPS][MI];
+  // A: packed [subtile][kb][group][lane] float4 (launch_pack_lat: zero past
+  // K inside a block); subtiles past M read past the buffer, which returns 0.
+  // Every load below is issued unconditionally, A then B, so a unit pays one
+  // memory round trip (a guarded load would be a branch and a wait each).
+  typedef unsigned int lat_u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t ar =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, (int)((int64_t)subs * nkb * LGROUPS * 64 * 16), 0x00020000);
+  lat_u32x4 av[LGROUPS][MI];
 #pragma unroll
   for (int g = 0; g < LGROUPS; g++)
 #pragma unroll
     for (int mi = 0; mi < MI; mi++) {
-      av[g][mi] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (g < ng && sub0 + mi < subs)
-        av[g][mi] = ap[(((int64_t)(sub0 + mi) * nkb + kb) * LGROUPS + g) * 64 + lane];
+      const uint32_t off = (sub0 + mi < subs && g < ng)
+                               ? (uint32_t)((((sub0 + mi) * nkb + kb) * LGROUPS + g) * 64 + lane) * 16u
+                               : DMA_OOB;
+      av[g][mi] = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
     }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
-
-  wait();
 
   // B: step s = 4g + j covers k = k0 + 4s + h for this lane.
   float bv[LKC / 4];
 #pragma unroll
   for (int g = 0; g < LGROUPS; g++) {
-    bv[4 * g] = bv[4 * g + 1] = bv[4 * g + 2] = bv[4 * g + 3] = 0.f;
-    if (g < ng) {
-      uint32_t ko[4];
-      if (linear) {
+    uint32_t ko[4];
+    if (linear || k3) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int k = k0 + 16 * g + 4 * j + h;
-          ko[j] = k < K ? (uint32_t)k * (uint32_t)d.kstride * 4u : DMA_OOB;
-        }
-      } else if (k3) {
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int st = 4 * g + j;
-          const int k = k0 + 16 * g + 4 * j + h;
-          ko[j] = k < K ? k3off[st % 9] + (uint32_t)(st / 9) * k3step : DMA_OOB;
-        }
-      } else {
-        const uint4 t = *(const uint4*)&ktl[h * 64 + 4 * g];
-        ko[0] = t.x;
-        ko[1] = t.y;
-        ko[2] = t.z;
-        ko[3] = t.w;
+      for (int j = 0; j < 4; j++) {
+        const int st = 4 * g + j;
+        const int k = k0 + 16 * g + 4 * j + h;
+        const uint32_t lin = (uint32_t)k * (uint32_t)d.kstride * 4u;
+        const uint32_t win = k3off[st % 9] + (uint32_t)(st / 9) * k3step;
+        ko[j] = k < K ? (linear ? lin : win) : DMA_OOB;
       }
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        bv[4 * g + j] = __uint_as_float(sc1_ld ? __builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + ko[j], 0, kLoadSc1)
-                                               : __builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + ko[j], 0, 0));
+    } else {
+      const uint4 t = *(const uint4*)&ktl[h * 64 + 4 * g];  // DMA_OOB past K (padded table)
+      ko[0] = t.x;
+      ko[1] = t.y;
+      ko[2] = t.z;
+      ko[3] = t.w;
     }
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      bv[4 * g + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + ko[j], 0, 0));
   }
 
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // timing experiments only
 #pragma unroll
   for (int mi = 0; mi < MI; mi++) acc[mi] = (lat_f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -163,13 +151,13 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
       for (int j = 0; j < 4; j++)
 #pragma unroll
         for (int mi = 0; mi < MI; mi++)
-          acc[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(lat_f4(av[g][mi], j), bv[4 * g + j], acc[mi], 0, 0, 0);
+          acc[mi] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(av[g][mi][j]), bv[4 * g + j], acc[mi], 0, 0, 0);
     }
   }
 }
 
 // Epilogue operands of this lane's accumulator elements: the row bias and the
-// residual (sc1 loads for chain hand-offs).  Element r of lane (c, h) is row
+// residual.  Element r of lane (c, h) is row
 // 4h + r, column c.
 template <int MI>
 struct LatEpi {
@@ -177,7 +165,7 @@ struct LatEpi {
   float cbv;
 };
 template <int MI>
-__device__ __forceinline__ void lat_epi_loads(const DmaDesc& d, const int sub0, const LatCol& col, const bool sc1_ld,
+__device__ __forceinline__ void lat_epi_loads(const DmaDesc& d, const int sub0, const LatCol& col,
                                               LatEpi<MI>& e) {
   const int h = (threadIdx.x & 63) >> 4;
   const int64_t rbase = (int64_t)col.img * d.res_img + col.p;
@@ -191,7 +179,7 @@ __device__ __forceinline__ void lat_epi_loads(const DmaDesc& d, const int sub0, 
       e.res[mi][r] = 0.f;
       if (d.residual && col.n < d.N) {
         const float* rp = d.residual + rbase + (int64_t)mc * d.res_c;
-        e.res[mi][r] = sc1_ld ? __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *rp;
+        e.res[mi][r] = *rp;
       }
     }
   e.cbv = (d.colbias && col.n < d.N) ? d.colbias[col.p] : 0.f;
@@ -207,7 +195,7 @@ __device__ __forceinline__ float lat_first_block(const DmaDesc& d, float a, floa
 // Column bias, residual, activation and the store of the folded tile.
 template <int MI>
 __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, const LatCol& col, const LatEpi<MI>& e,
-                                           const lat_f32x4 (&sum)[MI], const bool sc1_st) {
+                                           const lat_f32x4 (&sum)[MI]) {
   const int h = (threadIdx.x & 63) >> 4;
   const bool act_relu = d.act == RTENHIP_ACT_RELU, act_clip = d.act == RTENHIP_ACT_CLIP;
   const bool act_gelu = d.act == RTENHIP_ACT_GELU;
@@ -229,43 +217,51 @@ __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, con
         const float cl = x < lo ? lo : (x > hi ? hi : x);
         x = act_relu ? rl : (act_clip ? cl : x);
       }
-      if (m < d.M) {
-        float* op = d.out + obase + (int64_t)m * d.out_c;
-        if (sc1_st)
-          __hip_atomic_store(op, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          *op = x;
-      }
+      if (m < d.M) d.out[obase + (int64_t)m * d.out_c] = x;
     }
 }
 
-// One unit (sub0: first 16-row subtile, n0: first column, kb: KC block, wt:
-// the tile's index into ws / counters) with the global fold: with K > 256
-// this block's chains go to the workspace ([tile][kb][mi][lane] x 16 bytes,
-// 8-byte agent-scope stores), drained before the arrival count, and the last
-// block of the tile to arrive folds all chains in K order.  wait(): see
-// lat_chain.  CHAIN: x and the residual are read with sc1 loads, the output is
-// stored sc1 and drained, and the wave that stored the tile then calls done()
-// (the inter-layer hand-off of conv_chain.hip).
-template <int MI, bool CHAIN, typename Wait, typename Done>
-__device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const int n0, const int kb, const int nkb,
-                                         const int subs, const int wt, uint32_t* ktl, Wait wait, Done done,
-                                         int dbg = 0) {
-  // dbg (timing experiments only, results not valid across XCDs): bit 0 plain
-  // x / residual loads, bit 1 plain output stores.
-  const bool sc1_ld = CHAIN && !(dbg & 1), sc1_st = CHAIN && !(dbg & 2);
+// Timing experiments only (rtenhip_debug_set_lat_stamps; d.stamps null in
+// every product launch): per wave kLatStampWords u64 = {launch seq << 48 |
+// XCC << 40 | hw id bits << 32 | kb << 16 | wave-in-grid low 16 bits, t_entry,
+// t_loaded, t_chain, t_arrived, t_folded, t_end, sub0 << 32 | n0, then for the
+// LDS-staged kernel t_a_landed, t_b_landed}, s_memrealtime (100 MHz).
+constexpr int kLatStampWords = 10;
+struct LatStamps {
+  unsigned long long* p = nullptr;
+  __device__ __forceinline__ void at(int i) {
+    if (p && (threadIdx.x & 63) == 0) p[i] = __builtin_amdgcn_s_memrealtime();
+  }
+};
+__device__ __forceinline__ LatStamps lat_stamps_init(const DmaDesc& d, int kb, int sub0, int n0) {
+  LatStamps st;
+  if (!d.stamps) return st;
+  const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  st.p = d.stamps + kLatStampWords * (size_t)gw;
+  if ((threadIdx.x & 63) == 0) {
+    unsigned xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    st.p[0] = ((unsigned long long)((unsigned)d.dbg >> 8) << 48) | ((unsigned long long)(xcc & 0xff) << 40) |
+              ((unsigned long long)((hw >> 8) & 0xff) << 32) | ((unsigned long long)(kb & 0xffff) << 16) | (gw & 0xffff);
+    st.p[7] = ((unsigned long long)(unsigned)sub0 << 32) | (unsigned)n0;
+    for (int i = 2; i < kLatStampWords; i++)
+      if (i != 7) st.p[i] = 0;
+  }
+  st.at(1);
+  return st;
+}
+
+// The K-block fold of one unit's chains and the tile's epilogue: with
+// nkb == 1 directly; else the chains go to the workspace ([tile][kb][mi][lane]
+// x 16 bytes, 8-byte agent-scope stores), drained before the arrival count,
+// and the last block of the tile to arrive folds all chains in K order.
+// Returns false for a unit that did not store the tile.
+template <int MI>
+__device__ __forceinline__ bool lat_fold_finish(const DmaDesc& d, const int sub0, const int kb, const int nkb,
+                                                const int wt, const LatCol& col, const LatEpi<MI>& e,
+                                                const lat_f32x4 (&acc)[MI], LatStamps& stp) {
   const int lane = threadIdx.x & 63;
-  const LatCol col = lat_col(d, n0);
-  // Epilogue operands, issued before any store (vmcnt retires in order); a
-  // standalone launch issues them with the operand loads (one memory round
-  // trip fewer on the unit's path), a chain after its dependency wait.
-  // (d.dbg & 4: A/B experiments only, the loads after the chain.)
-  const bool early = !CHAIN && !(d.dbg & 4);
-  LatEpi<MI> e;
-  if (early) lat_epi_loads<MI>(d, sub0, col, false, e);
-  lat_f32x4 acc[MI];
-  lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, wait, sc1_ld, acc);
-  if (!early) lat_epi_loads<MI>(d, sub0, col, sc1_ld, e);
   const float alpha = d.alpha;
 
   lat_f32x4 sum[MI];
@@ -290,7 +286,8 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
     int prev = 0;
     if (lane == 0) prev = __hip_atomic_fetch_add(d.counters + wt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     prev = __builtin_amdgcn_readfirstlane(prev);
-    if (prev != nkb - 1) return;
+    stp.at(4);
+    if (prev != nkb - 1) return false;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler ordering only
     auto ldq = [&](int64_t i) { return __hip_atomic_load(wsq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     constexpr int FG = 16;  // chains loaded per round
@@ -323,14 +320,42 @@ __device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const
       }
     }
     if (lane == 0) __hip_atomic_store(d.counters + wt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (stp.p) {
+      asm volatile("" ::"v"(sum[0][0]));
+      stp.at(5);
+    }
   }
 
-  lat_finish<MI>(d, sub0, col, e, sum, sc1_st);
-  if (CHAIN) {
-    // Every store of the tile drained, then one lane publishes it.
+  lat_finish<MI>(d, sub0, col, e, sum);
+  if (stp.p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    done();
+    stp.at(6);
   }
+  return true;
+}
+
+// One unit (sub0: first 16-row subtile, n0: first column, kb: KC block, wt:
+// the tile's index into ws / counters): the epilogue operands and the block's
+// operands in flight together (one memory round trip), the chains, then
+// lat_fold_finish.  (d.dbg & 4: A/B experiments only, the epilogue operands
+// loaded after the chain.)
+template <int MI>
+__device__ __forceinline__ void lat_unit(const DmaDesc& d, const int sub0, const int n0, const int kb, const int nkb,
+                                         const int subs, const int wt, uint32_t* ktl) {
+  LatStamps stp = lat_stamps_init(d, kb, sub0, n0);
+  const LatCol col = lat_col(d, n0);
+  const bool early = !(d.dbg & 4);
+  LatEpi<MI> e;
+  if (early) lat_epi_loads<MI>(d, sub0, col, e);
+  lat_f32x4 acc[MI];
+  lat_chain<MI>(d, sub0, kb, nkb, subs, col, ktl, acc, stp.p != nullptr);
+  if (stp.p) {
+    stp.at(2);  // operands in registers (lat_chain waited for them)
+    asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][3]));
+    stp.at(3);  // chain issued
+  }
+  if (!early) lat_epi_loads<MI>(d, sub0, col, e);
+  lat_fold_finish<MI>(d, sub0, kb, nkb, wt, col, e, acc, stp);
 }
 
 }  // namespace rtenhip

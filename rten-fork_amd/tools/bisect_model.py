@@ -42,13 +42,12 @@ def main():
         dict(),
         dict(RTENHIP_GRAPH="0"),
         dict(RTENHIP_TUNE="0"),
-        dict(RTENHIP_SIDE_STREAM="0"),
-        dict(RTENHIP_GRAPH="0", RTENHIP_TUNE="0", RTENHIP_SIDE_STREAM="0"),
+        dict(RTENHIP_GRAPH="0", RTENHIP_TUNE="0"),
     ]
     reps = int(os.environ.get("BISECT_REPS", "3"))
     for optimize in (False, True):
         for env in settings * reps:
-            for k in ("RTENHIP_GRAPH", "RTENHIP_TUNE", "RTENHIP_SIDE_STREAM"):
+            for k in ("RTENHIP_GRAPH", "RTENHIP_TUNE"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             g = spec.to_graph(optimize=optimize)
@@ -60,7 +59,7 @@ def main():
                 res.append(bits_equal(out[0].cpu().numpy(), exp))
             print(f"optimize={optimize} env={env} runs bit-exact={res}", flush=True)
             g.close()
-    for k in ("RTENHIP_GRAPH", "RTENHIP_TUNE", "RTENHIP_SIDE_STREAM"):
+    for k in ("RTENHIP_GRAPH", "RTENHIP_TUNE"):
         os.environ.pop(k, None)
     # Every op output requested: per-op comparison.
     g = spec.to_graph(optimize=False)

@@ -49,7 +49,7 @@ def _case_id(c):
     return "x".join(map(str, c[:6])) + f"s{c[6]}g{c[8]}-{c[9]}" + (f"d{c[11]}" if len(c) > 11 else "")
 
 
-@pytest.mark.parametrize("mode", ["41", "22", "12", "91", "92"])
+@pytest.mark.parametrize("mode", ["41", "22", "12", "91", "92", "71", "72", "74"])
 @pytest.mark.parametrize("case", CASES, ids=_case_id)
 def test_lat_conv_bitexact(rh, monkeypatch, mode, case):
     import torch
@@ -93,7 +93,8 @@ def test_lat_conv_bitexact(rh, monkeypatch, mode, case):
     g.set_timing(True)
     g.run(dev, g.output_ids, out=out)
     torch.cuda.synchronize()
-    assert f"cfg=lat{mode}" in g.timing_report()
+    if not (mode.startswith("7") and kh not in (1, 3)):  # (the LDS variants take 1x1 / 3x3 windows)
+        assert f"cfg=lat{mode}" in g.timing_report()
 
 
 @pytest.mark.parametrize("mode", ["41", "12"])
@@ -155,74 +156,3 @@ def test_resnet50_batch1_all_latency_convs(rh, monkeypatch):
     assert g.timing_report().count("cfg=lat41") >= 50
 
 
-@pytest.mark.parametrize("chain", ["1", "-1"])
-def test_resnet50_batch1_conv_chain(rh, monkeypatch, chain):
-    """ResNet-50 batch 1 with the convs between the stem and the pooling head
-    run as one persistent chain launch (conv_chain.hip): forced (1) and as the
-    plan decides by timing (-1; the chain is off by default).  Bit-exact against the oracle on the tuning
-    run, the capture and several replays (the chain's inter-layer hand-offs
-    cross XCDs, so a stale read would show up as a mismatch)."""
-    import torch
-    import graph_runner
-    from rten_hip import models
-
-    monkeypatch.setenv("RTENHIP_CHAIN", chain)
-    spec = models.resnet50()
-    x = np.random.default_rng(12).random((1, 3, 224, 224), dtype=np.float32)
-    exp = graph_runner.run(spec, {spec.inputs[0]: x})[spec.outputs[0]]
-    g = spec.to_graph()
-    xd = torch.from_numpy(x).cuda()
-    out = None
-    for _ in range(6):
-        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
-        torch.cuda.synchronize()
-        assert _bits_equal(out[0].cpu().numpy(), exp)
-    g.set_timing(True)
-    g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
-    torch.cuda.synchronize()
-    assert _bits_equal(out[0].cpu().numpy(), exp)
-    rep = g.timing_report()
-    if chain == "1":
-        assert "ConvChain" in rep, rep
-
-
-@pytest.mark.parametrize("mode", ["41", "-1"])
-def test_conv_chain_small(rh, monkeypatch, mode):
-    """A forced chain over a 1x1 -> 3x3 (zero-bordered hand-off) -> 1x1 +
-    residual block and a second block reusing the arena, at batch 2."""
-    import torch
-    import graph_runner
-    from rten_hip.graph import ModelSpec
-
-    monkeypatch.setenv("RTENHIP_CHAIN", "1")
-    monkeypatch.setenv("RTENHIP_LAT", mode)
-    rng = np.random.default_rng(99)
-    m = ModelSpec("chain_small")
-    x = m.value("x")
-    m.inputs = ["x"]
-    h = m.op("Relu", [x])  # keeps the graph input out of the chain
-
-    def block(h, i):
-        w1 = m.const(f"w1_{i}", rng.uniform(-0.3, 0.3, (32, 64, 1, 1)).astype(np.float32))
-        w2 = m.const(f"w2_{i}", rng.uniform(-0.2, 0.2, (32, 32, 3, 3)).astype(np.float32))
-        w3 = m.const(f"w3_{i}", rng.uniform(-0.2, 0.2, (64, 32, 1, 1)).astype(np.float32))
-        b = [m.const(f"b{j}_{i}", rng.uniform(-0.1, 0.1, (c,)).astype(np.float32)) for j, c in enumerate((32, 32, 64))]
-        a = m.op("Relu", [m.op("Conv", [h, w1, b[0]], {"pads": [0, 0, 0, 0], "strides": [1, 1]})])
-        a = m.op("Relu", [m.op("Conv", [a, w2, b[1]], {"pads": [1, 1, 1, 1], "strides": [1, 1]})])
-        return m.op("Relu", [m.op("Add", [m.op("Conv", [a, w3, b[2]], {"pads": [0, 0, 0, 0], "strides": [1, 1]}), h])])
-
-    h = block(block(block(h, 0), 1), 2)
-    m.outputs = [m.op("Relu", [h])]
-    ins = {"x": rng.uniform(-1, 1, (2, 64, 12, 12)).astype(np.float32)}
-    exp = graph_runner.run(m, ins)[m.outputs[0]]
-    g = m.to_graph()
-    dev = {g.input_ids[0]: torch.from_numpy(ins["x"]).cuda()}
-    out = None
-    for _ in range(5):
-        out = g.run(dev, g.output_ids, out=out)
-        torch.cuda.synchronize()
-        assert _bits_equal(out[0].cpu().numpy(), exp)
-    g.set_timing(True)
-    g.run(dev, g.output_ids, out=out)
-    torch.cuda.synchronize()
-    assert "ConvChain" in g.timing_report(), g.timing_report()

@@ -304,70 +304,3 @@ def test_expand_depthwise_fused_bitexact(rh, monkeypatch, case, policy):
         assert fused == (C == 16 and W % 4 == 0), g.timing_report()
 
 
-# Depthwise (3x3, stride 1, pad 1) -> project (1x1) pairs run as one kernel
-# (csrc/dwpw.hip): (N, C, H, W, M, dw act, project tail, biases)
-DW_PW = [
-    (2, 32, 112, 112, 16, "clip", "none", True),    # MobileNetV2 features.1
-    (2, 144, 56, 56, 24, "clip", "add", True),      # features.3 (residual)
-    (2, 192, 28, 28, 32, "clip", "add", True),      # features.5 / 6
-    (3, 40, 9, 20, 20, "relu", "relu", False),      # odd H (partial last band), no biases, M < 24
-    (1, 8, 14, 12, 3, "none", "clip", True),        # tiny M
-    (2, 96, 14, 14, 64, "clip", "none", True),      # M > 32: not fused, both run apart
-]
-
-
-@pytest.mark.parametrize("case", DW_PW, ids=lambda c: "x".join(map(str, c[:5])) + f"-{c[5]}-{c[6]}")
-@pytest.mark.parametrize("policy", ["on", "off"])
-def test_depthwise_pointwise_fused_bitexact(rh, monkeypatch, case, policy):
-    """The fused depthwise -> project kernel gives the two operators' bits
-    (conv_2d_depthwise_block then conv_2d_pointwise, with the graph's Clip /
-    Relu / residual Add), eager and replayed; opt-in with RTENHIP_DWPW=1."""
-    import torch
-    import graph_runner
-    from rten_hip.graph import ModelSpec
-
-    N, C, H, W, M, act_d, tail, biases = case
-    if policy == "off":
-        monkeypatch.delenv("RTENHIP_DWPW", raising=False)  # the default: apart
-    else:
-        monkeypatch.setenv("RTENHIP_DWPW", "1")
-    rng = np.random.default_rng(C * 5 + M + H)
-    m = ModelSpec("dwpw")
-    x = m.value("x")
-    m.inputs = ["x"]
-    lo, hi = m.const("lo", np.array(0.0, np.float32)), m.const("hi", np.array(6.0, np.float32))
-
-    def act(v, a):
-        if a == "clip":
-            return m.op("Clip", [v, lo, hi])
-        return m.op("Relu", [v]) if a == "relu" else v
-
-    wd = m.const("wd", rng.uniform(-0.5, 0.5, (C, 1, 3, 3)).astype(np.float32))
-    args = [x, wd] + ([m.const("bd", rng.uniform(-0.2, 0.2, (C,)).astype(np.float32))] if biases else [])
-    d = act(m.op("Conv", args, {"pads": [1, 1, 1, 1], "strides": [1, 1], "groups": C}, name="dw"), act_d)
-    wp = m.const("wp", rng.uniform(-0.3, 0.3, (M, C, 1, 1)).astype(np.float32))
-    args = [d, wp] + ([m.const("bp", rng.uniform(-0.2, 0.2, (M,)).astype(np.float32))] if biases else [])
-    y = m.op("Conv", args, {"pads": [0, 0, 0, 0], "strides": [1, 1]}, name="project")
-    ins = {"x": rng.uniform(-1, 2, (N, C, H, W)).astype(np.float32)}
-    if tail == "add":
-        r = m.value("r")
-        m.inputs.append("r")
-        ins["r"] = rng.uniform(-1, 1, (N, M, H, W)).astype(np.float32)
-        y = m.op("Add", [y, r])
-    else:
-        y = act(y, tail)
-    m.outputs = [y]
-    exp = graph_runner.run(m, ins)[y]
-    g = m.to_graph()
-    dev = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
-    out = None
-    for _ in range(3):
-        out = g.run(dev, g.output_ids, out=out)
-        torch.cuda.synchronize()
-        got = out[0].cpu().numpy()
-        assert _bits_equal(got, exp), np.abs(got - exp).max()
-    g.set_timing(True)
-    g.run(dev, g.output_ids, out=out)
-    torch.cuda.synchronize()
-    fused = "Conv(dw+pw)" in g.timing_report()
-    assert fused == (policy == "on" and M <= 32 and W % 4 == 0), g.timing_report()

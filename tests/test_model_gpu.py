@@ -85,19 +85,6 @@ def test_resnet50_batch64_full_size(rh, monkeypatch):
             assert _bits_equal(out[0].cpu().numpy(), exp), f"RTENHIP_PERSIST={mode}"
 
 
-@pytest.mark.parametrize("side", ["1", "-1"])
-def test_resnet50_side_stream(rh, monkeypatch, side):
-    """The downsample branch on the executor's second stream (off by
-    default; RTENHIP_SIDE_STREAM=1 always, -1 for batches up to 4): same
-    bits, eager and replayed."""
-    from rten_hip import models
-
-    monkeypatch.setenv("RTENHIP_SIDE_STREAM", side)
-    exp, outs = _run_both(rh, models.resnet50(), batch=2, runs=3)
-    for o in outs:
-        assert _bits_equal(o, exp), np.abs(o - exp).max()
-
-
 @pytest.mark.parametrize("mode", ["2", "3", "0"])
 def test_resnet50_persistent_modes(rh, monkeypatch, mode):
     """Persistent (per-XCD work queue) and one-block-per-tile DMA launches give
