@@ -167,6 +167,8 @@ static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaT
   d.res_img = a.O * P;
   d.res_c = P;
   d.bias = a.bias ? a.bias + g * opg : nullptr;
+  d.bn = a.bn ? a.bn + g * opg : nullptr;
+  d.bn_c = (int)a.bn_c;
   d.alpha = 1.f;
   d.beta = 0.f;
   d.vec4 = (P % 4 == 0 && d.out_c == P && d.out_row == a.ow && d.out_off == 0 && d.out_img % 4 == 0 &&
@@ -188,17 +190,6 @@ static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaT
     d.kt_row = (int)(a.dh * a.Wp);
     d.kt_col = (int)a.dw;
   }
-}
-
-rtenhip_status lat_conv_desc(Ctx* c, const ConvDmaArgs& a, DmaDesc& d) {
-  if (a.groups != 1) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency conv descriptor: grouped conv");
-  const int* tab = nullptr;
-  if (!(a.kh == 1 && a.kw == 1)) {
-    tab = c->dtab((int)a.C, (int)a.Hp, (int)a.Wp, (int)a.kh, (int)a.kw, (int)a.dh, (int)a.dw);
-    if (!tab) return fail(RTENHIP_HIP_ERROR, "DMA table allocation failed");
-  }
-  fill_conv_desc(a, 0, true, DmaTile{16, 256, 1}, tab, d);
-  return RTENHIP_OK;
 }
 
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {

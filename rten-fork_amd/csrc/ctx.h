@@ -69,6 +69,8 @@ struct ConvDmaArgs {
   int64_t N, C, Hp, Wp, O, kh, kw, sh, sw, dh, dw, oh, ow, groups;
   const float* packed_w;  // groups * packed_a_floats(opg, K)
   const float* bias;
+  const float* bn;  // fused BatchNormalization: [3][bn_c] mean, scale / sqrt(var + eps), beta (DmaDesc::bn)
+  int64_t bn_c;
   const float* residual;
   int act;
   float lo, hi;
@@ -92,10 +94,6 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
 // packed for it.
 bool conv_dual_ok(const ConvDmaArgs& a3, const ConvDmaArgs& ad, int cfg);
 rtenhip_status conv_dma_dual(Ctx* c, const ConvDmaArgs& a3, const ConvDmaArgs& ad);
-// The latency GEMM's descriptor of an ungrouped conv (conv chains), without
-// split workspace: the caller sets d.ws / d.counters when K > 256.
-struct DmaDesc;
-rtenhip_status lat_conv_desc(Ctx* c, const ConvDmaArgs& a, DmaDesc& d);
 
 // Pointwise convs on the vector ALUs (conv_pointwise.hip): 1x1 / stride 1 /
 // unpadded / ungrouped, K <= 256, P % 4 == 0, unpadded output; mc = output

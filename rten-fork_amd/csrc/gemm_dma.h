@@ -45,6 +45,12 @@ struct DmaDesc {
   const float* colbias;     // per-column bias colbias[p] (p = oy*OW + ox), added after the
                             // K fold and before the residual (MatMul -> Add(bias[N]))
   const float* cin;         // beta != 0 (dense outputs only; out_c = row stride)
+  // Conv -> BatchNormalization (Graph::optimize): per output row m, after the
+  // K fold and the bias and before the residual, x = (x - bn[m]) * bn[bn_c + m]
+  // + bn[2 * bn_c + m] -- mean, scale / sqrt(var + eps), beta
+  // (batch_norm_in_place, src/ops/norm.rs:45-49); null otherwise.
+  const float* bn;
+  int bn_c;
   float alpha, beta;
   int act;
   float act_lo, act_hi;

@@ -714,6 +714,16 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
         }
         float4 cb = make_float4(0.f, 0.f, 0.f, 0.f);
         if (d.colbias) cb = *(const float4*)(d.colbias + nn);  // (colbias over all N columns)
+        float bnm[4] = {0.f, 0.f, 0.f, 0.f}, bns[4] = {0.f, 0.f, 0.f, 0.f}, bnb[4] = {0.f, 0.f, 0.f, 0.f};
+        if (d.bn) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int mr = min(tm + wm + mi * 32 + i * 8 + rr, M - 1);
+            bnm[i] = d.bn[mr];
+            bns[i] = d.bn[d.bn_c + mr];
+            bnb[i] = d.bn[2 * d.bn_c + mr];
+          }
+        }
         float4 rl[RES_PRE ? 1 : 4];
         if constexpr (!RES_PRE) {
           if (d.residual) {
@@ -757,6 +767,12 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
             x.y = __fadd_rn(x.y, cb.y);
             x.z = __fadd_rn(x.z, cb.z);
             x.w = __fadd_rn(x.w, cb.w);
+          }
+          if (d.bn) {  // (x - mean) * s + beta, each step rounded (norm.rs:49)
+            x.x = __fadd_rn(__fmul_rn(__fsub_rn(x.x, bnm[i]), bns[i]), bnb[i]);
+            x.y = __fadd_rn(__fmul_rn(__fsub_rn(x.y, bnm[i]), bns[i]), bnb[i]);
+            x.z = __fadd_rn(__fmul_rn(__fsub_rn(x.z, bnm[i]), bns[i]), bnb[i]);
+            x.w = __fadd_rn(__fmul_rn(__fsub_rn(x.w, bnm[i]), bns[i]), bnb[i]);
           }
           if (d.residual) {
             float4 r;
@@ -839,6 +855,10 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
         float x = v[j];
         if (bias_late) x = __fadd_rn(x, bv[j]);
         if (d.colbias) x = __fadd_rn(x, cbv);
+        if (d.bn) {  // (x - mean) * s + beta (norm.rs:49); loaded here: BN-fused convs only
+          const int mr = min(tm + ml, M - 1);
+          x = __fadd_rn(__fmul_rn(__fsub_rn(x, d.bn[mr]), d.bn[d.bn_c + mr]), d.bn[2 * d.bn_c + mr]);
+        }
         if (d.residual) x = __fadd_rn(x, rv[j]);
         x = gelu_any ? apply_act(x) : apply_act_sel(x);
         if (ok) d.out[obase + (int64_t)(tm + ml) * d.out_c] = x;

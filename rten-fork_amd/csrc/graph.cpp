@@ -17,6 +17,7 @@
 #include "gemm_dma.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -149,8 +150,10 @@ static ConvAttrs conv_attrs(const Node& n, bool one_d) {
 Graph::~Graph() {
   for (auto& pl : plans)
     if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
-  for (auto& n : nodes)
+  for (auto& n : nodes) {
     if (n.kind == NodeKind::Constant && n.dev && n.owns_dev) (void)hipFree(n.dev);
+    if (n.bn_dev) (void)hipFree(n.bn_dev);
+  }
   if (arena) (void)hipFree(arena);
   for (auto& kv : mm_cat) {
     if (kv.second.first) (void)hipFree(kv.second.first);
@@ -1098,14 +1101,14 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       const Node& n = nodes[op];
       auto c3 = p.convs.find(op);
       if (n.op_type != "Conv" || c3 == p.convs.end() || c3->second.fc || c3->second.g.groups != 1 ||
-          n.fused_residual < 0 || p.conv_unfused.count(op) || !producer.count(n.fused_residual))
+          n.fused_residual < 0 || n.fused_bn >= 0 || p.conv_unfused.count(op) || !producer.count(n.fused_residual))
         continue;
       const int v = n.fused_residual;
       const int ds = producer[v];
       const Node& dn = nodes[ds];
       auto cd = p.convs.find(ds);
       if (dn.op_type != "Conv" || cd == p.convs.end() || cd->second.fc || cd->second.g.groups != 1 ||
-          dn.fused_residual >= 0 || dn.fused_act || outset.count(v) || uses[v] != 1 ||
+          dn.fused_residual >= 0 || dn.fused_act || dn.fused_bn >= 0 || outset.count(v) || uses[v] != 1 ||
           p.conv_unfused.count(ds) || p.expand_fused.count(ds) || p.padded.count(v))
         continue;
       const ConvPlan& gd = cd->second.g;
@@ -1355,6 +1358,13 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       return fail(RTENHIP_UNSUPPORTED_VALUE, "zero-bordered value needs the DMA conv path");
     rtenhip_tensor w = T(n.inputs[1]);
     ConvAttrs ca = conv_attrs(n, x.ndim == 3);
+    // A fused BatchNormalization off the DMA path: the standalone BN kernel
+    // on the conv output, before the residual and the activation.
+    auto run_bn = [&](rtenhip_tensor& t) -> rtenhip_status {
+      const Node& bn = nodes[n.fused_bn];
+      return rtenhip_batch_norm_f32(c, &t, ptr_of(p, bn.inputs[1]), ptr_of(p, bn.inputs[2]), ptr_of(p, bn.inputs[3]),
+                                    ptr_of(p, bn.inputs[4]), (float)bn.attrs.num("epsilon", 1e-5), &t);
+    };
     auto uf = p.conv_unfused.find(op_id);
     if (uf != p.conv_unfused.end()) {
       // Broadcasting Add after the conv: conv -> Add -> activation, unfused.
@@ -1362,11 +1372,24 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       rtenhip_status st = conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(),
                                     ca.dil.data(), ca.groups, nullptr, RTENHIP_ACT_NONE, 0.f, 0.f, &cy);
       if (st) return st;
+      if (n.fused_bn >= 0 && (st = run_bn(cy))) return st;
       rtenhip_tensor r = T(n.fused_residual);
       if ((st = rtenhip_binary_f32(c, RTENHIP_BINARY_ADD, &cy, &r, &y))) return st;
       if (n.fused_act == RTENHIP_ACT_RELU) return rtenhip_unary_f32(c, RTENHIP_UNARY_RELU, &y, 0.f, 0.f, &y);
       if (n.fused_act == RTENHIP_ACT_CLIP)
         return rtenhip_unary_f32(c, RTENHIP_UNARY_CLIP, &y, n.act_lo, n.act_hi, &y);
+      return RTENHIP_OK;
+    }
+    if (n.fused_bn >= 0) {
+      rtenhip_status st = conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(),
+                                    ca.groups, nullptr, RTENHIP_ACT_NONE, 0.f, 0.f, &y);
+      if (st || (st = run_bn(y))) return st;
+      if (n.fused_residual >= 0) {
+        rtenhip_tensor r = T(n.fused_residual);
+        if ((st = rtenhip_binary_f32(c, RTENHIP_BINARY_ADD, &y, &r, &y))) return st;
+      }
+      if (n.fused_act == RTENHIP_ACT_RELU) return rtenhip_unary_f32(c, RTENHIP_UNARY_RELU, &y, 0.f, 0.f, &y);
+      if (n.fused_act == RTENHIP_ACT_CLIP) return rtenhip_unary_f32(c, RTENHIP_UNARY_CLIP, &y, n.act_lo, n.act_hi, &y);
       return RTENHIP_OK;
     }
     return conv_impl(ctx, &x, &w, P(2), ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(),
@@ -2054,6 +2077,8 @@ void Graph::conv_io_args(Plan& p, int op_id, ConvDmaArgs& a) {
   a.ow = g.ow;
   a.groups = g.groups;
   a.bias = n.inputs.size() > 2 ? ptr_of(p, n.inputs[2]) : nullptr;
+  a.bn = n.bn_dev;
+  a.bn_c = g.O;
   a.residual = ptr_of(p, n.fused_residual);
   a.act = n.fused_act;
   a.lo = n.act_lo;
@@ -2125,9 +2150,11 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     return RTENHIP_OK;
   };
   // Pointwise VALU kernel (conv_pointwise.hip) as a further tuner candidate.
-  const bool pw_ok = pin == p.padded.end() && conv_pw_valu_eligible(g, a.Hp, a.Wp, pout != p.padded.end()) &&
+  // (The VALU kernels have no BatchNormalization epilogue: a conv with a fused
+  // BN tunes over the DMA and latency GEMMs only.)
+  const bool pw_ok = n.fused_bn < 0 && pin == p.padded.end() && conv_pw_valu_eligible(g, a.Hp, a.Wp, pout != p.padded.end()) &&
                      ((uintptr_t)a.xin | (uintptr_t)a.y) % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
-  const bool direct_ok = pin == p.padded.end() && conv_direct_valu_eligible(g, pout != p.padded.end()) &&
+  const bool direct_ok = n.fused_bn < 0 && pin == p.padded.end() && conv_direct_valu_eligible(g, pout != p.padded.end()) &&
                          (uintptr_t)a.y % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
   const bool direct_lds_ok = direct_ok && conv_direct_lds_eligible(g, pout != p.padded.end());
   auto launch = [&]() -> rtenhip_status {
@@ -2762,7 +2789,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         const Node& n = nodes[plan->ops[i]];
         std::string key = n.op_type;
         if ((n.op_type == "Conv" || n.op_type == "MatMul") &&
-            (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0))
+            (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0 || n.fused_bn >= 0))
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
@@ -2989,6 +3016,40 @@ rtenhip_status Graph::optimize() {
     int v = conv.outputs[0];
     int nxt = sole(v);
     if (nxt < 0 || nodes[nxt].removed) continue;
+    // Conv -> BatchNormalization with constant per-channel parameters: the
+    // conv's epilogue applies batch_norm_in_place's formula (norm.rs:45-49) to
+    // the rounded conv output -- (x - mean) * (scale / sqrt(var + eps)) + bias,
+    // the factor formed here in f32 exactly as the reference does per channel
+    // -- then the residual / activation fusions continue after it.  (Folding
+    // BN into the weights would change the rounding: DESIGN.md §6.)
+    if (nodes[nxt].op_type == "BatchNormalization" && conv.fused_bn < 0 && !getenv("RTENHIP_NO_BN_FUSION")) {
+      Node& bn = nodes[nxt];
+      const int wv = conv.inputs.size() > 1 ? conv.inputs[1] : -1;
+      const int64_t O = wv >= 0 && nodes[wv].kind == NodeKind::Constant && !nodes[wv].shape.empty() ? nodes[wv].shape[0] : -1;
+      std::vector<float> prm[4];  // scale, bias, mean, var
+      bool ok = O > 0 && bn.inputs.size() == 5 && bn.inputs[0] == v && !bn.outputs.empty() && bn.input_perm.empty();
+      for (int k = 0; ok && k < 4; k++)
+        ok = bn.inputs[k + 1] >= 0 && const_values(*this, bn.inputs[k + 1], prm[k]) && (int64_t)prm[k].size() == O;
+      if (ok) {
+        const float eps = (float)bn.attrs.num("epsilon", 1e-5);
+        std::vector<float> tab((size_t)3 * O);
+        for (int64_t c = 0; c < O; c++) {
+          const float t = prm[3][c] + eps;  // f32 add, sqrt and division, each rounded (norm.rs:45)
+          tab[c] = prm[2][c];
+          tab[O + c] = prm[0][c] / std::sqrt(t);
+          tab[2 * O + c] = prm[1][c];
+        }
+        if (hipMalloc(&conv.bn_dev, tab.size() * 4) != hipSuccess) return fail(RTENHIP_HIP_ERROR, "hipMalloc failed");
+        RTENHIP_HIP_CHECK(hipMemcpy(conv.bn_dev, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+        conv.fused_bn = nxt;
+        bn.removed = true;
+        conv.outputs[0] = bn.outputs[0];
+        fused++;
+        v = conv.outputs[0];
+        nxt = sole(v);
+        if (nxt < 0 || nodes[nxt].removed) continue;
+      }
+    }
     Node& a = nodes[nxt];
     if (a.op_type == "Add" && a.inputs.size() == 2 && a.outputs.size() == 1) {
       int other = a.inputs[0] == v ? a.inputs[1] : a.inputs[0];
@@ -3029,7 +3090,7 @@ rtenhip_status Graph::optimize() {
   // (mbconv.hip); the depthwise conv now reads the expand's input.
   for (int i = 0; i < (int)nodes.size(); i++) {
     Node& e = nodes[i];
-    if (e.kind != NodeKind::Operator || e.removed || e.op_type != "Conv" || e.fused_residual >= 0 ||
+    if (e.kind != NodeKind::Operator || e.removed || e.op_type != "Conv" || e.fused_residual >= 0 || e.fused_bn >= 0 ||
         e.outputs.size() != 1 || e.inputs.size() < 2 || !e.input_perm.empty())
       continue;
     const int wv = e.inputs[1];
@@ -3045,7 +3106,7 @@ rtenhip_status Graph::optimize() {
     const int d_op = sole(e.outputs[0]);
     if (d_op < 0) continue;
     Node& dn = nodes[d_op];
-    if (dn.removed || dn.op_type != "Conv" || dn.fused_residual >= 0 || dn.fe_op >= 0 || dn.inputs.size() < 2 ||
+    if (dn.removed || dn.op_type != "Conv" || dn.fused_residual >= 0 || dn.fused_bn >= 0 || dn.fe_op >= 0 || dn.inputs.size() < 2 ||
         dn.inputs[0] != e.outputs[0] || !dn.input_perm.empty())
       continue;
     const int dw = dn.inputs[1];

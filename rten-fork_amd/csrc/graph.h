@@ -97,6 +97,11 @@ struct Node {
   std::vector<int> inputs;   // -1 = absent optional input
   std::vector<int> outputs;
   // Load-time fusion (rtenhip_graph_optimize): Conv epilogue.
+  // Conv -> BatchNormalization: the BN node (kept, removed from the plan) and
+  // its per-channel [3][O] device table {mean, scale / sqrt(var + eps), beta}
+  // (owned), applied to the rounded conv output before the residual.
+  int fused_bn = -1;
+  float* bn_dev = nullptr;
   int fused_residual = -1;   // value id added after the bias
   int fused_act = 0;         // RTENHIP_ACT_*
   float act_lo = 0.f, act_hi = 0.f;

@@ -202,6 +202,20 @@ __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, con
   const float lo = d.act_lo, hi = d.act_hi;
   const int64_t obase = (int64_t)col.img * d.out_img + (int64_t)col.oy * d.out_row + col.ox + d.out_off;
   if (col.n >= d.N) return;
+  // Fused BatchNormalization (DmaDesc::bn): its parameters are loaded here,
+  // after the chains, so convs without one keep the registers.
+  float bnp[MI][4][3];
+  if (d.bn) {
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int mc = min((sub0 + mi) * 16 + 4 * h + r, d.M - 1);
+        bnp[mi][r][0] = d.bn[mc];
+        bnp[mi][r][1] = d.bn[d.bn_c + mc];
+        bnp[mi][r][2] = d.bn[2 * d.bn_c + mc];
+      }
+  }
 #pragma unroll
   for (int mi = 0; mi < MI; mi++)
 #pragma unroll
@@ -209,6 +223,7 @@ __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, con
       const int m = (sub0 + mi) * 16 + 4 * h + r;
       float x = sum[mi][r];
       if (d.colbias) x = __fadd_rn(x, e.cbv);
+      if (d.bn) x = __fadd_rn(__fmul_rn(__fsub_rn(x, bnp[mi][r][0]), bnp[mi][r][1]), bnp[mi][r][2]);
       if (d.residual) x = __fadd_rn(x, e.res[mi][r]);
       if (act_gelu) {
         x = vm_gelu(x);

@@ -42,21 +42,33 @@ class _Init:
 
 
 def _conv(m: ModelSpec, init: _Init, name, x, cin, cout, k, stride=1, pad=0, groups=1,
-          scale=1.0):
+          scale=1.0, bn=False):
     w, b = init.conv(cout, cin // groups, k, k, scale)
     wn = m.const(f"{name}.weight", w)
-    bn = m.const(f"{name}.bias", b)
-    return m.op("Conv", [x, wn, bn], {"pads": [pad] * 4, "strides": [stride, stride],
-                                      "dilations": [1, 1], "groups": groups}, name=name)
+    attrs = {"pads": [pad] * 4, "strides": [stride, stride], "dilations": [1, 1], "groups": groups}
+    if not bn:
+        return m.op("Conv", [x, wn, m.const(f"{name}.bias", b)], attrs, name=name)
+    # An export without BN folding (torchvision layout: bias-free conv, then
+    # BatchNormalization with its running statistics).
+    y = m.op("Conv", [x, wn], attrs, name=name)
+    rng = init.rng
+    p = [rng.uniform(0.8, 1.2, cout), rng.uniform(-0.1, 0.1, cout), rng.uniform(-0.1, 0.1, cout),
+         rng.uniform(0.5, 1.5, cout)]
+    scale_n, bias_n, mean_n, var_n = (m.const(f"{name}.bn.{k}", v.astype(np.float32))
+                                      for k, v in zip(("weight", "bias", "running_mean", "running_var"), p))
+    return m.op("BatchNormalization", [y, scale_n, bias_n, mean_n, var_n], {"epsilon": 1e-5}, name=f"{name}.bn")
 
 
-def resnet50(num_classes: int = 1000, seed: int = 4321) -> ModelSpec:
-    """ResNet-50 v1.5 (stride on the 3x3 conv), BN folded, NCHW input [N,3,224,224]."""
-    m = ModelSpec("resnet50")
+def resnet50(num_classes: int = 1000, seed: int = 4321, unfolded_bn: bool = False) -> ModelSpec:
+    """ResNet-50 v1.5 (stride on the 3x3 conv), NCHW input [N,3,224,224]; BN
+    folded into the convs (the benchmark export), or with ``unfolded_bn`` every
+    conv bias-free and followed by a BatchNormalization node."""
+    m = ModelSpec("resnet50_bn" if unfolded_bn else "resnet50")
     init = _Init(seed)
     x = m.value("input")
     m.inputs = ["input"]
-    h = _conv(m, init, "conv1", x, 3, 64, 7, stride=2, pad=3)
+    bn = unfolded_bn
+    h = _conv(m, init, "conv1", x, 3, 64, 7, stride=2, pad=3, bn=bn)
     h = m.op("Relu", [h], name="relu1")
     h = m.op("MaxPool", [h], {"kernel_size": [3, 3], "strides": [2, 2], "pads": [1, 1, 1, 1]},
              name="maxpool")
@@ -67,13 +79,13 @@ def resnet50(num_classes: int = 1000, seed: int = 4321) -> ModelSpec:
             s = stride if bi == 0 else 1
             pre = f"layer{li + 1}.{bi}"
             cout = width * 4
-            t = _conv(m, init, f"{pre}.conv1", h, cin, width, 1)
+            t = _conv(m, init, f"{pre}.conv1", h, cin, width, 1, bn=bn)
             t = m.op("Relu", [t], name=f"{pre}.relu1")
-            t = _conv(m, init, f"{pre}.conv2", t, width, width, 3, stride=s, pad=1)
+            t = _conv(m, init, f"{pre}.conv2", t, width, width, 3, stride=s, pad=1, bn=bn)
             t = m.op("Relu", [t], name=f"{pre}.relu2")
-            t = _conv(m, init, f"{pre}.conv3", t, width, cout, 1, scale=0.2)
+            t = _conv(m, init, f"{pre}.conv3", t, width, cout, 1, scale=0.2, bn=bn)
             if bi == 0:
-                ident = _conv(m, init, f"{pre}.downsample", h, cin, cout, 1, stride=s)
+                ident = _conv(m, init, f"{pre}.downsample", h, cin, cout, 1, stride=s, bn=bn)
             else:
                 ident = h
             t = m.op("Add", [t, ident], name=f"{pre}.add")

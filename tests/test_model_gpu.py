@@ -55,6 +55,35 @@ def test_resnet50_bitexact(rh, optimize):
                         f"rel {d.max() / np.abs(exp).max():.3g}, {(d > 0).sum()} elems")
 
 
+@pytest.mark.parametrize("batch", [1, 2, 64])
+def test_resnet50_unfolded_bn_bitexact(rh, batch):
+    """ResNet-50 exported without BN folding (bias-free convs, each followed by
+    BatchNormalization): the BN runs in the conv epilogue on the rounded conv
+    output, with the reference's per-channel formula (norm.rs:45-49), on the
+    latency GEMM (batch 1) and the DMA GEMM (batch 2, 64): bit-exact against
+    the oracle running every BatchNormalization op, and no BN launch is left
+    in the plan."""
+    import torch
+    from rten_hip import models
+
+    spec = models.resnet50(unfolded_bn=True)
+    exp, outs = _run_both(rh, spec, batch=batch, runs=3, seed=11)
+    assert np.isfinite(exp).all()
+    for o in outs:
+        if not _bits_equal(o, exp):
+            d = np.abs(o.astype(np.float64) - exp)
+            pytest.fail(f"logits differ: max abs {d.max():.3g}, {(d > 0).sum()} elems")
+    g = spec.to_graph()
+    x = torch.from_numpy(np.random.default_rng(11).random((batch, 3, 224, 224), dtype=np.float32)).cuda()
+    g.set_timing(True)
+    out = g.run({g.input_ids[0]: x}, g.output_ids)
+    g.run({g.input_ids[0]: x}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    rep = g.timing_report()
+    assert "BatchNormalization" not in rep, rep
+    assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
 def test_mobilenet_v2_bitexact(rh):
     from rten_hip import models
 

@@ -25,7 +25,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, total, q):
+def _spec_and_input(model, total):
+    from test_parallel import tiny_spec
+
+    if model == "resnet50":
+        from rten_hip import models
+
+        return models.resnet50(), np.random.default_rng(1234).random((total, 3, 224, 224), dtype=np.float32)
+    return tiny_spec(), np.random.default_rng(1234).random((total, 4, 6, 6), dtype=np.float32)
+
+
+def _worker(rank, world, port, total, q, model="tiny"):
     for p in (os.path.join(ROOT, "rten-fork_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
         sys.path.insert(0, p)
     import torch
@@ -37,13 +47,11 @@ def _worker(rank, world, port, total, q):
     try:
         import rten_hip
         from rten_hip.parallel import BatchShardRunner
-        from test_parallel import tiny_spec
 
         torch.cuda.set_device(0)
         rten_hip.default_context()
-        spec = tiny_spec()
+        spec, x = _spec_and_input(model, total)
         g = spec.to_graph()
-        x = np.random.default_rng(1234).random((total, 4, 6, 6), dtype=np.float32)
 
         def fn(xb):
             outs = None
@@ -61,8 +69,13 @@ def _worker(rank, world, port, total, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("total", [6, 5])
-def test_world2_device_graph_matches_oracle(total):
+@pytest.mark.parametrize("model,total", [("tiny", 6), ("tiny", 5), ("resnet50", 4), ("resnet50", 3)])
+def test_world2_device_graph_matches_oracle(model, total):
+    """Two ranks shard the batch (even: 2 + 2; ragged: 2 + 1) and run the
+    device graph eagerly, then captured and replayed; the all-gathered
+    logits are bit-identical to the oracle's whole-batch run.  ResNet-50 is
+    BASELINE.json configs[4]'s model (there 64 images per GPU over 8 GPUs;
+    here the same plan-per-shard path at 2 ranks on one GPU)."""
     import torch
 
     if not torch.cuda.is_available():
@@ -70,16 +83,15 @@ def test_world2_device_graph_matches_oracle(total):
     import torch.multiprocessing as mp
 
     import graph_runner
-    from test_parallel import tiny_spec
 
-    spec = tiny_spec()
-    x = np.random.default_rng(1234).random((total, 4, 6, 6), dtype=np.float32)
+    sys.path.insert(0, os.path.join(ROOT, "rten-fork_amd"))
+    spec, x = _spec_and_input(model, total)
     expect = np.ascontiguousarray(graph_runner.run(spec, {"input": x})[spec.outputs[0]], np.float32)
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, total, q, model)) for r in range(2)]
     for p in procs:
         p.start()
     results = [q.get(timeout=240) for _ in procs]
