@@ -2231,19 +2231,27 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       std::vector<float*>& bufs = ts.bufs;
       // Launch times of the current binding: best of n (screening) or median
       // of n (final round).
+      // A sample of a short launch times `reps` back-to-back launches between
+      // one event pair (per-launch event overhead amortised; kernel boundaries
+      // as in the replayed graph).
       auto time_it = [&](int n, bool median, float& out_ms) -> rtenhip_status {
         rtenhip_status st = launch();  // warm-up
         if (st) return st;
+        int reps = 1;
         std::vector<float> ts;
-        for (int r = 0; r < n; r++) {
+        for (int r = 0; r <= n; r++) {
           RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
-          st = launch();
-          if (st) return st;
+          for (int k = 0; k < reps; k++)
+            if ((st = launch())) return st;
           RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
           RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
           float t = 0;
           RTENHIP_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
-          ts.push_back(t);
+          if (r == 0) {  // probe: choose reps
+            reps = t < 0.03f ? 8 : (t < 0.1f ? 3 : 1);
+            continue;
+          }
+          ts.push_back(t / reps);
         }
         std::sort(ts.begin(), ts.end());
         out_ms = median ? ts[ts.size() / 2] : ts[0];
