@@ -48,6 +48,7 @@ template <bool FULL>
 __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   __shared__ float Ks[AT_S * KS];
   __shared__ float Vs[AT_S * VS];
+  __shared__ float Ms[AT_S];  // the mask row when it does not depend on the query row (m_i == 0)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
   const int bh = blockIdx.x;
@@ -82,6 +83,12 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
       }
     }
   }
+  // A query-independent mask row ([B, 1, 1, S], BERT's) is staged with K and
+  // V, so the softmax phase reads it from LDS instead of making 64 global
+  // loads per lane on the critical path.
+  const bool mask_lds = d.mask && d.m_i == 0;
+  float mv = 0.f;
+  if (mask_lds && tid < S) mv = d.mask[b * d.m_b + hd * d.m_h + (int64_t)tid * d.m_j];
 #pragma unroll
   for (int u = 0; u < ST; u++) {
     const int t = tid + u * AT_THREADS;
@@ -93,13 +100,26 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
     kd[3] = kk[u].w;
     *(float4*)(Vs + j * VS + c) = vv[u];
   }
+  if (mask_lds && tid < S) Ms[tid] = mv;
   const int i0 = wave * 32;
   const int i = i0 + l32;  // this lane's query row
   const bool row_ok = FULL || i < S;
   // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand),
   // loaded while the K / V stores land.
   float qf[AT_D / 2];
-  {
+  if (((uintptr_t)q % 16) == 0 && d.q_s % 4 == 0) {
+    // The whole row as 16 float4s (16 load instructions instead of 32 strided
+    // dwords); this lane keeps elements h and h + 2 of each 4.
+    const float4* qr4 = reinterpret_cast<const float4*>(q + (int64_t)(row_ok ? i : 0) * d.q_s);
+    float4 q4[AT_D / 4];
+#pragma unroll
+    for (int m = 0; m < AT_D / 4; m++) q4[m] = qr4[m];
+#pragma unroll
+    for (int m = 0; m < AT_D / 4; m++) {
+      qf[2 * m] = row_ok ? (h ? q4[m].y : q4[m].x) : 0.f;
+      qf[2 * m + 1] = row_ok ? (h ? q4[m].w : q4[m].z) : 0.f;
+    }
+  } else {
     const float* qr = q + (int64_t)(row_ok ? i : 0) * d.q_s + h;
 #pragma unroll
     for (int s = 0; s < AT_D / 2; s++) qf[s] = row_ok ? qr[2 * s] : 0.f;
@@ -123,7 +143,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   // Scale and mask (separately rounded, as the Div|Mul and Add operators),
   // then the row max over the keys < S.
   const float* mrow =
-      (d.mask && row_ok) ? d.mask + b * d.m_b + hd * d.m_h + (int64_t)i * d.m_i : nullptr;
+      (d.mask && row_ok && !mask_lds) ? d.mask + b * d.m_b + hd * d.m_h + (int64_t)i * d.m_i : nullptr;
   float m = -FLT_MAX;
 #pragma unroll
   for (int t = 0; t < 4; t++)
@@ -136,7 +156,8 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
       else if (d.scale_op == 2)
         x = __fmul_rn(x, d.scale);
       if (FULL || j < S) {
-        if (mrow) x = __fadd_rn(x, mrow[(int64_t)j * d.m_j]);
+        if (mask_lds) x = __fadd_rn(x, Ms[j]);
+        else if (mrow) x = __fadd_rn(x, mrow[(int64_t)j * d.m_j]);
         m = rust_max(m, x);
       }
       acc[t][e] = x;

@@ -52,6 +52,25 @@ __global__ void gather_kernel(const float* __restrict__ x, const int32_t* __rest
   }
 }
 
+// Row gather (axis 0 of a contiguous [V, D] table, D % 4 == 0, contiguous
+// indices and output): one wave per index copies its row as float4s -- the
+// embedding lookups of BERT.  Same values and the same out-of-range flag as
+// gather_kernel (an out-of-range row is zero-filled).
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float* __restrict__ x, const int32_t* __restrict__ idx,
+                                                          float* __restrict__ y, int64_t rows, int64_t V, int D4,
+                                                          int* __restrict__ bad) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const int lane = threadIdx.x & 63;
+  int64_t j = idx[r];
+  if (j < 0) j += V;
+  const bool ok = j >= 0 && j < V;
+  if (!ok && lane == 0) atomicOr(bad, 1);
+  const float4* src = reinterpret_cast<const float4*>(x) + (ok ? j : 0) * D4;
+  float4* dst = reinterpret_cast<float4*>(y) + r * D4;
+  for (int c = lane; c < D4; c += 64) dst[c] = ok ? src[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
 __global__ void where_kernel(const int32_t* __restrict__ c, const float* __restrict__ x,
                              const float* __restrict__ y, float* __restrict__ out, int64_t n,
                              IdxDesc d) {
@@ -172,6 +191,15 @@ rtenhip_status launch_gather(const rtenhip_tensor* x, const rtenhip_tensor_i32* 
     return fail(RTENHIP_INCOMPATIBLE_INPUT_SHAPES, "Output tensor has the wrong shape");
   const int64_t n = numel(*y);
   if (n == 0) return RTENHIP_OK;
+  if (ax == 0 && x->ndim == 2 && is_contiguous(*x) && x->shape[1] % 4 == 0 && x->shape[1] / 4 < (1 << 30) &&
+      is_contiguous(*reinterpret_cast<const rtenhip_tensor*>(indices)) && ((uintptr_t)x->data % 16) == 0 &&
+      ((uintptr_t)y->data % 16) == 0) {
+    const int64_t rows = n / x->shape[1];
+    hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x->data,
+                       indices->data, y->data, rows, x->shape[0], (int)(x->shape[1] / 4), flag);
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   hipLaunchKernelGGL(gather_kernel, ix_grid(n), dim3(256), 0, s, x->data, indices->data, y->data, n,
                      d, x->shape[ax], x->strides[ax], flag);
   RTENHIP_LAUNCH_CHECK();

@@ -214,7 +214,38 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   const int64_t left = rows - row0;
   const int nr = left < R ? (int)left : R;
   const float4* x4 = reinterpret_cast<const float4*>(x + row0 * len);
-  for (int t = threadIdx.x; t < nr * q; t += 256) lds4[t] = x4[t];
+  // LEN instances: the lane's scale / bias float4s (columns lane + 64 i) are
+  // loaded first, in flight with the staging (loaded per output row instead,
+  // each row's stores would wait on a round trip).
+  constexpr int NCP = (LEN > 0 && LEN % 256 == 0) ? LEN / 256 : 1;
+  float4 scp[NCP], bbp[NCP];
+  if constexpr (LEN > 0 && LEN % 256 == 0) {
+    const float4* s4p = reinterpret_cast<const float4*>(scale);
+    const float4* b4p = reinterpret_cast<const float4*>(bias);
+#pragma unroll
+    for (int i = 0; i < NCP; i++) {
+      scp[i] = s4p[lane + 64 * i];
+      bbp[i] = bias ? b4p[lane + 64 * i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  // Staging: a thread's loads are issued together (8 in flight), then stored
+  // to LDS -- a load-then-store loop would pay one memory round trip per trip.
+  {
+    // (Loads past the rows read a clamped in-range index: unconditional, so
+    // no branch or wait sits between them; only the LDS stores are guarded.)
+    const int n4 = nr * q;
+    for (int t = threadIdx.x; t < n4; t += 8 * 256) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) v[u] = x4[min(t + u * 256, n4 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; u++)  // an unconditional use: keeps the loads out of the guarded stores
+        asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (t + u * 256 < n4) lds4[t + u * 256] = v[u];
+    }
+  }
   __syncthreads();
   // slice_sum: chunk c = ((x0 + x4) + (x1 + x5)) + (x2 + x6)) + (x3 + x7)
   for (int r = wave; r < nr; r += 4)
@@ -267,25 +298,34 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   float4* y4 = reinterpret_cast<float4*>(y + row0 * len);
   const float4* s4 = reinterpret_cast<const float4*>(scale);
   const float4* b4 = reinterpret_cast<const float4*>(bias);
-  for (int r = wave; r < nr; r += 4) {
+  auto out_row = [&](int r, const float4* sc, const float4* bb, int c0, int nc) __attribute__((always_inline)) {
     const float mean = stat[r], inv = stat[R + r];
-    for (int c = lane; c < q; c += 64) {
-      const float4 v = lds4[r * q + c], sc = s4[c];
+    for (int i = 0; i < nc; i++) {
+      const int c = c0 + 64 * i;
+      const float4 v = lds4[r * q + c];
       float4 o;
-      o.x = __fmul_rn(__fmul_rn(__fsub_rn(v.x, mean), inv), sc.x);
-      o.y = __fmul_rn(__fmul_rn(__fsub_rn(v.y, mean), inv), sc.y);
-      o.z = __fmul_rn(__fmul_rn(__fsub_rn(v.z, mean), inv), sc.z);
-      o.w = __fmul_rn(__fmul_rn(__fsub_rn(v.w, mean), inv), sc.w);
+      o.x = __fmul_rn(__fmul_rn(__fsub_rn(v.x, mean), inv), sc[i].x);
+      o.y = __fmul_rn(__fmul_rn(__fsub_rn(v.y, mean), inv), sc[i].y);
+      o.z = __fmul_rn(__fmul_rn(__fsub_rn(v.z, mean), inv), sc[i].z);
+      o.w = __fmul_rn(__fmul_rn(__fsub_rn(v.w, mean), inv), sc[i].w);
       if (bias) {
-        const float4 bb = b4[c];
-        o.x = __fadd_rn(o.x, bb.x);
-        o.y = __fadd_rn(o.y, bb.y);
-        o.z = __fadd_rn(o.z, bb.z);
-        o.w = __fadd_rn(o.w, bb.w);
+        o.x = __fadd_rn(o.x, bb[i].x);
+        o.y = __fadd_rn(o.y, bb[i].y);
+        o.z = __fadd_rn(o.z, bb[i].z);
+        o.w = __fadd_rn(o.w, bb[i].w);
       }
       y4[r * q + c] = o;
       if (pk.p) lds4[r * q + c] = o;  // this thread's own element: no hazard
     }
+  };
+  if constexpr (LEN > 0 && LEN % 256 == 0) {
+    for (int r = wave; r < nr; r += 4) out_row(r, scp, bbp, lane, NCP);
+  } else {
+    for (int r = wave; r < nr; r += 4)
+      for (int c = lane; c < q; c += 64) {
+        const float4 sc = s4[c], bb = bias ? b4[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+        out_row(r, &sc, &bb, c, 1);
+      }
   }
   if (pk.p) {
     // The MatMul's packed A (packed_a.h): one 16-byte chunk per (k tile,

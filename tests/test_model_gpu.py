@@ -208,20 +208,21 @@ def test_bert_embeddings_bitexact(rh, mask_op):
         assert _bits_equal(out[0].cpu().numpy(), exp)
 
 
-def _gather_graph():
+def _gather_graph(width=3):
     from rten_hip.graph import ModelSpec
 
     m = ModelSpec("gather")
     ids = m.value("ids")
     m.inputs = ["ids"]
-    table = m.const("table", np.arange(12, dtype=np.float32).reshape(4, 3))
+    table = m.const("table", np.arange(4 * width, dtype=np.float32).reshape(4, width))
     y = m.op("Gather", [table, ids], {"axis": 0}, name="gather")
     c = m.op("Cast", [ids], {"to": 1}, name="cast")
     m.outputs = [y, c, m.op("Relu", [y], name="relu")]
     return m
 
 
-def test_graph_gather_index_error_and_types(rh):
+@pytest.mark.parametrize("width", [3, 8])  # 8: the float4 row-gather path (embeddings)
+def test_graph_gather_index_error_and_types(rh, width):
     """Gather in the captured plan reports an out-of-range index with the
     reference's error (gather.rs:52-60) without a host round trip per run:
     at synchronize(), or at the next run of the plan (before it is queued);
@@ -231,10 +232,10 @@ def test_graph_gather_index_error_and_types(rh):
     from rten_hip import OpError
     from rten_hip.graph import ModelSpec
 
-    g = _gather_graph().to_graph()
+    g = _gather_graph(width).to_graph()
     good = torch.tensor([[0, 3], [-1, 2]], dtype=torch.int32).cuda()
     bad = torch.tensor([[0, 4], [1, 2]], dtype=torch.int32).cuda()
-    table = np.arange(12, dtype=np.float32).reshape(4, 3)
+    table = np.arange(4 * width, dtype=np.float32).reshape(4, width)
     exp = table[np.array([[0, 3], [3, 2]])]
     outs = None
     # eager, capture, replays; "bad+next": the error surfaces at the next run
