@@ -29,6 +29,7 @@
 
 #include "common.h"
 #include "vecmath.h"
+#include "stage.h"
 
 namespace rtenhip {
 
@@ -88,8 +89,10 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   float* b_d = b_e + d.cpb;           // [cnt]
   int* fin = reinterpret_cast<int*>(b_d + d.cpb);  // [cnt]: every tap weight finite
   const int t = threadIdx.x;
-  for (int i = t; i < cnt * CIN; i += 256) w_e[i] = d.we[(int64_t)c_begin * CIN + i];
-  for (int i = t; i < cnt * 9; i += 256) w_d[i] = d.wd[(int64_t)c_begin * 9 + i];
+  stage_batched<4, float>(cnt * CIN, [&](int e) { return d.we[(int64_t)c_begin * CIN + e]; },
+                          [&](int e, float v) { w_e[e] = v; });
+  stage_batched<4, float>(cnt * 9, [&](int e) { return d.wd[(int64_t)c_begin * 9 + e]; },
+                          [&](int e, float v) { w_d[e] = v; });
   for (int i = t; i < cnt; i += 256) {
     b_e[i] = d.be ? d.be[c_begin + i] : 0.f;
     b_d[i] = d.bd ? d.bd[c_begin + i] : 0.f;
@@ -252,9 +255,10 @@ __global__ __launch_bounds__(256) void expand_dw_flat_kernel(ExpandDwDesc d, int
     const float* xp = d.x + (int64_t)n * cin * P;
     const int total = cin * P;
     if ((total & 3) == 0 && ((uintptr_t)xp & 15) == 0) {
-      for (int i = t; i < total / 4; i += 256) reinterpret_cast<float4*>(xs)[i] = reinterpret_cast<const float4*>(xp)[i];
+      stage_batched<8, float4>(total / 4, [&](int e) { return reinterpret_cast<const float4*>(xp)[e]; },
+                               [&](int e, const float4& v) { reinterpret_cast<float4*>(xs)[e] = v; });
     } else {
-      for (int i = t; i < total; i += 256) xs[i] = xp[i];
+      stage_batched<8, float>(total, [&](int e) { return xp[e]; }, [&](int e, float v) { xs[e] = v; });
     }
   }
   __syncthreads();

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include "vecmath.h"
 #include "fastdiv_dev.h"
+#include "stage.h"
 
 namespace rtenhip {
 
@@ -65,10 +66,10 @@ __global__ __launch_bounds__(256) void pool_plane_kernel(const float* __restrict
   const float* xp = x + pidx * H * W + (int64_t)r_lo * W;
   const int n = max(0, r_hi - r_lo) * W;
   if ((W & 3) == 0) {
-    for (int i = threadIdx.x * 4; i < n; i += 1024)
-      *(float4*)(plane + i) = *(const float4*)(xp + i);
+    stage_batched<4, float4>(n >> 2, [&](int e) { return *(const float4*)(xp + 4 * e); },
+                             [&](int e, const float4& v) { *(float4*)(plane + 4 * e) = v; });
   } else {
-    for (int i = threadIdx.x; i < n; i += 256) plane[i] = xp[i];
+    stage_batched<8, float>(n, [&](int e) { return xp[e]; }, [&](int e, float v) { plane[e] = v; });
   }
   __syncthreads();
   float* yp = y + pidx * OH * OW;
@@ -190,7 +191,7 @@ __global__ __launch_bounds__(256) void gap_lds_kernel(const float* __restrict__ 
   const int np = (int)min((int64_t)ppb, NC - p0);
   const float* src = x + p0 * HW;
   const int n = np * HW;
-  for (int i = threadIdx.x; i < n; i += 256) buf[i] = src[i];
+  stage_batched<8, float>(n, [&](int e) { return src[e]; }, [&](int e, float v) { buf[e] = v; });
   __syncthreads();
   if ((int)threadIdx.x < np) {
     const float* p = buf + threadIdx.x * HW;
@@ -325,8 +326,8 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
   if (flat) {
     const int n = np * H * W, n4 = n >> 2;
     const float4* src = reinterpret_cast<const float4*>(x + (int64_t)plane0 * H * W);
-#pragma unroll 4
-    for (int t = threadIdx.x; t < n4; t += blockDim.x) reinterpret_cast<float4*>(tile)[t] = src[t];
+    stage_batched<4, float4>(n4, [&](int e) { return src[e]; },
+                             [&](int e, const float4& v) { reinterpret_cast<float4*>(tile)[e] = v; });
     for (int t = 4 * n4 + (int)threadIdx.x; t < n; t += blockDim.x) tile[t] = x[(int64_t)plane0 * H * W + t];
   } else if (r1 > r0) {
     const int span = (r1 - r0) * W;
@@ -334,24 +335,31 @@ __global__ __launch_bounds__(256) void depthwise_lds_kernel(
       // 16-byte copies, several in flight per thread (loads are batched
       // ahead of the LDS stores: the two address spaces cannot alias).
       const int n4 = span >> 2, total4 = np * n4;
-#pragma unroll 4
-      for (int t = threadIdx.x; t < total4; t += blockDim.x) {
-        const int pp = t / n4, q4 = t - pp * n4;
-        const float4 v =
-            *(const float4*)(x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + 4 * q4);
-        *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
-      }
+      stage_batched<4, float4>(
+          total4,
+          [&](int t) {
+            const int pp = t / n4, q4 = t - pp * n4;
+            return *(const float4*)(x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + 4 * q4);
+          },
+          [&](int t, const float4& v) {
+            const int pp = t / n4, q4 = t - pp * n4;
+            *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
+          });
     } else {
       // Rows of 14 or 7 floats (MobileNetV2's last stages): one flat loop over
       // every plane's span, so a block of 36 small planes issues its loads
       // together instead of one plane (49 active lanes) per round trip.
       const int total = np * span;
-#pragma unroll 4
-      for (int t = threadIdx.x; t < total; t += blockDim.x) {
-        const int pp = t / span, q = t - pp * span;
-        tile[(pp * rows_in + (r0 - iy_lo)) * W + q] =
-            x[(int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + q];
-      }
+      stage_batched<8, float>(
+          total,
+          [&](int t) {
+            const int pp = t / span, q = t - pp * span;
+            return x[(int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + q];
+          },
+          [&](int t, float v) {
+            const int pp = t / span, q = t - pp * span;
+            tile[(pp * rows_in + (r0 - iy_lo)) * W + q] = v;
+          });
     }
   }
   __syncthreads();
@@ -484,12 +492,16 @@ __global__ __launch_bounds__(256) void depthwise_lds4_kernel(
   if (r1 > r0) {
     // W % 4 == 0 here (OW % 4 == 0 and W >= (OW - 1) * S + 1 ... checked on the host)
     const int n4 = ((r1 - r0) * W) >> 2, total4 = np * n4;
-#pragma unroll 4
-    for (int t = threadIdx.x; t < total4; t += blockDim.x) {
-      const int pp = t / n4, q4 = t - pp * n4;
-      const float4 v = *(const float4*)(x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + 4 * q4);
-      *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
-    }
+    stage_batched<4, float4>(
+        total4,
+        [&](int t) {
+          const int pp = t / n4, q4 = t - pp * n4;
+          return *(const float4*)(x + (int64_t)(plane0 + pp) * H * W + (int64_t)r0 * W + 4 * q4);
+        },
+        [&](int t, const float4& v) {
+          const int pp = t / n4, q4 = t - pp * n4;
+          *(float4*)(tile + (pp * rows_in + (r0 - iy_lo)) * W + 4 * q4) = v;
+        });
   }
   __syncthreads();
   const int per_plane = RS * CG;
