@@ -10,7 +10,7 @@ usage: rocprof_per_forward.py run_kernel_trace.csv [forwards] [min_period] [--se
 (--seq: also list one forward's dispatches in order, each with its duration
 and the gap since the previous dispatch ended, averaged over the forwards)
 (min_period: dispatches per forward at least -- BERT's layers repeat inside a
-forward, so its period is given as 12 layers x 13 dispatches = 156)"""
+forward, so its period is given as more than 12 layers x 7 dispatches, e.g. 85)"""
 import csv
 import re
 import sys

@@ -31,7 +31,7 @@ for c in "$@"; do
     resnet50_b64) prof resnet50_b64 4 --steps 20 --warmup 3 ;;
     resnet50_b1) prof resnet50_b1 4 --batch 1 --steps 50 --warmup 5 ;;
     mobilenet_v2_b128) prof mobilenet_v2_b128 4 --model mobilenet_v2 --batch 128 --steps 20 --warmup 3 ;;
-    bert_b32) prof bert_b32 156 --model bert --batch 32 --steps 20 --warmup 3 ;;
+    bert_b32) prof bert_b32 85 --model bert --batch 32 --steps 20 --warmup 3 ;;
     pmc_*) m=${c#pmc_}; pmc ${m%_*} ${m##*_} ;;
   esac
 done
