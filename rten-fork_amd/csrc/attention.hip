@@ -33,9 +33,24 @@
 #include <cfloat>
 #include <cmath>
 
+// Timing experiments only (never set in a product build): 1 = no exp / divide,
+// 2 = no Q K^T MFMAs, 3 = no P V MFMAs, 4 = no K / V / Q global loads,
+// 5 = no MFMAs at all (staging, softmax on zeros, stores).
+#ifndef RTENHIP_ATT_EXPERIMENT
+#define RTENHIP_ATT_EXPERIMENT 0
+#endif
+
 namespace rtenhip {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Value of lane l ^ 1 / l ^ 2 within each quad (DPP quad_perm, no LDS trip).
+__device__ __forceinline__ float quad_xor1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float quad_xor2(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, true));
+}
 
 constexpr int AT_D = 64;
 constexpr int AT_S = 128;        // max sequence length (query rows and keys)
@@ -44,7 +59,9 @@ constexpr int VS = AT_D;         // V rows [k][n]: each half-wave reads one row
 constexpr int AT_THREADS = 256;  // 4 waves
 
 // FULL: S == AT_S, every key and row guard folds away at compile time.
-template <bool FULL>
+// VEC: q, k and v rows are 16-byte aligned with unit element stride (checked
+// at launch, attention_vec_ok), so only the float4 staging paths are built.
+template <bool FULL, bool VEC>
 __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   __shared__ float Ks[AT_S * KS];
   __shared__ float Vs[AT_S * VS];
@@ -63,8 +80,8 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   // contiguous floats are read as float4 when 16-byte aligned.  All of a
   // thread's loads are issued before its LDS stores (one memory round trip
   // for the whole staging, not one per row group).
-  const bool v4 = ((uintptr_t)v % 16 == 0) && d.v_s % 4 == 0;
-  const bool k4 = d.k_d == 1 && ((uintptr_t)kt % 16 == 0) && d.k_s % 4 == 0;
+  const bool v4 = VEC || (((uintptr_t)v % 16 == 0) && d.v_s % 4 == 0);
+  const bool k4 = VEC || (d.k_d == 1 && ((uintptr_t)kt % 16 == 0) && d.k_s % 4 == 0);
   constexpr int ST = AT_S * (AT_D / 4) / AT_THREADS;  // float4 positions per thread (8)
   float4 kk[ST], vv[ST];
 #pragma unroll
@@ -72,7 +89,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
     const int t = tid + u * AT_THREADS;
     const int j = t >> 4, c = (t & 15) * 4;
     kk[u] = vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (FULL || j < S) {
+    if ((FULL || j < S) && RTENHIP_ATT_EXPERIMENT != 4) {
       const float* vp = v + (int64_t)j * d.v_s + c;
       vv[u] = v4 ? *(const float4*)vp : make_float4(vp[0], vp[1], vp[2], vp[3]);
       if (k4) {
@@ -105,24 +122,16 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   const int i = i0 + l32;  // this lane's query row
   const bool row_ok = FULL || i < S;
   // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand),
-  // loaded while the K / V stores land.
+  // loaded while the K / V stores land
   float qf[AT_D / 2];
-  if (((uintptr_t)q % 16) == 0 && d.q_s % 4 == 0) {
-    // The whole row as 16 float4s (16 load instructions instead of 32 strided
-    // dwords); this lane keeps elements h and h + 2 of each 4.
-    const float4* qr4 = reinterpret_cast<const float4*>(q + (int64_t)(row_ok ? i : 0) * d.q_s);
-    float4 q4[AT_D / 4];
-#pragma unroll
-    for (int m = 0; m < AT_D / 4; m++) q4[m] = qr4[m];
-#pragma unroll
-    for (int m = 0; m < AT_D / 4; m++) {
-      qf[2 * m] = row_ok ? (h ? q4[m].y : q4[m].x) : 0.f;
-      qf[2 * m + 1] = row_ok ? (h ? q4[m].w : q4[m].z) : 0.f;
-    }
-  } else {
+  // (32 strided dword loads, all in flight together.  Loading the row as
+  // float4s and selecting elements h, h + 2 by lane half turned into a
+  // private-array round trip through scratch.)
+  {
     const float* qr = q + (int64_t)(row_ok ? i : 0) * d.q_s + h;
 #pragma unroll
-    for (int s = 0; s < AT_D / 2; s++) qf[s] = row_ok ? qr[2 * s] : 0.f;
+    for (int s = 0; s < AT_D / 2; s++)
+      qf[s] = RTENHIP_ATT_EXPERIMENT == 4 ? 1.f : row_ok ? qr[2 * s] : 0.f;
   }
   __syncthreads();
   if (i0 >= S) return;  // no barrier follows
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
   for (int t = 0; t < 4; t++) acc[t] = (f32x16){0};
 #pragma unroll
-  for (int s = 0; s < AT_D / 2; s++) {
+  for (int s = 0; s < (RTENHIP_ATT_EXPERIMENT == 2 || RTENHIP_ATT_EXPERIMENT == 5 ? 0 : AT_D / 2); s++) {
     const float* kr = Ks + l32 * KS + 2 * s + h;
 #pragma unroll
     for (int t = 0; t < 4; t++)
@@ -142,25 +151,53 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 
   // Scale and mask (separately rounded, as the Div|Mul and Add operators),
   // then the row max over the keys < S.
-  const float* mrow =
-      (d.mask && row_ok && !mask_lds) ? d.mask + b * d.m_b + hd * d.m_h + (int64_t)i * d.m_i : nullptr;
+  // Each a uniform branch around a whole loop (not one per element).
+  if (d.scale_op == 1) {
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++) acc[t][e] = __fdiv_rn(acc[t][e], d.scale);
+  } else if (d.scale_op == 2) {
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++) acc[t][e] = __fmul_rn(acc[t][e], d.scale);
+  }
+  if (mask_lds) {
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int j = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (FULL || j < S) acc[t][e] = __fadd_rn(acc[t][e], Ms[j]);
+      }
+  } else if (d.mask) {
+    // A per-row mask: the row's 64 values loaded together (clamped to the
+    // last key / row, results past S unused), then added.
+    const float* mrow = d.mask + b * d.m_b + hd * d.m_h + (int64_t)(row_ok ? i : S - 1) * d.m_i;
+    float mk[4][16];
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int j = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+        mk[t][e] = mrow[(int64_t)(FULL ? j : min(j, S - 1)) * d.m_j];
+      }
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int j = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (FULL || j < S) acc[t][e] = __fadd_rn(acc[t][e], mk[t][e]);
+      }
+  }
   float m = -FLT_MAX;
 #pragma unroll
   for (int t = 0; t < 4; t++)
 #pragma unroll
     for (int e = 0; e < 16; e++) {
       const int j = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
-      float x = acc[t][e];
-      if (d.scale_op == 1)
-        x = __fdiv_rn(x, d.scale);
-      else if (d.scale_op == 2)
-        x = __fmul_rn(x, d.scale);
-      if (FULL || j < S) {
-        if (mask_lds) x = __fadd_rn(x, Ms[j]);
-        else if (mrow) x = __fadd_rn(x, mrow[(int64_t)j * d.m_j]);
-        m = rust_max(m, x);
-      }
-      acc[t][e] = x;
+      if (FULL || j < S) m = rust_max(m, acc[t][e]);
     }
   m = rust_max(m, __shfl_xor(m, 32));
 
@@ -172,12 +209,17 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
     for (int g = 0; g < 4; g++)
 #pragma unroll
-      for (int c = 0; c < 4; c++)
-        if (FULL || 32 * t + 8 * g + 4 * h + c < S) {
-          const float ex = vm_exp(__fsub_rn(acc[t][4 * g + c], m));
-          acc[t][4 * g + c] = ex;
-          part[c] = __fadd_rn(part[c], ex);
-        }
+      for (int c = 0; c < 4; c += 2) {
+        // (two keys per packed vm_exp2; a key past S is computed and dropped)
+        vm_f32x2 x = {__fsub_rn(acc[t][4 * g + c], m), __fsub_rn(acc[t][4 * g + c + 1], m)};
+        const vm_f32x2 ex = RTENHIP_ATT_EXPERIMENT == 1 ? x : vm_exp2(x);
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+          if (FULL || 32 * t + 8 * g + 4 * h + c + u < S) {
+            acc[t][4 * g + c + u] = ex[u];
+            part[c + u] = __fadd_rn(part[c + u], ex[u]);
+          }
+      }
   // 0 + p0 + ... + p7 (half 0 holds p0..p3, half 1 p4..p7): both halves fold
   // the same eight values in the same order.
   float other[4];
@@ -188,11 +230,29 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   for (int c = 0; c < 4; c++) sum = __fadd_rn(sum, h ? other[c] : part[c]);
 #pragma unroll
   for (int c = 0; c < 4; c++) sum = __fadd_rn(sum, h ? part[c] : other[c]);
+  const DivBy dv = div_by_init(sum);
+  // p = e / sum: the same-divisor shortcut (vecmath.h div_by) when it is
+  // exact for every value of the wave -- always, unless some e is below
+  // 2^-60 but not 0 -- else the plain division; one wave-uniform branch.
+  bool dok = true;
 #pragma unroll
   for (int t = 0; t < 4; t++)
 #pragma unroll
-    for (int e = 0; e < 16; e++)
-      if (FULL || 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) acc[t][e] = __fdiv_rn(acc[t][e], sum);
+    for (int e = 0; e < 16; e++) dok = dok && div_by_ok(dv, acc[t][e]);
+  if (RTENHIP_ATT_EXPERIMENT == 1) {
+  } else if (__all(dok)) {
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++)
+        if (FULL || 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) acc[t][e] = div_by_fast(dv, acc[t][e]);
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+      for (int e = 0; e < 16; e++)
+        if (FULL || 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) acc[t][e] = __fdiv_rn(acc[t][e], sum);
+  }
 
   // out[i][n] = sum over k < S of P[i][k] V[k][n] in k order.  Keys kb + 0..3
   // of an 8-key group are in half 0, kb + 4..7 in half 1; MFMA step k needs
@@ -206,14 +266,21 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
     for (int g = 0; g < 4; g++) {
       const int kb = 32 * t + 8 * g;
       if (FULL || kb < S) {
-        const float s01 = __shfl_xor(h ? acc[t][4 * g] : acc[t][4 * g + 1], 32);
-        const float s23 = __shfl_xor(h ? acc[t][4 * g + 2] : acc[t][4 * g + 3], 32);
-        const float a[4] = {h ? s01 : acc[t][4 * g], h ? s23 : acc[t][4 * g + 2],
-                            h ? acc[t][4 * g + 1] : s01, h ? acc[t][4 * g + 3] : s23};
+        // v_permlane32_swap exchanges lanes 32..63 of its first operand with
+        // lanes 0..31 of its second (no LDS trip): the first results then
+        // hold keys kb, kb + 2 in half 0 and kb + 1, kb + 3 in half 1, the
+        // second results keys kb + 4, kb + 6 and kb + 5, kb + 7 -- MFMA
+        // steps kb, kb + 2, kb + 4, kb + 6.
+        const auto sw0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][4 * g]),
+                                                          __float_as_uint(acc[t][4 * g + 1]), false, false);
+        const auto sw1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[t][4 * g + 2]),
+                                                          __float_as_uint(acc[t][4 * g + 3]), false, false);
+        const float a[4] = {__uint_as_float(sw0[0]), __uint_as_float(sw1[0]), __uint_as_float(sw0[1]),
+                            __uint_as_float(sw1[1])};
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const int k = kb + 2 * u;  // S even: k < S implies k + 1 < S
-          if (FULL || k < S) {
+          if ((FULL || k < S) && RTENHIP_ATT_EXPERIMENT != 3 && RTENHIP_ATT_EXPERIMENT != 5) {
             const float* vr = Vs + (k + h) * VS + l32;
             o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], vr[0], o[0], 0, 0, 0);
             o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], vr[32], o[1], 0, 0, 0);
@@ -233,33 +300,40 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   }
   if (d.pk) {
     // Packed-A copy for the output projection: a lane quad (4g .. 4g + 3)
-    // holds a 4 x 4 block (rows e & 3 of group e >> 2, one column per lane);
-    // transposed through 4 rotations so lane 4g + c holds row c's 4 columns,
-    // stored as one k-quad (store_packed_a4).  Same values, new places.
+    // holds a 4 x 4 block (lane c: rows 0..3 of column 4g + c); two DPP
+    // exchange steps (partner c ^ 1, then c ^ 2) transpose it so lane c holds
+    // row c's 4 columns, stored as one k-quad (store_packed_a4).  Same values,
+    // new places.
     const int c = l32 & 3, g4 = l32 & ~3;
+    const bool odd = c & 1, hi = c & 2;
 #pragma unroll
     for (int n2 = 0; n2 < 2; n2++)
 #pragma unroll
       for (int a = 0; a < 4; a++) {
-        float w[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-          const int si = (c - t) & 3;  // element this lane sends in round t
-          const float sv = si == 0 ? o[n2][4 * a] : si == 1 ? o[n2][4 * a + 1] : si == 2 ? o[n2][4 * a + 2] : o[n2][4 * a + 3];
-          const float rv = __shfl(sv, h * 32 + g4 + ((c + t) & 3));
-          const int di = (c + t) & 3;  // column of the received value
-          if (t == 0) w[0] = w[1] = w[2] = w[3] = 0.f;
-          w[0] = di == 0 ? rv : w[0];
-          w[1] = di == 1 ? rv : w[1];
-          w[2] = di == 2 ? rv : w[2];
-          w[3] = di == 3 ? rv : w[3];
-        }
+        const float v0 = o[n2][4 * a], v1 = o[n2][4 * a + 1], v2 = o[n2][4 * a + 2], v3 = o[n2][4 * a + 3];
+        const float r0 = quad_xor1(odd ? v0 : v1), r1 = quad_xor1(odd ? v2 : v3);
+        const float x0 = odd ? r0 : v0, x1 = odd ? v1 : r0, x2 = odd ? r1 : v2, x3 = odd ? v3 : r1;
+        const float q0 = quad_xor2(hi ? x0 : x2), q1 = quad_xor2(hi ? x1 : x3);
         const int r = i0 + c + 8 * a + 4 * h;
         if (FULL || r < S)
           store_packed_a4(d.pk, d.pk_lbm, d.pk_lbk, d.pk_tiles_k, (int64_t)b * S + r, hd * AT_D + 32 * n2 + g4,
-                          make_float4(w[0], w[1], w[2], w[3]));
+                          make_float4(hi ? q0 : x0, hi ? q1 : x1, hi ? x2 : q0, hi ? x3 : q1));
       }
   }
+}
+
+// Check of the vecmath.h shortcuts against their plain forms (tests only):
+// out[0, n) = div_by(a / b), out[n, 2n) = __fdiv_rn(a, b), out[2n, 3n) =
+// vm_exp2 on (a[i], a[i ^ 1]) component 0, out[3n, 4n) = vm_exp(a[i]).
+__global__ void vecmath_check_kernel(const float* a, const float* b, int64_t n, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DivBy d = div_by_init(b[i]);
+  out[i] = div_by(d, a[i]);
+  out[n + i] = __fdiv_rn(a[i], b[i]);
+  const int64_t i2 = (i ^ 1) < n ? (i ^ 1) : i;
+  out[2 * n + i] = vm_exp2((vm_f32x2){a[i], a[i2]})[0];
+  out[3 * n + i] = vm_exp(a[i]);
 }
 
 bool attention_fast_ok(const AttnDesc& d) {
@@ -278,12 +352,28 @@ rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s) {
     e.scale_op = 2;
     e.scale = std::ldexp(1.f, 1 - ex);
   }
-  if (d.S == AT_S)
-    hipLaunchKernelGGL(attention_kernel<true>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, e);
+  const auto al16 = [](const float* p) { return (uintptr_t)p % 16 == 0; };
+  const bool vec = al16(d.q) && al16(d.k) && al16(d.v) && d.q_b % 4 == 0 && d.q_h % 4 == 0 &&
+                   d.q_s % 4 == 0 && d.k_d == 1 && d.k_b % 4 == 0 && d.k_h % 4 == 0 && d.k_s % 4 == 0 &&
+                   d.v_b % 4 == 0 && d.v_h % 4 == 0 && d.v_s % 4 == 0;
+  const dim3 grid((unsigned)(d.B * d.H)), block(AT_THREADS);
+  if (d.S == AT_S && vec)
+    hipLaunchKernelGGL((attention_kernel<true, true>), grid, block, 0, s, e);
+  else if (d.S == AT_S)
+    hipLaunchKernelGGL((attention_kernel<true, false>), grid, block, 0, s, e);
+  else if (vec)
+    hipLaunchKernelGGL((attention_kernel<false, true>), grid, block, 0, s, e);
   else
-    hipLaunchKernelGGL(attention_kernel<false>, dim3((unsigned)(d.B * d.H)), dim3(AT_THREADS), 0, s, e);
+    hipLaunchKernelGGL((attention_kernel<false, false>), grid, block, 0, s, e);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }
 
 }  // namespace rtenhip
+
+extern "C" int rtenhip_debug_vecmath_check(const float* a, const float* b, int64_t n, float* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rtenhip::vecmath_check_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, a, b, n, out);
+  return hipGetLastError() == hipSuccess ? 0 : 7;
+}

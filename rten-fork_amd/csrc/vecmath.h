@@ -38,6 +38,82 @@ __device__ __forceinline__ float vm_exp(float x) {
   return r;
 }
 
+// vm_exp on two values at once: the same operations in the same order, the
+// fma / mul / add steps as packed f32 instructions (v_pk_fma_f32 etc., one
+// IEEE-rounded operation per component), so each lane equals vm_exp bit for bit.
+typedef float vm_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ vm_f32x2 vm_exp2(vm_f32x2 x) {
+  const vm_f32x2 INV_LOG2 = {1.44269504088896340736f, 1.44269504088896340736f};
+  const vm_f32x2 MAGIC = {12582912.f, 12582912.f};
+  const vm_f32x2 LN2_HI = {-6.93145752e-1f, -6.93145752e-1f}, LN2_LO = {-1.42860677e-6f, -1.42860677e-6f};
+  vm_f32x2 j = __builtin_elementwise_fma(x, INV_LOG2, MAGIC);
+  j = j - MAGIC;
+  vm_f32x2 r = __builtin_elementwise_fma(j, LN2_HI, x);
+  r = __builtin_elementwise_fma(j, LN2_LO, r);
+  vm_f32x2 t = {1.37805939e-3f, 1.37805939e-3f};
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){8.37312452e-3f, 8.37312452e-3f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){4.16695364e-2f, 4.16695364e-2f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){1.66664720e-1f, 1.66664720e-1f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){4.99999851e-1f, 4.99999851e-1f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){1.0f, 1.0f});
+  r = __builtin_elementwise_fma(t, r, (vm_f32x2){1.0f, 1.0f});
+  vm_f32x2 s1, s2;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const float jc = j[c];
+    const int32_t k = (jc != jc || jc >= 2147483648.f || jc < -2147483648.f) ? INT32_MIN : (int32_t)jc;
+    const uint32_t ia = k > 0 ? 0u : 0x83000000u;
+    s1[c] = __uint_as_float(ia + 0x7f000000u);
+    s2[c] = __uint_as_float(((uint32_t)k << 23) - ia);
+  }
+  r = r * s1;
+  r = r * s2;
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    if (x[c] >= 104.f) r[c] = __builtin_huge_valf();
+    if (x[c] <= -104.f) r[c] = 0.f;
+  }
+  return r;
+}
+
+// a / b for many a over one b (softmax's normalisation).  The compiler's f32
+// division is v_div_scale (both operands), v_rcp, two fma refinements of the
+// reciprocal, three fma quotient steps, v_div_fmas and v_div_fixup; with the
+// divisor in [1, 256] and a == +0 or a in [2^-60, 2] div_scale scales neither
+// operand (VCC = 0, so div_fmas is a plain fma) and div_fixup has nothing to
+// fix, so the same steps without them, the divisor-only ones done once, give
+// __fdiv_rn(a, b) bit for bit (checked on random operands by
+// tests/test_vecmath_gpu.py through rtenhip_debug_div_check).  Other a take
+// __fdiv_rn.
+struct DivBy {
+  float b, nb, r;
+  bool ok;
+};
+__device__ __forceinline__ DivBy div_by_init(float b) {
+  DivBy d;
+  d.b = b;
+  d.nb = -b;
+  const float r0 = __builtin_amdgcn_rcpf(b);
+  d.r = __fmaf_rn(__fmaf_rn(d.nb, r0, 1.f), r0, r0);
+  d.ok = b >= 1.f && b <= 256.f;
+  return d;
+}
+// Whether div_by_fast(d, a) is exact for this a.
+__device__ __forceinline__ bool div_by_ok(const DivBy& d, float a) {
+  return d.ok && (__float_as_uint(a) == 0u || (a >= 0x1p-60f && a <= 2.f));
+}
+// The shortcut alone (callers check div_by_ok first, e.g. once per wave).
+__device__ __forceinline__ float div_by_fast(const DivBy& d, float a) {
+  const float q = __fmul_rn(a, d.r);
+  const float f2 = __fmaf_rn(d.nb, q, a);
+  const float f3 = __fmaf_rn(f2, d.r, q);
+  const float f4 = __fmaf_rn(d.nb, f3, a);
+  return __fmaf_rn(f4, d.r, f3);
+}
+__device__ __forceinline__ float div_by(const DivBy& d, float a) {
+  return div_by_ok(d, a) ? div_by_fast(d, a) : __fdiv_rn(a, d.b);
+}
+
 // simd_sigmoid (exp.rs:144-148): 1 / (1 + exp(0 - x)).
 __device__ __forceinline__ float vm_sigmoid(float x) {
   return __fdiv_rn(1.f, __fadd_rn(1.f, vm_exp(__fsub_rn(0.f, x))));
