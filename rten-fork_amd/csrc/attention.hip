@@ -324,7 +324,8 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 
 // Check of the vecmath.h shortcuts against their plain forms (tests only):
 // out[0, n) = div_by(a / b), out[n, 2n) = __fdiv_rn(a, b), out[2n, 3n) =
-// vm_exp2 on (a[i], a[i ^ 1]) component 0, out[3n, 4n) = vm_exp(a[i]).
+// vm_exp2 on (a[i], a[i ^ 1]) component 0, out[3n, 4n) = vm_exp(a[i]),
+// out[4n, 5n) = vm_gelu2 likewise, out[5n, 6n) = vm_gelu(a[i]).
 __global__ void vecmath_check_kernel(const float* a, const float* b, int64_t n, float* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -334,6 +335,8 @@ __global__ void vecmath_check_kernel(const float* a, const float* b, int64_t n, 
   const int64_t i2 = (i ^ 1) < n ? (i ^ 1) : i;
   out[2 * n + i] = vm_exp2((vm_f32x2){a[i], a[i2]})[0];
   out[3 * n + i] = vm_exp(a[i]);
+  out[4 * n + i] = vm_gelu2((vm_f32x2){a[i], a[i2]})[0];
+  out[5 * n + i] = vm_gelu(a[i]);
 }
 
 bool attention_fast_ok(const AttnDesc& d) {

@@ -786,10 +786,8 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
             x.w = __fadd_rn(x.w, r.w);
           }
           if (gelu) {
-            x.x = vm_gelu(x.x);
-            x.y = vm_gelu(x.y);
-            x.z = vm_gelu(x.z);
-            x.w = vm_gelu(x.w);
+            const vm_f32x2 g0 = vm_gelu2((vm_f32x2){x.x, x.y}), g1 = vm_gelu2((vm_f32x2){x.z, x.w});
+            x = make_float4(g0[0], g0[1], g1[0], g1[1]);
           } else {
             x.x = apply_act_sel(x.x);
             x.y = apply_act_sel(x.y);

@@ -196,6 +196,12 @@ __device__ __forceinline__ float strided_sum_n(const float* p, int s) {
 // instruction advances R rows' chains, where layer_norm_kernel spends a whole
 // wave instruction per add of one row.  Same operations in the same order.
 // LEN > 0: instance for that row length (folds fully unrolled); 0: any.
+// Timing experiments only (never set in a product build): 1 = no packed-A
+// phase, 2 = no serial folds, 3 = no row-major output stores.
+#ifndef RTENHIP_LN_EXPERIMENT
+#define RTENHIP_LN_EXPERIMENT 0
+#endif
+
 template <int LEN>
 __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const float* __restrict__ x, float* __restrict__ y, int64_t rows, int len_arg, int R,
@@ -259,7 +265,9 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   if ((int)threadIdx.x < nr) {
     const int r = threadIdx.x;
     float total;
-    if constexpr (LEN > 0)
+    if constexpr (RTENHIP_LN_EXPERIMENT == 2)
+      total = part[r];
+    else if constexpr (LEN > 0)
       total = strided_sum_n<LEN / 8>(part + r, ps);
     else
       total = strided_sum(part + r, ps, nchunks);
@@ -283,7 +291,9 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const int r = threadIdx.x;
     const float mean = stat[r];
     float sum;
-    if constexpr (LEN > 0)
+    if constexpr (RTENHIP_LN_EXPERIMENT == 2)
+      sum = part[r];
+    else if constexpr (LEN > 0)
       sum = strided_sum_n<(LEN - 1) / 4>(part + r, ps);
     else
       sum = strided_sum(part + r, ps, ngroups);
@@ -314,7 +324,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         o.z = __fadd_rn(o.z, bb[i].z);
         o.w = __fadd_rn(o.w, bb[i].w);
       }
-      y4[r * q + c] = o;
+      if (RTENHIP_LN_EXPERIMENT != 3) y4[r * q + c] = o;
       if (pk.p) lds4[r * q + c] = o;  // this thread's own element: no hazard
     }
   };
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         out_row(r, &sc, &bb, c, 1);
       }
   }
-  if (pk.p) {
+  if (pk.p && RTENHIP_LN_EXPERIMENT != 1) {
     // The MatMul's packed A (packed_a.h): one 16-byte chunk per (k tile,
     // plane, row) with the row fastest, so consecutive threads write
     // consecutive chunks of a plane (rows are 16 bytes apart in it).

@@ -142,6 +142,36 @@ __device__ __forceinline__ float vm_gelu(float x) {
   return __fmul_rn(half_x, y);
 }
 
+// vm_gelu on two values at once (vm_erf inlined): the same operations in the
+// same order, packed where both components take the same one, so each lane
+// equals vm_gelu bit for bit.
+__device__ __forceinline__ vm_f32x2 vm_gelu2(vm_f32x2 x) {
+  const vm_f32x2 zero = {0.f, 0.f}, one = {1.f, 1.f};
+  const vm_f32x2 half_x = x * (vm_f32x2){0.5f, 0.5f};
+  const vm_f32x2 z = x * (vm_f32x2){0.70710678118654752440f, 0.70710678118654752440f};
+  const vm_f32x2 nz = zero - z;
+  vm_f32x2 az;
+  az[0] = z[0] < 0.f ? nz[0] : z[0];
+  az[1] = z[1] < 0.f ? nz[1] : z[1];
+  const vm_f32x2 den = __builtin_elementwise_fma(az, (vm_f32x2){0.3275911f, 0.3275911f}, one);
+  vm_f32x2 t;
+  t[0] = __fdiv_rn(1.f, den[0]);
+  t[1] = __fdiv_rn(1.f, den[1]);
+  vm_f32x2 y = {1.061405429f, 1.061405429f};
+  y = __builtin_elementwise_fma(y, t, (vm_f32x2){-1.453152027f, -1.453152027f});
+  y = __builtin_elementwise_fma(y, t, (vm_f32x2){1.421413741f, 1.421413741f});
+  y = __builtin_elementwise_fma(y, t, (vm_f32x2){-0.284496736f, -0.284496736f});
+  y = __builtin_elementwise_fma(y, t, (vm_f32x2){0.254829592f, 0.254829592f});
+  const vm_f32x2 at = y * t;
+  const vm_f32x2 e = vm_exp2(zero - az * az);
+  const vm_f32x2 r = one - at * e;
+  const vm_f32x2 nr = zero - r;
+  vm_f32x2 erf;
+  erf[0] = z[0] < 0.f ? nr[0] : r[0];
+  erf[1] = z[1] < 0.f ? nr[1] : r[1];
+  return half_x * (erf + one);
+}
+
 // simd_tanh (tanh.rs:14-65).
 __device__ __forceinline__ float vm_tanh(float x) {
   const bool x_neg = x <= 0.f;

@@ -3,7 +3,9 @@ plain forms, bit for bit, on random and edge operands:
 - div_by: softmax's p = e / sum with the divisor-only steps of the compiler's
   f32 division done once (used by the attention kernel), vs __fdiv_rn;
 - vm_exp2: two vm_exp (rten-vecmath exp.rs:12-80 restatement) as packed f32
-  operations, vs vm_exp.
+  operations, vs vm_exp;
+- vm_gelu2: two vm_gelu (erf.rs:29-91) as packed operations (the GEMM
+  epilogue's Gelu), vs vm_gelu.
 Called through rtenhip_debug_vecmath_check (a test-only entry point)."""
 import ctypes
 
@@ -28,10 +30,10 @@ def lib():
 def _run(lib, a, b):
     import torch
     ad, bd = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
-    out = torch.empty(4 * a.size, dtype=torch.float32, device="cuda")
+    out = torch.empty(6 * a.size, dtype=torch.float32, device="cuda")
     assert lib.rtenhip_debug_vecmath_check(ad.data_ptr(), bd.data_ptr(), a.size, out.data_ptr(), None) == 0
     torch.cuda.synchronize()
-    return out.cpu().numpy().reshape(4, a.size)
+    return out.cpu().numpy().reshape(6, a.size)
 
 
 def _bits(x):
@@ -64,3 +66,13 @@ def test_vm_exp2_matches_vm_exp(lib):
     x[:6] = [np.inf, -np.inf, np.nan, 104.0, -104.0, 0.0]
     o = _run(lib, x, np.ones_like(x))
     assert np.array_equal(_bits(o[2]), _bits(o[3]))
+
+
+def test_vm_gelu2_matches_vm_gelu(lib):
+    rng = np.random.default_rng(3)
+    n = 1 << 22
+    x = np.concatenate([rng.normal(0, 3, n // 2), rng.uniform(-2000, 2000, n // 4),
+                        rng.uniform(-1e-3, 1e-3, n // 4)]).astype(np.float32)
+    x[:7] = [np.inf, -np.inf, np.nan, 0.0, -0.0, 1e-40, -1e-40]
+    o = _run(lib, x, np.ones_like(x))
+    assert np.array_equal(_bits(o[4]), _bits(o[5]))
