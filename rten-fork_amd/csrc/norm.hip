@@ -345,9 +345,14 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const int BK = 1 << pk.lbk, nq = BK >> 2;
     const int ktiles = (len + BK - 1) >> pk.lbk;
     const int total = nr * nq * ktiles;
+    // (A full block of an instance has nr = R known at compile time (the host
+    // picks R the same way): the index split below is then shifts and
+    // multiplies instead of two integer divisions per chunk.)
+    constexpr int RC = LEN > 0 ? (6144 / LEN < 16 ? 6144 / LEN : 16) : 0;
+    const bool rc = RC > 0 && nr == RC;
     for (int i = threadIdx.x; i < total; i += 256) {
-      const int r = i % nr, t2 = i / nr;
-      const int qq = t2 % nq, tk = t2 / nq;
+      const int r = rc ? i % (RC > 0 ? RC : 1) : i % nr, t2 = rc ? i / (RC > 0 ? RC : 1) : i / nr;
+      const int qq = t2 & (nq - 1), tk = t2 >> (pk.lbk - 2);
       const int kb = tk * BK + 8 * (qq >> 1) + (qq & 1);
       const float* xr = xs + r * len;
       const float4 v = make_float4(kb < len ? xr[kb] : 0.f, kb + 2 < len ? xr[kb + 2] : 0.f,
