@@ -65,6 +65,11 @@ struct DmaDesc {
   // item), enforced with LDS padding so that every CU holds exactly that many;
   // items are dealt out statically per XCD (see gemm_dma_kernel).
   int persist_k;
+  // Tile order (0: m tile fastest).  swz > 0: strips of swz tile columns, the
+  // tiles of a strip row by row (n fastest within the strip), so a run of
+  // consecutive tiles -- what one XCD's resident blocks work on together --
+  // is a compact block of A rows and B columns in that XCD's L2.
+  int swz;
   int bvec;                 // B copied 16 bytes per lane (dma_cfg_bvec(cfg) and pointwise:
                             // koff(k) = k * kstride, P % 4 == 0, K % BK == 0)
   int kstride;              // elements between consecutive k rows of B (bvec)

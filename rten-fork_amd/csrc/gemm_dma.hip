@@ -106,6 +106,15 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
   dd.dbg = g_dma_dbg;
   dd.stamps = g_dma_stamps;
   if (g_dma_persist >= 0) dd.persist_k = g_dma_persist;
+  {
+    // Tile-order experiments (DmaDesc::swz): RTENHIP_DMA_SWZ=g strips of g tile
+    // columns for every DMA GEMM; RTENHIP_DMA_SWZ_MM=g for dense MatMuls only
+    // (P == N: no image structure).
+    static const int swz_all = [] { const char* e = getenv("RTENHIP_DMA_SWZ"); return e ? atoi(e) : -1; }();
+    static const int swz_mm = [] { const char* e = getenv("RTENHIP_DMA_SWZ_MM"); return e ? atoi(e) : -1; }();
+    if (swz_all >= 0) dd.swz = swz_all;
+    if (swz_mm >= 0 && d.P == d.N) dd.swz = swz_mm;
+  }
   const DmaCfgInfo& ci = kDmaCfgs[cfg];
   const int tiles = ((d.M + ci.bm - 1) / ci.bm) * ((d.N + ci.bn - 1) / ci.bn);
   if (d.split_tiles > 0) {

@@ -175,10 +175,20 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = (wave / WAVES_N) * WM;
   const int wn = (wave % WAVES_N) * WN;
-  const int tmi = wg % tiles_m;
-  const int tm = tmi * BM;
-  const int tn = (wg / tiles_m) * BN;
   const int M = d.M, N = d.N, K = d.K;
+  int tmi, tni;
+  if (d.swz > 0) {  // strips of swz tile columns, n fastest within a strip (see DmaDesc::swz)
+    const int tiles_n = (N + BN - 1) / BN, sw = d.swz * tiles_m;
+    const int st = wg / sw, r = wg - st * sw;
+    const int gw = min(d.swz, tiles_n - st * d.swz);
+    tmi = r / gw;
+    tni = st * d.swz + (r - tmi * gw);
+  } else {
+    tmi = wg % tiles_m;
+    tni = wg / tiles_m;
+  }
+  const int tm = tmi * BM;
+  const int tn = tni * BN;
   const int tiles_k = (K + BK - 1) / BK;
   constexpr int TPB = DKC / BK;  // K tiles per KC block
   const int kt_lo = kb_split >= 0 ? kb_split * TPB : 0;
