@@ -7,6 +7,7 @@ trailing dispatches, cut into forwards by the period of the kernel-name
 sequence, and reports per kernel (template arguments dropped) the time and
 launches per forward and the average launch duration.
 usage: rocprof_per_forward.py run_kernel_trace.csv [forwards] [min_period] [--seq]
+(ROCclr fill / copy kernels are counted like any other dispatch.)
 (--seq: also list one forward's dispatches in order, each with its duration
 and the gap since the previous dispatch ended, averaged over the forwards)
 (min_period: dispatches per forward at least -- BERT's layers repeat inside a
@@ -28,7 +29,9 @@ def main():
     path = argv[1]
     want = int(argv[2]) if len(argv) > 2 else 10
     min_period = int(argv[3]) if len(argv) > 3 else 4
-    rows = [r for r in csv.DictReader(open(path)) if "rocclr" not in r["Kernel_Name"]]
+    # ROCclr's own fill / copy kernels (hipMemsetAsync / hipMemcpyAsync inside
+    # the step) are kept: they are part of the forward and explain gaps.
+    rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     # smallest period p of the trailing sequence that repeats at least twice
