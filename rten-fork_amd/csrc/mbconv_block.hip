@@ -1,0 +1,456 @@
+// MobileNetV2 inverted residual block in one kernel: 1x1 expand (+ bias,
+// Clip) -> 3x3 depthwise (+ bias, Clip) -> 1x1 project (+ bias) [+ the
+// block's residual Add], with neither the expanded nor the depthwise
+// activation ever written to HBM.  At batch 128 those two intermediates are
+// ~5.5 GB of the ~5.8 GB a MobileNetV2 step moves when the three convs run
+// apart.
+//
+// Arithmetic is exactly that of the three operators run apart (bit-identical
+// to the unfused graph and to RTen):
+//  - expand, conv_2d_pointwise (src/ops/conv.rs:24-68, K = C_in < 256: one
+//    KC block): the k-ordered fma chain from +0 (kernels.rs:206-316) as
+//    v_mfma_f32_16x16x4f32 steps (bitwise that chain), then + bias
+//    (gemm.rs:1034-1047), then the fused Clip / Relu;
+//  - depthwise, conv_2d_depthwise_block (src/ops/conv/depthwise.rs:49-120):
+//    bias, then + v * w per tap in ky, kx order with separate roundings,
+//    skipping rows outside the image and columns outside the reference's
+//    min_max_out_x_coords range, then Clip / Relu;
+//  - project, conv_2d_pointwise with K = hidden: one fma chain per KC = 256
+//    block from +0 (MFMA steps again), block 0 + bias, later blocks added in
+//    K order (gemm.rs:733-1050), then the residual Add and the activation.
+//
+// Mapping: a workgroup owns one image and a band of TR output rows, all
+// output channels.  The band's input rows (clipped to the image) are staged
+// in LDS once as X[c][pixel].  The hidden channels are walked in chunks of
+// 16 (one MFMA tile of rows):
+//  1. expand: the chunk's 16 channels at every band input pixel, 16x16
+//     MFMA tiles (16 channels x 16 pixels) split over the waves, into the
+//     LDS plane set E[chunk % 2][16][pixel] (double-buffered: one barrier per
+//     chunk);
+//  2. depthwise + project: wave w owns output pixel tiles w, w + NW, ...;
+//     lane (c, h) forms the depthwise outputs of channels h, h + 4, h + 8,
+//     h + 12 at pixel c of the tile -- exactly the project MFMA's B operand
+//     for k = 4s + h, s = 0..3 -- and feeds them straight into the project
+//     accumulators (all output channels of that tile).  The depthwise values
+//     never leave registers.
+// Weights are repacked once per plan (pack_mbconv_block) into the lanes'
+// operand order: one float4 load per lane per MFMA group.
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "stage.h"
+#include "vecmath.h"
+
+namespace rtenhip {
+
+typedef float mb_f32x4 __attribute__((ext_vector_type(4)));
+
+struct MbBlockDesc {
+  const float* x;    // [N, CIN, H, W]
+  const float* pk;   // packed weights (mbconv_block_pack_floats)
+  const float* res;  // residual [N, COUT, OH, OW] (null: none); res_lds: it is x (read from the staged band)
+  float* y;          // [N, COUT, OH, OW]
+  int hid, cout, H, W, OH, OW, pt, pl;
+  int TR;            // output rows per band
+  int RX, RE;        // LDS row strides (floats) of X and E
+  int res_lds;
+  int act_e, act_d, act_p;
+  float lo_e, hi_e, lo_d, hi_d, lo_p, hi_p;
+  int omin[3], omax[3];  // min_max_out_x_coords per kx (depthwise.rs:24-38)
+  int has_be, has_bd, has_bp;
+};
+
+// Packed record sizes (floats).  Per 16-channel chunk: expand A operand
+// [GE][64 lanes][4], expand bias [4 h][4], depthwise [4 h][9 taps][4],
+// depthwise bias [4 h][4], project A operand [MT][64][4]; then the project
+// bias [MT][4 h][4].
+__host__ __device__ inline int mb_ge(int cin) { return (cin + 15) / 16; }
+__host__ __device__ inline int mb_chunk_floats(int cin, int mt) { return mb_ge(cin) * 256 + 16 + 144 + 16 + mt * 256; }
+
+__device__ __forceinline__ float mb_act(float v, int act, float lo, float hi) {
+  if (act == RTENHIP_ACT_RELU) return rust_max(v, 0.f);
+  if (act == RTENHIP_ACT_CLIP) return rust_clamp(v, lo, hi);
+  return v;
+}
+
+// NT threads; S stride; CIN input channels; MT = ceil(COUT / 16) project
+// row tiles; MAXT = output pixel tiles per wave (host-checked).
+template <int NT, int S, int CIN, int MT, int MAXT>
+__global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
+  constexpr int NW = NT / 64;
+  constexpr int KS = CIN / 4;  // expand MFMA steps
+  constexpr int GE = (CIN + 15) / 16;
+  extern __shared__ float4 mb_lds4[];
+  float* X = reinterpret_cast<float*>(mb_lds4);  // [CIN][RX]
+  float* E = X + CIN * d.RX;                      // [2][16][RE]
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c = lane & 15, h = lane >> 4;
+  const int n = blockIdx.y;
+  const int oy0 = blockIdx.x * d.TR;
+  const int orows = min(d.TR, d.OH - oy0);
+  const int ia = max(0, oy0 * S - d.pt);
+  const int ib = min(d.H, (oy0 + orows - 1) * S - d.pt + 3);  // input rows [ia, ib) of the band
+  const int W = d.W, OW = d.OW;
+  const int pin = (ib - ia) * W, pout = orows * OW;
+  const int tin = (pin + 15) >> 4, tout = (pout + 15) >> 4;
+  const int64_t HW = (int64_t)d.H * W;
+
+  // Stage the band: X[ci][(iy - ia) * W + ix] = x[n][ci][iy][ix].
+  {
+    const float* xb = d.x + (int64_t)n * CIN * HW + (int64_t)ia * W;
+    const int total = CIN * pin;
+    if ((pin & 3) == 0 && (HW & 3) == 0 && ((uintptr_t)xb & 15) == 0 && (d.RX & 3) == 0) {
+      const int q = pin >> 2;
+      stage_batched<8, float4>(
+          total >> 2, [&](int e) { const int ci = e / q; return *reinterpret_cast<const float4*>(xb + ci * HW + 4 * (e - ci * q)); },
+          [&](int e, const float4& v) { const int ci = e / q; *reinterpret_cast<float4*>(X + ci * d.RX + 4 * (e - ci * q)) = v; });
+    } else {
+      stage_batched<8, float>(
+          total, [&](int e) { const int ci = e / pin; return xb[ci * HW + (e - ci * pin)]; },
+          [&](int e, float v) { const int ci = e / pin; X[ci * d.RX + (e - ci * pin)] = v; });
+    }
+  }
+
+  // This lane's output pixels (column c of each owned tile): the depthwise
+  // tap base (E offset of tap (0, 0)) and the 9-bit tap mask.
+  int tbase[MAXT];
+  uint32_t tmask[MAXT];
+#pragma unroll
+  for (int u = 0; u < MAXT; u++) {
+    const int tile = wave + u * NW;
+    const int o = tile * 16 + c;
+    const int ol = min(o, pout - 1) / OW, ox = min(o, pout - 1) - (min(o, pout - 1) / OW) * OW;
+    const int oy = oy0 + ol;
+    uint32_t m = 0;
+#pragma unroll
+    for (int ky = 0; ky < 3; ky++) {
+      const int r = oy * S + ky - d.pt;
+      const bool row_ok = r >= 0 && r < d.H;
+#pragma unroll
+      for (int kx = 0; kx < 3; kx++)
+        m |= (tile < tout && o < pout && row_ok && ox >= d.omin[kx] && ox < d.omax[kx]) ? 1u << (ky * 3 + kx) : 0u;
+    }
+    tmask[u] = m;
+    tbase[u] = (oy * S - d.pt - ia) * W + ox * S - d.pl;  // may be negative: only masked taps go out of range
+  }
+
+  const int nchunks = d.hid >> 4;
+  const int cf = mb_chunk_floats(CIN, MT);
+  const float4* pk4 = reinterpret_cast<const float4*>(d.pk);
+  // Project accumulators (current KC block) and the folded sum.
+  mb_f32x4 acc[MAXT][MT], sum[MAXT][MT];
+#pragma unroll
+  for (int u = 0; u < MAXT; u++)
+#pragma unroll
+    for (int m = 0; m < MT; m++) acc[u][m] = sum[u][m] = (mb_f32x4){0.f, 0.f, 0.f, 0.f};
+  bool folded = false;  // block 0 folded into sum (with the project bias)
+  const float4* bp4 = pk4 + (int64_t)nchunks * (cf >> 2);  // [MT][4][4]
+
+  __syncthreads();  // X staged
+
+  for (int ch = 0; ch < nchunks; ch++) {
+    const float4* rec = pk4 + (int64_t)ch * (cf >> 2);
+    float* Eb = E + (ch & 1) * 16 * d.RE;
+    // 1. Expand: tiles of 16 channels x 16 band pixels, wave-strided.
+    {
+      float4 wa[GE];
+#pragma unroll
+      for (int g = 0; g < GE; g++) wa[g] = rec[g * 64 + lane];
+      const float4 be = rec[GE * 64 + h];
+      for (int tile = wave; tile < tin; tile += NW) {
+        mb_f32x4 e = {0.f, 0.f, 0.f, 0.f};
+        const float* xc = X + h * d.RX + tile * 16 + c;
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+          const float a = s % 4 == 0 ? wa[s / 4].x : s % 4 == 1 ? wa[s / 4].y : s % 4 == 2 ? wa[s / 4].z : wa[s / 4].w;
+          e = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xc[4 * s * d.RX], e, 0, 0, 0);
+        }
+        // Lane (c, h) holds channels 4h + r of pixel tile * 16 + c.
+        float v[4] = {e[0], e[1], e[2], e[3]};
+        const float bb[4] = {be.x, be.y, be.z, be.w};
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          if (d.has_be) v[r] = __fadd_rn(v[r], bb[r]);
+          Eb[(4 * h + r) * d.RE + tile * 16 + c] = mb_act(v[r], d.act_e, d.lo_e, d.hi_e);
+        }
+      }
+    }
+    __syncthreads();  // chunk ch's expand planes complete (and chunk ch - 1's reads of the other buffer done)
+    // 2. Depthwise (channels h + 4j of this lane's pixel) -> project MFMAs.
+    {
+      const float4* dwr = rec + GE * 64 + 4;
+      float4 wd[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) wd[k] = dwr[h * 9 + k];
+      const float4 bd = dwr[36 + h];
+      float4 wp[MT];
+#pragma unroll
+      for (int m = 0; m < MT; m++) wp[m] = dwr[40 + m * 64 + lane];
+      const int ky_off[3] = {0, W, 2 * W};
+#pragma unroll
+      for (int u = 0; u < MAXT; u++) {
+        if (wave + u * NW >= tout) break;
+        float dv[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const float* ep = Eb + (h + 4 * j) * d.RE;
+          float a = d.has_bd ? (j == 0 ? bd.x : j == 1 ? bd.y : j == 2 ? bd.z : bd.w) : 0.f;
+#pragma unroll
+          for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+            for (int kx = 0; kx < 3; kx++) {
+              const int k = ky * 3 + kx;
+              const bool on = (tmask[u] >> k) & 1u;
+              const float ev = ep[on ? tbase[u] + ky_off[ky] + kx : 0];
+              const float w = j == 0 ? wd[k].x : j == 1 ? wd[k].y : j == 2 ? wd[k].z : wd[k].w;
+              const float s = __fadd_rn(a, __fmul_rn(ev, w));
+              a = on ? s : a;
+            }
+          dv[j] = mb_act(a, d.act_d, d.lo_d, d.hi_d);
+        }
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+          acc[u][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[m].x, dv[0], acc[u][m], 0, 0, 0);
+          acc[u][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[m].y, dv[1], acc[u][m], 0, 0, 0);
+          acc[u][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[m].z, dv[2], acc[u][m], 0, 0, 0);
+          acc[u][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(wp[m].w, dv[3], acc[u][m], 0, 0, 0);
+        }
+      }
+    }
+    // End of a KC block of the project chain (every 16 chunks) or of K.
+    if (((ch + 1) & 15) == 0 || ch + 1 == nchunks) {
+#pragma unroll
+      for (int u = 0; u < MAXT; u++)
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+          const float4 bp = bp4[m * 4 + h];
+          const float bb[4] = {bp.x, bp.y, bp.z, bp.w};
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            if (!folded)
+              sum[u][m][r] = d.has_bp ? __fadd_rn(acc[u][m][r], bb[r]) : acc[u][m][r];
+            else
+              sum[u][m][r] = __fadd_rn(sum[u][m][r], acc[u][m][r]);
+          }
+          acc[u][m] = (mb_f32x4){0.f, 0.f, 0.f, 0.f};
+        }
+      folded = true;
+    }
+  }
+
+  // Epilogue: residual, activation, store.  Lane (c, h) holds output
+  // channels 16m + 4h + r of pixel tile * 16 + c.
+#pragma unroll
+  for (int u = 0; u < MAXT; u++) {
+    const int tile = wave + u * NW;
+    const int o = tile * 16 + c;
+    if (tile >= tout) break;
+    const bool ok = o < pout;
+    const int ol = min(o, pout - 1) / OW, ox = min(o, pout - 1) - ol * OW;
+    const int oy = oy0 + ol;
+    const int64_t opix = (int64_t)oy * OW + ox;
+#pragma unroll
+    for (int m = 0; m < MT; m++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int co = 16 * m + 4 * h + r;
+        if (co >= d.cout || !ok) continue;
+        float v = sum[u][m][r];
+        if (d.res_lds)
+          v = __fadd_rn(v, X[co * d.RX + (oy - ia) * W + ox]);
+        else if (d.res)
+          v = __fadd_rn(v, d.res[((int64_t)n * d.cout + co) * d.OH * OW + opix]);
+        d.y[((int64_t)n * d.cout + co) * d.OH * OW + opix] = mb_act(v, d.act_p, d.lo_p, d.hi_p);
+      }
+  }
+}
+
+// Host side --------------------------------------------------------------
+
+int mbconv_block_pack_floats(int cin, int hid, int cout) {
+  const int mt = (cout + 15) / 16;
+  return (hid / 16) * mb_chunk_floats(cin, mt) + mt * 16;
+}
+
+// Repack the three convs' weights and biases into the lanes' operand order
+// (see MbBlockDesc / the kernel): we [hid][cin], be [hid], wd [hid][9], bd
+// [hid], wp [cout][hid], bp [cout] (biases may be null: zeros).
+void mbconv_block_pack(const float* we, const float* be, const float* wd, const float* bd, const float* wp,
+                       const float* bp, int cin, int hid, int cout, float* out) {
+  const int mt = (cout + 15) / 16, ge = mb_ge(cin), cf = mb_chunk_floats(cin, mt);
+  for (int ch = 0; ch < hid / 16; ch++) {
+    float* r = out + (size_t)ch * cf;
+    const int h0 = ch * 16;
+    // Expand A: lane L: row h0 + L % 16, step s = 4g + i covers k = 4s + L / 16.
+    for (int g = 0; g < ge; g++)
+      for (int L = 0; L < 64; L++)
+        for (int i = 0; i < 4; i++) {
+          const int k = 4 * (4 * g + i) + L / 16;
+          r[(g * 64 + L) * 4 + i] = k < cin ? we[(size_t)(h0 + L % 16) * cin + k] : 0.f;
+        }
+    r += ge * 256;
+    // Expand bias: [h][r] = be[h0 + 4h + r].
+    for (int i = 0; i < 16; i++) r[i] = be ? be[h0 + i] : 0.f;
+    r += 16;
+    // Depthwise: [h][tap][j] = wd[h0 + h + 4j][tap]; bias [h][j].
+    for (int h = 0; h < 4; h++)
+      for (int k = 0; k < 9; k++)
+        for (int j = 0; j < 4; j++) r[(h * 9 + k) * 4 + j] = wd[(size_t)(h0 + h + 4 * j) * 9 + k];
+    r += 144;
+    for (int h = 0; h < 4; h++)
+      for (int j = 0; j < 4; j++) r[h * 4 + j] = bd ? bd[h0 + h + 4 * j] : 0.f;
+    r += 16;
+    // Project A: tile m, lane L: row 16m + L % 16, step s covers k = h0 + 4s + L / 16.
+    for (int m = 0; m < mt; m++)
+      for (int L = 0; L < 64; L++)
+        for (int s = 0; s < 4; s++) {
+          const int o = 16 * m + L % 16;
+          r[(m * 64 + L) * 4 + s] = o < cout ? wp[(size_t)o * hid + h0 + 4 * s + L / 16] : 0.f;
+        }
+  }
+  float* b = out + (size_t)(hid / 16) * cf;
+  for (int m = 0; m < mt; m++)
+    for (int i = 0; i < 16; i++) b[m * 16 + i] = (bp && 16 * m + i < cout) ? bp[16 * m + i] : 0.f;
+}
+
+namespace {
+// The instantiated shapes (MobileNetV2's blocks features.2 .. features.13):
+// stride, C_in, project row tiles ceil(C_out / 16), threads per workgroup.
+// 512 threads where the accumulators of 4 tiles per wave would not fit.
+struct MbInst {
+  int S, cin, mt, nt;
+};
+constexpr MbInst kMbInsts[] = {{2, 16, 2, 256}, {1, 24, 2, 256}, {2, 24, 2, 256}, {1, 32, 2, 256},
+                               {2, 32, 4, 512}, {1, 64, 4, 512}, {1, 64, 6, 512}, {1, 96, 6, 512}};
+
+const MbInst* mb_inst(int S, int cin, int mt) {
+  for (const MbInst& m : kMbInsts)
+    if (m.S == S && m.cin == cin && m.mt == mt) return &m;
+  return nullptr;
+}
+
+struct MbGeom {
+  int TR, RX, RE, NT, MAXT;
+  size_t lds;
+};
+
+// Band height and LDS layout: the most output rows whose staged input band
+// and two expand plane sets fit 72 KB (two workgroups per CU), with at most
+// 4 (256 threads) / 2 (512 threads) output pixel tiles per wave.  Row
+// strides: X rows are read 16 consecutive floats per half-wave (2 rows per
+// 32-lane group): stride = 16 (mod 32); E rows are read at pixel steps of S:
+// stride 16 (mod 32) for S = 1, odd for S = 2.
+bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, MbGeom& g) {
+  const MbInst* in = mb_inst(S, cin, (cout + 15) / 16);
+  if (!in) return false;
+  const size_t budget = 72 * 1024;
+  const int nt = in->nt, nw = nt / 64, maxt = nt == 256 ? 4 : 2;
+  for (int tr = OH; tr >= 1; tr--) {
+    const int rows = std::min(H, (tr - 1) * S + 3);  // input rows of the widest band
+    const int tin16 = (rows * W + 15) / 16 * 16;
+    int rx = tin16;
+    while (rx % 32 != 16) rx++;
+    int re = tin16;
+    if (S == 1)
+      while (re % 32 != 16) re++;
+    else if (re % 2 == 0)
+      re++;
+    const size_t lds = ((size_t)cin * rx + 2 * 16 * (size_t)re) * sizeof(float);
+    const int tout = (tr * OW + 15) / 16;
+    if (lds > budget || (tout + nw - 1) / nw > maxt) continue;
+    g.TR = tr;
+    g.RX = rx;
+    g.RE = re;
+    g.NT = nt;
+    g.MAXT = maxt;
+    g.lds = lds;
+    return true;
+  }
+  return false;
+}
+}  // namespace
+
+// Whether the fused kernel takes this block: an instantiated (stride, C_in,
+// C_out) shape (kMbInsts), 3x3 depthwise with pads <= 1, hidden a multiple
+// of 16, and a band that fits LDS.  RTENHIP_MBCONV=0 disables the fusion.
+bool mbconv_block_eligible(int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl, int pb,
+                           int pr) {
+  const char* e = getenv("RTENHIP_MBCONV");
+  if (e && strcmp(e, "0") == 0) return false;
+  if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
+  if (hid % 16 != 0 || hid <= 0 || cout <= 0) return false;
+  MbGeom g;
+  return mb_geom(cin, cout, H, W, OH, OW, S, g);
+}
+
+rtenhip_status launch_mbconv_block(const float* x, const float* pk, const float* res, bool res_is_x, float* y, int N,
+                                   int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl,
+                                   int act_e, float lo_e, float hi_e, int act_d, float lo_d, float hi_d, int act_p,
+                                   float lo_p, float hi_p, bool has_be, bool has_bd, bool has_bp, hipStream_t s) {
+  if ((int64_t)N * cout * OH * OW == 0) return RTENHIP_OK;
+  MbGeom g;
+  if (hid % 16 != 0 || !mb_geom(cin, cout, H, W, OH, OW, S, g))
+    return fail(RTENHIP_UNSUPPORTED_VALUE, "inverted residual block: unsupported shape");
+  if (res_is_x && (S != 1 || cin != cout || OH != H || OW != W))
+    return fail(RTENHIP_INVALID_VALUE, "inverted residual block: residual shape");
+  if (N > 65535) return fail(RTENHIP_UNSUPPORTED_VALUE, "inverted residual block: batch too large");
+  MbBlockDesc d{};
+  d.x = x;
+  d.pk = pk;
+  d.res = res_is_x ? nullptr : res;
+  d.res_lds = res_is_x ? 1 : 0;
+  d.y = y;
+  d.hid = hid;
+  d.cout = cout;
+  d.H = H;
+  d.W = W;
+  d.OH = OH;
+  d.OW = OW;
+  d.pt = pt;
+  d.pl = pl;
+  d.TR = g.TR;
+  d.RX = g.RX;
+  d.RE = g.RE;
+  d.act_e = act_e;
+  d.lo_e = lo_e;
+  d.hi_e = hi_e;
+  d.act_d = act_d;
+  d.lo_d = lo_d;
+  d.hi_d = hi_d;
+  d.act_p = act_p;
+  d.lo_p = lo_p;
+  d.hi_p = hi_p;
+  d.has_be = has_be;
+  d.has_bd = has_bd;
+  d.has_bp = has_bp;
+  for (int kx = 0; kx < 3; kx++) {
+    d.omin[kx] = pl - kx > 0 ? pl - kx : 0;
+    const int t = W + pl - kx > 0 ? W + pl - kx : 0;
+    const int omax = (t + S - 1) / S;
+    d.omax[kx] = omax > OW ? OW : omax;
+  }
+  const int bands = (OH + g.TR - 1) / g.TR;
+  const dim3 grid((unsigned)bands, (unsigned)N);
+  const int mt = (cout + 15) / 16;
+#define MB_LAUNCH(S_, CIN_, MT_, NT_)                                                                         \
+  if (S == S_ && cin == CIN_ && mt == MT_) {                                                                 \
+    hipLaunchKernelGGL((mbconv_block_kernel<NT_, S_, CIN_, MT_, NT_ == 256 ? 4 : 2>), grid, dim3(NT_), g.lds, s, d); \
+    RTENHIP_LAUNCH_CHECK();                                                                                   \
+    return RTENHIP_OK;                                                                                        \
+  }
+  MB_LAUNCH(2, 16, 2, 256)
+  MB_LAUNCH(1, 24, 2, 256)
+  MB_LAUNCH(2, 24, 2, 256)
+  MB_LAUNCH(1, 32, 2, 256)
+  MB_LAUNCH(2, 32, 4, 512)
+  MB_LAUNCH(1, 64, 4, 512)
+  MB_LAUNCH(1, 64, 6, 512)
+  MB_LAUNCH(1, 96, 6, 512)
+#undef MB_LAUNCH
+  return fail(RTENHIP_UNSUPPORTED_VALUE, "inverted residual block: unsupported shape");
+}
+
+}  // namespace rtenhip
