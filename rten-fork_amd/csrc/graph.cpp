@@ -804,35 +804,41 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       const Node& pn = nodes[op];
       if (pn.op_type != "Conv" || pn.fb_op < 0 || !in_plan.count(pn.fb_op)) continue;
       const Node& dn = nodes[pn.fb_op];
-      if (dn.fe_op < 0 || !in_plan.count(dn.fe_op)) continue;
-      const Node& en = nodes[dn.fe_op];
-      if (outset0.count(dn.outputs[0]) || outset0.count(en.outputs[0]) || uses_of_value(p.ops, dn.outputs[0]) != 1 ||
-          uses_of_value(p.ops, en.outputs[0]) != 1 || dn.inputs[0] != en.outputs[0] || pn.inputs[0] != dn.outputs[0])
+      // With the expand (fe_op in this plan) or as depthwise -> project.
+      const bool expand = dn.fe_op >= 0 && in_plan.count(dn.fe_op);
+      if (dn.fe_op >= 0 && !expand) continue;
+      const Node& en = nodes[expand ? dn.fe_op : pn.fb_op];  // without an expand: the depthwise op reads x
+      const int xv = en.inputs[0];
+      if (outset0.count(dn.outputs[0]) || uses_of_value(p.ops, dn.outputs[0]) != 1 || pn.inputs[0] != dn.outputs[0])
         continue;
-      const Shape* xs = shape_of(en.inputs[0]);
+      if (expand && (outset0.count(en.outputs[0]) || uses_of_value(p.ops, en.outputs[0]) != 1 ||
+                     dn.inputs[0] != en.outputs[0]))
+        continue;
+      const Shape* xs = shape_of(xv);
       const Shape* ys = shape_of(pn.outputs[0]);
-      if (!xs || !ys || xs->size() != 4 || ys->size() != 4 || p.dtypes[en.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
-      const Shape& wes = nodes[en.inputs[1]].shape;
+      if (!xs || !ys || xs->size() != 4 || ys->size() != 4 || p.dtypes[xv] == RTENHIP_DTYPE_INT32) continue;
+      const Shape& wes = nodes[dn.inputs[1]].shape;  // [hidden, 1, 3, 3]
       const Shape& wps = nodes[pn.inputs[1]].shape;
       ConvAttrs ca = conv_attrs(dn, false);
       int64_t ohw[2], fp[4];
       const bool ok = ca.mode == 0 && ca.dil == std::vector<int64_t>{1, 1} && ca.strides.size() == 2 &&
-                      ca.strides[0] == ca.strides[1] && wes[1] == (*xs)[1] &&
+                      ca.strides[0] == ca.strides[1] &&
+                      (expand ? nodes[en.inputs[1]].shape[1] == (*xs)[1] : wes[0] == (*xs)[1]) &&
                       output_size_and_padding((*xs)[2], (*xs)[3], 3, 3, ca.strides[0], ca.strides[1], 0,
                                               ca.pads.data(), 1, 1, ohw, fp) == RTENHIP_OK &&
                       (*ys)[0] == (*xs)[0] && (*ys)[1] == wps[0] && (*ys)[2] == ohw[0] && (*ys)[3] == ohw[1] &&
                       mbconv_block_eligible((int)(*xs)[1], (int)wes[0], (int)wps[0], (int)(*xs)[2], (int)(*xs)[3],
                                             (int)ohw[0], (int)ohw[1], (int)ca.strides[0], (int)fp[0], (int)fp[1],
-                                            (int)fp[2], (int)fp[3]);
+                                            (int)fp[2], (int)fp[3], expand);
       if (!ok) continue;
-      if (pn.fused_residual >= 0 && pn.fused_residual != en.inputs[0]) {
+      if (pn.fused_residual >= 0 && pn.fused_residual != xv) {
         const Shape* rs = shape_of(pn.fused_residual);
         if (!rs || *rs != *ys) continue;
       }
-      if (pn.fused_residual == en.inputs[0] && (ca.strides[0] != 1 || (*xs)[1] != wps[0] || *xs != *ys)) continue;
-      p.block_fused[op] = en.inputs[0];
+      if (pn.fused_residual == xv && (ca.strides[0] != 1 || (*xs)[1] != wps[0] || *xs != *ys)) continue;
+      p.block_fused[op] = xv;
       drop.push_back(pn.fb_op);
-      drop.push_back(dn.fe_op);
+      if (expand) drop.push_back(dn.fe_op);
     }
     for (int op : p.ops) {
       const Node& n = nodes[op];
@@ -1660,16 +1666,17 @@ rtenhip_status Graph::exec_expand_dw(Plan& p, int op_id) {
 rtenhip_status Graph::exec_mbconv_block(Plan& p, int op_id) {
   const Node& pn = nodes[op_id];
   const Node& dn = nodes[pn.fb_op];
-  const Node& en = nodes[dn.fe_op];
   const int xv = p.block_fused[op_id];
+  const bool expand = dn.inputs[0] != xv;  // else depthwise -> project (no expand conv)
+  const Node& en = nodes[expand ? dn.fe_op : pn.fb_op];
   const Shape* xsp = plan_shape(*this, p, xv);
   const Shape* ysp = plan_shape(*this, p, pn.outputs[0]);
   if (!xsp || !ysp) return fail(RTENHIP_HIP_ERROR, "inverted residual block: missing shapes");
   const Shape& xs = *xsp;
   const Shape& ys = *ysp;
-  const int cin = (int)xs[1], hid = (int)nodes[en.inputs[1]].shape[0], cout = (int)ys[1];
+  const int cin = (int)xs[1], hid = (int)nodes[dn.inputs[1]].shape[0], cout = (int)ys[1];
   auto bias_of = [&](const Node& n) -> int { return n.inputs.size() > 2 && n.inputs[2] >= 0 ? n.inputs[2] : -1; };
-  const int be = bias_of(en), bd = bias_of(dn), bp = bias_of(pn);
+  const int be = expand ? bias_of(en) : -1, bd = bias_of(dn), bp = bias_of(pn);
   auto pk = mb_pack.find(op_id);
   if (pk == mb_pack.end()) {
     // Plan-time work on the first (eager) run of this block.
@@ -1678,12 +1685,14 @@ rtenhip_status Graph::exec_mbconv_block(Plan& p, int op_id) {
       if (v >= 0 && n) (void)hipMemcpy(h.data(), nodes[v].dev, n * sizeof(float), hipMemcpyDeviceToHost);
       return h;
     };
-    const std::vector<float> we = host(en.inputs[1], (size_t)hid * cin), hbe = host(be, be >= 0 ? hid : 0),
+    const std::vector<float> we = host(expand ? en.inputs[1] : -1, expand ? (size_t)hid * cin : 0),
+                             hbe = host(be, be >= 0 ? hid : 0),
                              wd = host(dn.inputs[1], (size_t)hid * 9), hbd = host(bd, bd >= 0 ? hid : 0),
                              wp = host(pn.inputs[1], (size_t)cout * hid), hbp = host(bp, bp >= 0 ? cout : 0);
-    std::vector<float> packed((size_t)mbconv_block_pack_floats(cin, hid, cout));
+    const int cin_e = expand ? cin : 0;  // packed without expand operands
+    std::vector<float> packed((size_t)mbconv_block_pack_floats(cin_e, hid, cout));
     mbconv_block_pack(we.data(), be >= 0 ? hbe.data() : nullptr, wd.data(), bd >= 0 ? hbd.data() : nullptr, wp.data(),
-                      bp >= 0 ? hbp.data() : nullptr, cin, hid, cout, packed.data());
+                      bp >= 0 ? hbp.data() : nullptr, cin_e, hid, cout, packed.data());
     float* dev = nullptr;
     RTENHIP_HIP_CHECK(hipMalloc(&dev, packed.size() * sizeof(float)));
     RTENHIP_HIP_CHECK(hipMemcpy(dev, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice));
@@ -1699,7 +1708,7 @@ rtenhip_status Graph::exec_mbconv_block(Plan& p, int op_id) {
   return launch_mbconv_block(ptr_of(p, xv), pk->second, res, res_x, ptr_of(p, pn.outputs[0]), (int)xs[0], cin, hid,
                              cout, (int)xs[2], (int)xs[3], (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0],
                              (int)fp[1], en.fused_act, en.act_lo, en.act_hi, dn.fused_act, dn.act_lo, dn.act_hi,
-                             pn.fused_act, pn.act_lo, pn.act_hi, be >= 0, bd >= 0, bp >= 0, ctx->stream);
+                             pn.fused_act, pn.act_lo, pn.act_hi, be >= 0, bd >= 0, bp >= 0, expand, ctx->stream);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -3243,17 +3252,27 @@ rtenhip_status Graph::optimize() {
     if (pa.mode != 0 || pa.groups != 1 || pa.pads != std::vector<int64_t>{0, 0, 0, 0} ||
         pa.strides != std::vector<int64_t>{1, 1} || pa.dil != std::vector<int64_t>{1, 1})
       continue;
+    // The producer: a depthwise 3x3 Conv (constant [C, 1, 3, 3] weights,
+    // groups C), with its expand (fe_op) or without one (features.1).
     int d_op = -1;
     for (int j = 0; j < (int)nodes.size(); j++) {
       const Node& dn = nodes[j];
-      if (dn.kind == NodeKind::Operator && !dn.removed && dn.op_type == "Conv" && dn.fe_op >= 0 &&
-          dn.outputs.size() == 1 && dn.outputs[0] == pn.inputs[0]) {
+      if (dn.kind == NodeKind::Operator && !dn.removed && dn.op_type == "Conv" && dn.outputs.size() == 1 &&
+          dn.outputs[0] == pn.inputs[0]) {
         d_op = j;
         break;
       }
     }
-    if (d_op < 0 || sole(pn.inputs[0]) != i || nodes[d_op].fused_residual >= 0) continue;
-    if (nodes[wv].shape[1] != nodes[nodes[nodes[d_op].fe_op].inputs[1]].shape[0]) continue;  // K = hidden
+    if (d_op < 0 || sole(pn.inputs[0]) != i) continue;
+    const Node& dn = nodes[d_op];
+    if (dn.fused_residual >= 0 || dn.fused_bn >= 0 || dn.inputs.size() < 2 || !dn.input_perm.empty()) continue;
+    const int dwv = dn.inputs[1];
+    if (dwv < 0 || nodes[dwv].kind != NodeKind::Constant) continue;
+    const int64_t hidden = nodes[dwv].shape.empty() ? -1 : nodes[dwv].shape[0];
+    if (nodes[dwv].shape != Shape{hidden, 1, 3, 3} || (int64_t)dn.attrs.num("groups", 1) != hidden ||
+        (dn.inputs.size() > 2 && dn.inputs[2] >= 0 && nodes[dn.inputs[2]].kind != NodeKind::Constant))
+      continue;
+    if (nodes[wv].shape[1] != hidden) continue;  // project K = hidden
     pn.fb_op = d_op;
     fused++;
   }

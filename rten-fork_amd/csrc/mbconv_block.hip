@@ -76,12 +76,15 @@ __device__ __forceinline__ float mb_act(float v, int act, float lo, float hi) {
 }
 
 // NT threads; S stride; CIN input channels; MT = ceil(COUT / 16) project
-// row tiles; MAXT = output pixel tiles per wave (host-checked).
-template <int NT, int S, int CIN, int MT, int MAXT>
+// row tiles; MAXT = output pixel tiles per wave (host-checked).  EXP false:
+// a block without the expand conv (MobileNetV2's features.1, depthwise ->
+// project): the depthwise reads the staged band itself (hidden = CIN), no
+// per-chunk planes or barriers.
+template <int NT, int S, int CIN, int MT, int MAXT, bool EXP = true>
 __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
   constexpr int NW = NT / 64;
   constexpr int KS = CIN / 4;  // expand MFMA steps
-  constexpr int GE = (CIN + 15) / 16;
+  constexpr int GE = EXP ? (CIN + 15) / 16 : 0;
   extern __shared__ float4 mb_lds4[];
   float* X = reinterpret_cast<float*>(mb_lds4);  // [CIN][RX]
   float* E = X + CIN * d.RX;                      // [2][16][RE]
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
   }
 
   const int nchunks = d.hid >> 4;
-  const int cf = mb_chunk_floats(CIN, MT);
+  const int cf = mb_chunk_floats(EXP ? CIN : 0, MT);
   const float4* pk4 = reinterpret_cast<const float4*>(d.pk);
   // Project accumulators (current KC block) and the folded sum.
   mb_f32x4 acc[MAXT][MT], sum[MAXT][MT];
@@ -153,9 +156,11 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
 
   for (int ch = 0; ch < nchunks; ch++) {
     const float4* rec = pk4 + (int64_t)ch * (cf >> 2);
-    float* Eb = E + (ch & 1) * 16 * d.RE;
+    // The chunk's 16 depthwise input planes: expand planes, or the band.
+    float* Eb = EXP ? E + (ch & 1) * 16 * d.RE : X + ch * 16 * d.RX;
+    const int re = EXP ? d.RE : d.RX;
     // 1. Expand: tiles of 16 channels x 16 band pixels, wave-strided.
-    {
+    if constexpr (EXP) {
       float4 wa[GE];
 #pragma unroll
       for (int g = 0; g < GE; g++) wa[g] = rec[g * 64 + lane];
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
         }
       }
     }
-    __syncthreads();  // chunk ch's expand planes complete (and chunk ch - 1's reads of the other buffer done)
+    if constexpr (EXP) __syncthreads();  // chunk ch's expand planes complete (and chunk ch - 1's reads of the other buffer done)
     // 2. Depthwise (channels h + 4j of this lane's pixel) -> project MFMAs.
     {
       const float4* dwr = rec + GE * 64 + 4;
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
         float dv[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-          const float* ep = Eb + (h + 4 * j) * d.RE;
+          const float* ep = Eb + (h + 4 * j) * re;
           float a = d.has_bd ? (j == 0 ? bd.x : j == 1 ? bd.y : j == 2 ? bd.z : bd.w) : 0.f;
 #pragma unroll
           for (int ky = 0; ky < 3; ky++)
@@ -270,6 +275,7 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
 
 // Host side --------------------------------------------------------------
 
+// cin = 0: a block without the expand conv (we, be unused).
 int mbconv_block_pack_floats(int cin, int hid, int cout) {
   const int mt = (cout + 15) / 16;
   return (hid / 16) * mb_chunk_floats(cin, mt) + mt * 16;
@@ -322,13 +328,15 @@ namespace {
 // 512 threads where the accumulators of 4 tiles per wave would not fit.
 struct MbInst {
   int S, cin, mt, nt;
+  bool exp;
 };
-constexpr MbInst kMbInsts[] = {{2, 16, 2, 256}, {1, 24, 2, 256}, {2, 24, 2, 256}, {1, 32, 2, 256},
-                               {2, 32, 4, 512}, {1, 64, 4, 512}, {1, 64, 6, 512}, {1, 96, 6, 512}};
+constexpr MbInst kMbInsts[] = {{2, 16, 2, 256, true}, {1, 24, 2, 256, true}, {2, 24, 2, 256, true},
+                               {1, 32, 2, 256, true}, {2, 32, 4, 512, true}, {1, 64, 4, 512, true},
+                               {1, 64, 6, 512, true}, {1, 96, 6, 512, true}, {1, 32, 1, 256, false}};
 
-const MbInst* mb_inst(int S, int cin, int mt) {
+const MbInst* mb_inst(int S, int cin, int mt, bool exp) {
   for (const MbInst& m : kMbInsts)
-    if (m.S == S && m.cin == cin && m.mt == mt) return &m;
+    if (m.S == S && m.cin == cin && m.mt == mt && m.exp == exp) return &m;
   return nullptr;
 }
 
@@ -343,22 +351,26 @@ struct MbGeom {
 // strides: X rows are read 16 consecutive floats per half-wave (2 rows per
 // 32-lane group): stride = 16 (mod 32); E rows are read at pixel steps of S:
 // stride 16 (mod 32) for S = 1, odd for S = 2.
-bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, MbGeom& g) {
-  const MbInst* in = mb_inst(S, cin, (cout + 15) / 16);
+bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, MbGeom& g) {
+  const MbInst* in = mb_inst(S, cin, (cout + 15) / 16, exp);
   if (!in) return false;
   const size_t budget = 72 * 1024;
   const int nt = in->nt, nw = nt / 64, maxt = nt == 256 ? 4 : 2;
   for (int tr = OH; tr >= 1; tr--) {
     const int rows = std::min(H, (tr - 1) * S + 3);  // input rows of the widest band
     const int tin16 = (rows * W + 15) / 16 * 16;
+    // (without the expand, the depthwise reads the band: its stride follows E's rule)
     int rx = tin16;
-    while (rx % 32 != 16) rx++;
+    if (exp || S == 1)
+      while (rx % 32 != 16) rx++;
+    else if (rx % 2 == 0)
+      rx++;
     int re = tin16;
     if (S == 1)
       while (re % 32 != 16) re++;
     else if (re % 2 == 0)
       re++;
-    const size_t lds = ((size_t)cin * rx + 2 * 16 * (size_t)re) * sizeof(float);
+    const size_t lds = ((size_t)cin * rx + (exp ? 2 * 16 * (size_t)re : 0)) * sizeof(float);
     const int tout = (tr * OW + 15) / 16;
     if (lds > budget || (tout + nw - 1) / nw > maxt) continue;
     g.TR = tr;
@@ -377,22 +389,23 @@ bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, MbGeom& g) 
 // C_out) shape (kMbInsts), 3x3 depthwise with pads <= 1, hidden a multiple
 // of 16, and a band that fits LDS.  RTENHIP_MBCONV=0 disables the fusion.
 bool mbconv_block_eligible(int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl, int pb,
-                           int pr) {
+                           int pr, bool expand) {
   const char* e = getenv("RTENHIP_MBCONV");
   if (e && strcmp(e, "0") == 0) return false;
   if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
-  if (hid % 16 != 0 || hid <= 0 || cout <= 0) return false;
+  if (hid % 16 != 0 || hid <= 0 || cout <= 0 || (!expand && hid != cin)) return false;
   MbGeom g;
-  return mb_geom(cin, cout, H, W, OH, OW, S, g);
+  return mb_geom(cin, cout, H, W, OH, OW, S, expand, g);
 }
 
 rtenhip_status launch_mbconv_block(const float* x, const float* pk, const float* res, bool res_is_x, float* y, int N,
                                    int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl,
                                    int act_e, float lo_e, float hi_e, int act_d, float lo_d, float hi_d, int act_p,
-                                   float lo_p, float hi_p, bool has_be, bool has_bd, bool has_bp, hipStream_t s) {
+                                   float lo_p, float hi_p, bool has_be, bool has_bd, bool has_bp, bool expand,
+                                   hipStream_t s) {
   if ((int64_t)N * cout * OH * OW == 0) return RTENHIP_OK;
   MbGeom g;
-  if (hid % 16 != 0 || !mb_geom(cin, cout, H, W, OH, OW, S, g))
+  if (hid % 16 != 0 || (!expand && hid != cin) || !mb_geom(cin, cout, H, W, OH, OW, S, expand, g))
     return fail(RTENHIP_UNSUPPORTED_VALUE, "inverted residual block: unsupported shape");
   if (res_is_x && (S != 1 || cin != cout || OH != H || OW != W))
     return fail(RTENHIP_INVALID_VALUE, "inverted residual block: residual shape");
@@ -435,20 +448,22 @@ rtenhip_status launch_mbconv_block(const float* x, const float* pk, const float*
   const int bands = (OH + g.TR - 1) / g.TR;
   const dim3 grid((unsigned)bands, (unsigned)N);
   const int mt = (cout + 15) / 16;
-#define MB_LAUNCH(S_, CIN_, MT_, NT_)                                                                         \
-  if (S == S_ && cin == CIN_ && mt == MT_) {                                                                 \
-    hipLaunchKernelGGL((mbconv_block_kernel<NT_, S_, CIN_, MT_, NT_ == 256 ? 4 : 2>), grid, dim3(NT_), g.lds, s, d); \
+#define MB_LAUNCH(S_, CIN_, MT_, NT_, EXP_)                                                                   \
+  if (S == S_ && cin == CIN_ && mt == MT_ && expand == EXP_) {                                             \
+    hipLaunchKernelGGL((mbconv_block_kernel<NT_, S_, CIN_, MT_, NT_ == 256 ? 4 : 2, EXP_>), grid, dim3(NT_), g.lds, \
+                       s, d);                                                                                 \
     RTENHIP_LAUNCH_CHECK();                                                                                   \
     return RTENHIP_OK;                                                                                        \
   }
-  MB_LAUNCH(2, 16, 2, 256)
-  MB_LAUNCH(1, 24, 2, 256)
-  MB_LAUNCH(2, 24, 2, 256)
-  MB_LAUNCH(1, 32, 2, 256)
-  MB_LAUNCH(2, 32, 4, 512)
-  MB_LAUNCH(1, 64, 4, 512)
-  MB_LAUNCH(1, 64, 6, 512)
-  MB_LAUNCH(1, 96, 6, 512)
+  MB_LAUNCH(2, 16, 2, 256, true)
+  MB_LAUNCH(1, 24, 2, 256, true)
+  MB_LAUNCH(2, 24, 2, 256, true)
+  MB_LAUNCH(1, 32, 2, 256, true)
+  MB_LAUNCH(2, 32, 4, 512, true)
+  MB_LAUNCH(1, 64, 4, 512, true)
+  MB_LAUNCH(1, 64, 6, 512, true)
+  MB_LAUNCH(1, 96, 6, 512, true)
+  MB_LAUNCH(1, 32, 1, 256, false)
 #undef MB_LAUNCH
   return fail(RTENHIP_UNSUPPORTED_VALUE, "inverted residual block: unsupported shape");
 }

@@ -1,5 +1,5 @@
 """The fused inverted residual block (csrc/mbconv_block.hip): 1x1 expand
-(+ bias, Clip / Relu) -> 3x3 depthwise (+ bias, Clip / Relu) -> 1x1 project
+(+ bias, Clip / Relu; or none, MobileNetV2's features.1) -> 3x3 depthwise (+ bias, Clip / Relu) -> 1x1 project
 (+ bias) [+ Add], bit-identical to the three operators run apart by the
 oracle (conv_2d_pointwise, conv_2d_depthwise_block, conv_2d_pointwise:
 src/ops/conv.rs:24-68, src/ops/conv/depthwise.rs:49-120, the KC = 256 block
@@ -41,6 +41,10 @@ CASES = [
     (1, 64, 14, 14, 384, 96, 1, "clip", "relu", True, None),     # C_out 96
     (1, 96, 14, 14, 576, 96, 1, "clip", "clip", True, "x"),      # hidden 576: three KC blocks
     (1, 24, 10, 10, 144, 32, 2, "clip", "clip", True, "other"),  # residual from another tensor
+    # hidden 0: no expand conv (features.1: depthwise -> project)
+    (2, 32, 20, 20, 0, 16, 1, None, "clip", True, None),
+    (1, 32, 112, 112, 0, 16, 1, None, "clip", True, None),        # features.1 at full size
+    (2, 32, 9, 11, 0, 16, 1, None, "relu", False, None),
 ]
 
 
@@ -65,8 +69,12 @@ def _block_spec(case, rng):
     def bias(name, n):
         return [m.const(name, rng.uniform(-0.2, 0.2, (n,)).astype(np.float32))] if biases else []
 
-    we = m.const("we", rng.uniform(-0.4, 0.4, (M, C, 1, 1)).astype(np.float32))
-    e = act(m.op("Conv", [x, we] + bias("be", M), {"pads": [0, 0, 0, 0], "strides": [1, 1]}, name="expand"), act_e)
+    if M:
+        we = m.const("we", rng.uniform(-0.4, 0.4, (M, C, 1, 1)).astype(np.float32))
+        e = act(m.op("Conv", [x, we] + bias("be", M), {"pads": [0, 0, 0, 0], "strides": [1, 1]}, name="expand"),
+                act_e)
+    else:  # no expand: the depthwise conv reads the block input
+        M, e = C, x
     wd = m.const("wd", rng.uniform(-0.5, 0.5, (M, 1, 3, 3)).astype(np.float32))
     d = act(m.op("Conv", [e, wd] + bias("bd", M), {"pads": [1, 1, 1, 1], "strides": [s, s], "groups": M},
                  name="dw"), act_d)
