@@ -81,13 +81,17 @@ __device__ __forceinline__ float mb_act(float v, int act, float lo, float hi) {
 // project): the depthwise reads the staged band itself (hidden = CIN), no
 // per-chunk planes or barriers.
 template <int NT, int S, int CIN, int MT, int MAXT, bool EXP = true>
-__global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
+__global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
   constexpr int NW = NT / 64;
   constexpr int KS = CIN / 4;  // expand MFMA steps
   constexpr int GE = EXP ? (CIN + 15) / 16 : 0;
   extern __shared__ float4 mb_lds4[];
   float* X = reinterpret_cast<float*>(mb_lds4);  // [CIN][RX]
-  float* E = X + CIN * d.RX;                      // [2][16][RE]
+  float* E = X + CIN * d.RX;                      // [2][16][RE] (EXP)
+  // Weight records of three chunks (ch % 3): the record of chunk ch + 2 is
+  // loaded while chunk ch runs and stored after its barrier, so no chunk
+  // waits on a global load for its operands.
+  float4* Wr = reinterpret_cast<float4*>(EXP ? E + 2 * 16 * d.RE : E);
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int c = lane & 15, h = lane >> 4;
@@ -142,7 +146,10 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
 
   const int nchunks = d.hid >> 4;
   const int cf = mb_chunk_floats(EXP ? CIN : 0, MT);
+  const int cf4 = cf >> 2;  // float4s per record (<= 2 * NT, host-checked)
   const float4* pk4 = reinterpret_cast<const float4*>(d.pk);
+  // Records 0 and 1 staged with the band.
+  for (int i = t; i < min(2, nchunks) * cf4; i += NT) Wr[i] = pk4[i];
   // Project accumulators (current KC block) and the folded sum.
   mb_f32x4 acc[MAXT][MT], sum[MAXT][MT];
 #pragma unroll
@@ -155,7 +162,15 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
   __syncthreads();  // X staged
 
   for (int ch = 0; ch < nchunks; ch++) {
-    const float4* rec = pk4 + (int64_t)ch * (cf >> 2);
+    const float4* rec = Wr + (ch % 3) * cf4;
+    // Prefetch chunk ch + 2's record (stored after this chunk's barrier).
+    float4 nxt[2];
+    const bool pf = ch + 2 < nchunks;
+    {
+      const float4* src = pk4 + (int64_t)(ch + 2) * cf4;
+#pragma unroll
+      for (int u = 0; u < 2; u++) nxt[u] = pf ? src[min(t + u * NT, cf4 - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     // The chunk's 16 depthwise input planes: expand planes, or the band.
     float* Eb = EXP ? E + (ch & 1) * 16 * d.RE : X + ch * 16 * d.RX;
     const int re = EXP ? d.RE : d.RX;
@@ -183,7 +198,15 @@ __global__ __launch_bounds__(NT) void mbconv_block_kernel(MbBlockDesc d) {
         }
       }
     }
-    if constexpr (EXP) __syncthreads();  // chunk ch's expand planes complete (and chunk ch - 1's reads of the other buffer done)
+    // Chunk ch's expand planes complete; every wave is past chunk ch - 1
+    // (so its plane buffer and its record slot, (ch + 2) % 3, are free).
+    __syncthreads();
+    if (pf) {
+      float4* dst = Wr + ((ch + 2) % 3) * cf4;
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+        if (t + u * NT < cf4) dst[t + u * NT] = nxt[u];
+    }
     // 2. Depthwise (channels h + 4j of this lane's pixel) -> project MFMAs.
     {
       const float4* dwr = rec + GE * 64 + 4;
@@ -345,8 +368,8 @@ struct MbGeom {
   size_t lds;
 };
 
-// Band height and LDS layout: the most output rows whose staged input band
-// and two expand plane sets fit 72 KB (two workgroups per CU), with at most
+// Band height and LDS layout: the most output rows whose staged input band,
+// two expand plane sets and three weight records fit the budget, with at most
 // 4 (256 threads) / 2 (512 threads) output pixel tiles per wave.  Row
 // strides: X rows are read 16 consecutive floats per half-wave (2 rows per
 // 32-lane group): stride = 16 (mod 32); E rows are read at pixel steps of S:
@@ -354,8 +377,11 @@ struct MbGeom {
 bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, MbGeom& g) {
   const MbInst* in = mb_inst(S, cin, (cout + 15) / 16, exp);
   if (!in) return false;
-  const size_t budget = 72 * 1024;
+  // 256 threads: two workgroups per CU; 512 (about 200 VGPRs): one.
   const int nt = in->nt, nw = nt / 64, maxt = nt == 256 ? 4 : 2;
+  const size_t budget = nt == 256 ? 80 * 1024 : 156 * 1024;
+  const int cf = mb_chunk_floats(exp ? cin : 0, in->mt);
+  if (cf / 4 > 2 * nt) return false;  // a record is prefetched as two float4s per thread
   for (int tr = OH; tr >= 1; tr--) {
     const int rows = std::min(H, (tr - 1) * S + 3);  // input rows of the widest band
     const int tin16 = (rows * W + 15) / 16 * 16;
@@ -370,7 +396,7 @@ bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, M
       while (re % 32 != 16) re++;
     else if (re % 2 == 0)
       re++;
-    const size_t lds = ((size_t)cin * rx + (exp ? 2 * 16 * (size_t)re : 0)) * sizeof(float);
+    const size_t lds = ((size_t)cin * rx + (exp ? 2 * 16 * (size_t)re : 0) + 3 * (size_t)cf) * sizeof(float);
     const int tout = (tr * OW + 15) / 16;
     if (lds > budget || (tout + nw - 1) / nw > maxt) continue;
     g.TR = tr;

@@ -156,3 +156,24 @@ def test_resnet50_batch1_all_latency_convs(rh, monkeypatch):
     assert g.timing_report().count("cfg=lat41") >= 50
 
 
+
+
+@pytest.mark.parametrize("mode", ["71", "72", "74", "91", "92", "22", "12", "11", "21", "42"])
+def test_resnet50_batch1_forced_variant(rh, monkeypatch, mode):
+    """ResNet-50 at batch 1 with one latency-GEMM variant forced on every conv
+    it takes (the tuner may pick any of them per layer): oracle bits."""
+    import torch
+    import graph_runner
+    from rten_hip import models
+
+    monkeypatch.setenv("RTENHIP_LAT", mode)
+    spec = models.resnet50()
+    x = np.random.default_rng(12).random((1, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {spec.inputs[0]: x})[spec.outputs[0]]
+    g = spec.to_graph()
+    xd = torch.from_numpy(x).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)

@@ -101,4 +101,5 @@ def test_world2_device_graph_matches_oracle(model, total):
     for rank, dev, got in results:
         assert dev == "cuda", f"rank {rank}: gathered logits left the device"
         assert got.shape == expect.shape
-        assert (got.view(np.uint32) == expect.view(np.uint32)).all(), f"rank {rank}: gathered logits differ"
+        bad = sorted({int(i) for i in np.nonzero(got.view(np.uint32) != expect.view(np.uint32))[0]})
+        assert not bad, f"rank {rank}: gathered logits differ in images {bad} of {total}"
