@@ -5,7 +5,8 @@ separate dispatch the counters can attribute).  A torch fill kernel marks the
 end of the tuning run: tools/pmc_traffic.py --marker counts only the
 librten_hip dispatches after it.
 
-usage: model_once.py [runs] [model] [batch]   (defaults: 2 resnet50 64)"""
+usage: model_once.py [runs] [model] [batch] [--report]   (defaults: 2 resnet50 64;
+--report: one more eager run with per-op hipEvent timing, report printed)"""
 import os
 import sys
 
@@ -17,6 +18,8 @@ import torch
 import rten_hip
 from rten_hip import models
 
+report = "--report" in sys.argv
+sys.argv = [a for a in sys.argv if a != "--report"]
 runs = int(sys.argv[1]) if len(sys.argv) > 1 else 2
 model = sys.argv[2] if len(sys.argv) > 2 else "resnet50"
 batch = int(sys.argv[3]) if len(sys.argv) > 3 else 64
@@ -40,3 +43,8 @@ for _ in range(runs):
     g.run(dev, g.output_ids, out=[out])
 torch.cuda.synchronize()
 print("done", runs, flush=True)
+if report:
+    g.set_timing(True)
+    g.run(dev, g.output_ids, out=[out])
+    torch.cuda.synchronize()
+    print(g.timing_report(), flush=True)
