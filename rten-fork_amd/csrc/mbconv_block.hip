@@ -374,7 +374,9 @@ struct MbGeom {
 // strides: X rows are read 16 consecutive floats per half-wave (2 rows per
 // 32-lane group): stride = 16 (mod 32); E rows are read at pixel steps of S:
 // stride 16 (mod 32) for S = 1, odd for S = 2.
-bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, MbGeom& g) {
+// N > 0: then the band is also cut until the grid fills every CU once (two
+// 256-thread or one 512-thread workgroup per CU), down to 2 output rows.
+bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, MbGeom& g, int N = 0) {
   const MbInst* in = mb_inst(S, cin, (cout + 15) / 16, exp);
   if (!in) return false;
   // 256 threads: two workgroups per CU; 512 (about 200 VGPRs): one.
@@ -399,6 +401,8 @@ bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, M
     const size_t lds = ((size_t)cin * rx + (exp ? 2 * 16 * (size_t)re : 0) + 3 * (size_t)cf) * sizeof(float);
     const int tout = (tr * OW + 15) / 16;
     if (lds > budget || (tout + nw - 1) / nw > maxt) continue;
+    const int64_t wgs = (int64_t)N * ((OH + tr - 1) / tr);
+    if (N > 0 && tr > 2 && wgs < (nt == 256 ? 512 : 256)) continue;
     g.TR = tr;
     g.RX = rx;
     g.RE = re;
@@ -431,7 +435,7 @@ rtenhip_status launch_mbconv_block(const float* x, const float* pk, const float*
                                    hipStream_t s) {
   if ((int64_t)N * cout * OH * OW == 0) return RTENHIP_OK;
   MbGeom g;
-  if (hid % 16 != 0 || (!expand && hid != cin) || !mb_geom(cin, cout, H, W, OH, OW, S, expand, g))
+  if (hid % 16 != 0 || (!expand && hid != cin) || !mb_geom(cin, cout, H, W, OH, OW, S, expand, g, N))
     return fail(RTENHIP_UNSUPPORTED_VALUE, "inverted residual block: unsupported shape");
   if (res_is_x && (S != 1 || cin != cout || OH != H || OW != W))
     return fail(RTENHIP_INVALID_VALUE, "inverted residual block: residual shape");
