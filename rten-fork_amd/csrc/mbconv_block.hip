@@ -43,6 +43,13 @@
 #include "stage.h"
 #include "vecmath.h"
 
+// Timing experiments only (never set in a product build): 1 = no depthwise /
+// project phase, 2 = no expand MFMAs, 3 = no weight prefetch loads, 4 = no
+// project MFMAs.
+#ifndef RTENHIP_MB_EXPERIMENT
+#define RTENHIP_MB_EXPERIMENT 0
+#endif
+
 namespace rtenhip {
 
 typedef float mb_f32x4 __attribute__((ext_vector_type(4)));
@@ -165,7 +172,7 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
     const float4* rec = Wr + (ch % 3) * cf4;
     // Prefetch chunk ch + 2's record (stored after this chunk's barrier).
     float4 nxt[2];
-    const bool pf = ch + 2 < nchunks;
+    const bool pf = ch + 2 < nchunks && RTENHIP_MB_EXPERIMENT != 3;
     {
       const float4* src = pk4 + (int64_t)(ch + 2) * cf4;
 #pragma unroll
@@ -184,7 +191,7 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
         mb_f32x4 e = {0.f, 0.f, 0.f, 0.f};
         const float* xc = X + h * d.RX + tile * 16 + c;
 #pragma unroll
-        for (int s = 0; s < KS; s++) {
+        for (int s = 0; s < (RTENHIP_MB_EXPERIMENT == 2 ? 0 : KS); s++) {
           const float a = s % 4 == 0 ? wa[s / 4].x : s % 4 == 1 ? wa[s / 4].y : s % 4 == 2 ? wa[s / 4].z : wa[s / 4].w;
           e = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xc[4 * s * d.RX], e, 0, 0, 0);
         }
@@ -220,7 +227,7 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
       const int ky_off[3] = {0, W, 2 * W};
 #pragma unroll
       for (int u = 0; u < MAXT; u++) {
-        if (wave + u * NW >= tout) break;
+        if (wave + u * NW >= tout || RTENHIP_MB_EXPERIMENT == 1) break;
         float dv[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -238,6 +245,11 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
               a = on ? s : a;
             }
           dv[j] = mb_act(a, d.act_d, d.lo_d, d.hi_d);
+        }
+        if constexpr (RTENHIP_MB_EXPERIMENT == 4) {
+#pragma unroll
+          for (int m = 0; m < MT; m++) acc[u][m][0] += dv[0] + dv[1] + dv[2] + dv[3];
+          continue;
         }
 #pragma unroll
         for (int m = 0; m < MT; m++) {
