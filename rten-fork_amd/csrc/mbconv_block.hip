@@ -228,23 +228,28 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
 #pragma unroll
       for (int u = 0; u < MAXT; u++) {
         if (wave + u * NW >= tout || RTENHIP_MB_EXPERIMENT == 1) break;
+        // Two channels per packed f32 operation (v_pk_mul / v_pk_add: one
+        // IEEE rounding per component, the same ops as apart).
         float dv[4];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const float* ep = Eb + (h + 4 * j) * re;
-          float a = d.has_bd ? (j == 0 ? bd.x : j == 1 ? bd.y : j == 2 ? bd.z : bd.w) : 0.f;
+        for (int jp = 0; jp < 2; jp++) {
+          const float* ep0 = Eb + (h + 8 * jp) * re;
+          const float* ep1 = ep0 + 4 * re;
+          vm_f32x2 a = d.has_bd ? (jp == 0 ? (vm_f32x2){bd.x, bd.y} : (vm_f32x2){bd.z, bd.w}) : (vm_f32x2){0.f, 0.f};
 #pragma unroll
           for (int ky = 0; ky < 3; ky++)
 #pragma unroll
             for (int kx = 0; kx < 3; kx++) {
               const int k = ky * 3 + kx;
               const bool on = (tmask[u] >> k) & 1u;
-              const float ev = ep[on ? tbase[u] + ky_off[ky] + kx : 0];
-              const float w = j == 0 ? wd[k].x : j == 1 ? wd[k].y : j == 2 ? wd[k].z : wd[k].w;
-              const float s = __fadd_rn(a, __fmul_rn(ev, w));
-              a = on ? s : a;
+              const int idx = on ? tbase[u] + ky_off[ky] + kx : 0;
+              const vm_f32x2 ev = {ep0[idx], ep1[idx]};
+              const vm_f32x2 w = jp == 0 ? (vm_f32x2){wd[k].x, wd[k].y} : (vm_f32x2){wd[k].z, wd[k].w};
+              const vm_f32x2 sp = a + ev * w;
+              a = on ? sp : a;
             }
-          dv[j] = mb_act(a, d.act_d, d.lo_d, d.hi_d);
+          dv[2 * jp] = mb_act(a[0], d.act_d, d.lo_d, d.hi_d);
+          dv[2 * jp + 1] = mb_act(a[1], d.act_d, d.lo_d, d.hi_d);
         }
         if constexpr (RTENHIP_MB_EXPERIMENT == 4) {
 #pragma unroll
