@@ -168,15 +168,27 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
 
   __syncthreads();  // X staged
 
+  // Record prefetch: chunk ch loads record ch + 2 into registers and stores
+  // the one it loaded a chunk earlier (record ch + 1) into its slot during
+  // its expand phase, so a load has a whole chunk of work to land.  Slot
+  // (ch + 1) % 3 last held record ch - 2, read before barrier ch - 1; the
+  // stores are visible to expand ch + 1 after barrier ch.
+  float4 held[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+  bool held_ok = false;  // record 1 was staged with the band
   for (int ch = 0; ch < nchunks; ch++) {
     const float4* rec = Wr + (ch % 3) * cf4;
-    // Prefetch chunk ch + 2's record (stored after this chunk's barrier).
     float4 nxt[2];
     const bool pf = ch + 2 < nchunks && RTENHIP_MB_EXPERIMENT != 3;
     {
       const float4* src = pk4 + (int64_t)(ch + 2) * cf4;
 #pragma unroll
       for (int u = 0; u < 2; u++) nxt[u] = pf ? src[min(t + u * NT, cf4 - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (held_ok) {
+      float4* dst = Wr + ((ch + 1) % 3) * cf4;
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+        if (t + u * NT < cf4) dst[t + u * NT] = held[u];
     }
     // The chunk's 16 depthwise input planes: expand planes, or the band.
     float* Eb = EXP ? E + (ch & 1) * 16 * d.RE : X + ch * 16 * d.RX;
@@ -205,15 +217,12 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
         }
       }
     }
-    // Chunk ch's expand planes complete; every wave is past chunk ch - 1
-    // (so its plane buffer and its record slot, (ch + 2) % 3, are free).
+    // Chunk ch's expand planes (and record ch + 1) complete; every wave is
+    // past chunk ch - 1, so its plane buffer is free.
     __syncthreads();
-    if (pf) {
-      float4* dst = Wr + ((ch + 2) % 3) * cf4;
-#pragma unroll
-      for (int u = 0; u < 2; u++)
-        if (t + u * NT < cf4) dst[t + u * NT] = nxt[u];
-    }
+    held[0] = nxt[0];
+    held[1] = nxt[1];
+    held_ok = pf;
     // 2. Depthwise (channels h + 4j of this lane's pixel) -> project MFMAs.
     {
       const float4* dwr = rec + GE * 64 + 4;
