@@ -115,8 +115,8 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
     kd[1] = kk[u].y;
     kd[2] = kk[u].z;
     kd[3] = kk[u].w;
-    *(float4*)(Vs + j * VS + c) = vv[u];
   }
+  // (V stays in registers, still in flight, until the scores are done.)
   if (mask_lds && tid < S) Ms[tid] = mv;
   const int i0 = wave * 32;
   const int i = i0 + l32;  // this lane's query row
@@ -133,21 +133,33 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
     for (int s = 0; s < AT_D / 2; s++)
       qf[s] = RTENHIP_ATT_EXPERIMENT == 4 ? 1.f : row_ok ? qr[2 * s] : 0.f;
   }
-  __syncthreads();
-  if (i0 >= S) return;  // no barrier follows
+  __syncthreads();  // K and the mask row staged
+  const bool live = i0 < S;  // a wave past S only helps stage V
 
 
   // acc[t][e]: score of (row i, key 32t + (e & 3) + 8(e >> 2) + 4h).
   f32x16 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; t++) acc[t] = (f32x16){0};
+  if (live) {
 #pragma unroll
-  for (int s = 0; s < (RTENHIP_ATT_EXPERIMENT == 2 || RTENHIP_ATT_EXPERIMENT == 5 ? 0 : AT_D / 2); s++) {
-    const float* kr = Ks + l32 * KS + 2 * s + h;
+    for (int s = 0; s < (RTENHIP_ATT_EXPERIMENT == 2 || RTENHIP_ATT_EXPERIMENT == 5 ? 0 : AT_D / 2); s++) {
+      const float* kr = Ks + l32 * KS + 2 * s + h;
 #pragma unroll
-    for (int t = 0; t < 4; t++)
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[t * 32 * KS], qf[s], acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; t++)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[t * 32 * KS], qf[s], acc[t], 0, 0, 0);
+    }
   }
+  // V to LDS now (its loads had the score MFMAs to land); read after the
+  // softmax, past the second barrier.
+#pragma unroll
+  for (int u = 0; u < ST; u++) {
+    const int t = tid + u * AT_THREADS;
+    const int j = t >> 4, c = (t & 15) * 4;
+    *(float4*)(Vs + j * VS + c) = vv[u];
+  }
+  __syncthreads();  // V staged
+  if (!live) return;  // no barrier follows
 
   // Scale and mask (separately rounded, as the Div|Mul and Add operators),
   // then the row max over the keys < S.
@@ -158,18 +170,29 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
       for (int e = 0; e < 16; e++) acc[t][e] = __fdiv_rn(acc[t][e], d.scale);
   } else if (d.scale_op == 2) {
+    const vm_f32x2 sc = {d.scale, d.scale};
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
-      for (int e = 0; e < 16; e++) acc[t][e] = __fmul_rn(acc[t][e], d.scale);
+      for (int e = 0; e < 16; e += 2) {
+        const vm_f32x2 x = (vm_f32x2){acc[t][e], acc[t][e + 1]} * sc;
+        acc[t][e] = x[0];
+        acc[t][e + 1] = x[1];
+      }
   }
   if (mask_lds) {
+    // Keys j, j + 1 (e even) as one packed add; S even keeps pairs whole.
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
-      for (int e = 0; e < 16; e++) {
+      for (int e = 0; e < 16; e += 2) {
         const int j = 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (FULL || j < S) acc[t][e] = __fadd_rn(acc[t][e], Ms[j]);
+        if (FULL || j < S) {
+          const float2 mk = *(const float2*)(Ms + j);
+          const vm_f32x2 x = (vm_f32x2){acc[t][e], acc[t][e + 1]} + (vm_f32x2){mk.x, mk.y};
+          acc[t][e] = x[0];
+          acc[t][e + 1] = x[1];
+        }
       }
   } else if (d.mask) {
     // A per-row mask: the row's 64 values loaded together (clamped to the
@@ -203,23 +226,25 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 
   // e = exp(x - max) and the eight partial sums: chain 4h + c runs over
   // j = 32t + 8g + 4h + c in increasing j (t, then g).
-  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  // Chains c and c + 1 advance together as packed adds (keys j, j + 1; S
+  // even keeps pairs whole).
+  vm_f32x2 part2[2] = {{0.f, 0.f}, {0.f, 0.f}};
+  const vm_f32x2 m2 = {m, m};
 #pragma unroll
   for (int t = 0; t < 4; t++)
 #pragma unroll
     for (int g = 0; g < 4; g++)
 #pragma unroll
       for (int c = 0; c < 4; c += 2) {
-        // (two keys per packed vm_exp2; a key past S is computed and dropped)
-        vm_f32x2 x = {__fsub_rn(acc[t][4 * g + c], m), __fsub_rn(acc[t][4 * g + c + 1], m)};
-        const vm_f32x2 ex = RTENHIP_ATT_EXPERIMENT == 1 ? x : vm_exp2(x);
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-          if (FULL || 32 * t + 8 * g + 4 * h + c + u < S) {
-            acc[t][4 * g + c + u] = ex[u];
-            part[c + u] = __fadd_rn(part[c + u], ex[u]);
-          }
+        if (FULL || 32 * t + 8 * g + 4 * h + c < S) {
+          const vm_f32x2 x = (vm_f32x2){acc[t][4 * g + c], acc[t][4 * g + c + 1]} - m2;
+          const vm_f32x2 ex = RTENHIP_ATT_EXPERIMENT == 1 ? x : vm_exp2(x);
+          acc[t][4 * g + c] = ex[0];
+          acc[t][4 * g + c + 1] = ex[1];
+          part2[c / 2] = part2[c / 2] + ex;
+        }
       }
+  const float part[4] = {part2[0][0], part2[0][1], part2[1][0], part2[1][1]};
   // 0 + p0 + ... + p7 (half 0 holds p0..p3, half 1 p4..p7): both halves fold
   // the same eight values in the same order.
   float other[4];
@@ -244,8 +269,12 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 #pragma unroll
     for (int t = 0; t < 4; t++)
 #pragma unroll
-      for (int e = 0; e < 16; e++)
-        if (FULL || 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) acc[t][e] = div_by_fast(dv, acc[t][e]);
+      for (int e = 0; e < 16; e += 2)
+        if (FULL || 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h < S) {
+          const vm_f32x2 p2 = div_by_fast2(dv, (vm_f32x2){acc[t][e], acc[t][e + 1]});
+          acc[t][e] = p2[0];
+          acc[t][e + 1] = p2[1];
+        }
   } else {
 #pragma unroll
     for (int t = 0; t < 4; t++)
