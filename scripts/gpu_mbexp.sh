@@ -10,6 +10,7 @@ for blk in ${BLOCKS:-3 8}; do
     lib=""; env=""
     [ $v != product ] && [ $v != apart ] && lib=rten-fork_amd/exp_mb/librten_hip_mb$v.so
     [ $v = apart ] && env="RTENHIP_MBCONV=0"
+    [ $v != apart ] && env="RTENHIP_MBCONV=all"
     env RTENHIP_LIB=$lib $env timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O/$v -o run --output-format csv \
       -- python3 rten-fork_amd/tools/mb_bench.py $blk > $O/${blk}_$v.log 2>&1 || { echo "mb $blk $v failed"; tail $O/${blk}_$v.log; exit 1; }
     f=$(find $O/$v -name 'run_kernel_stats.csv' | head -n 1)
