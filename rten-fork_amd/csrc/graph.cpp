@@ -836,6 +836,17 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
         if (!rs || *rs != *ys) continue;
       }
       if (pn.fused_residual == xv && (ca.strides[0] != 1 || (*xs)[1] != wps[0] || *xs != *ys)) continue;
+      {
+        // The kernel's skipped taps add w * copysign(0, -w) = -0: finite
+        // depthwise weights only (mbconv_block.hip MB_ZS).
+        std::vector<float> wdh((size_t)wes[0] * 9);
+        if (hipMemcpy(wdh.data(), nodes[dn.inputs[1]].dev, wdh.size() * sizeof(float), hipMemcpyDeviceToHost) !=
+            hipSuccess)
+          continue;
+        bool finite = true;
+        for (float w : wdh) finite = finite && std::isfinite(w);
+        if (!finite) continue;
+      }
       p.block_fused[op] = xv;
       drop.push_back(pn.fb_op);
       if (expand) drop.push_back(dn.fe_op);

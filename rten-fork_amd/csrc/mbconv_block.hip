@@ -74,6 +74,12 @@ struct MbBlockDesc {
 // depthwise bias [4 h][4], project A operand [MT][64][4]; then the project
 // bias [MT][4 h][4].
 __host__ __device__ inline int mb_ge(int cin) { return (cin + 15) / 16; }
+// Every LDS plane row (X and E) starts with MB_ZS floats: slots 0..8 hold
+// copysign(0, -w) of the row channel's 9 depthwise taps, so a tap the
+// reference skips reads its slot and adds w * slot = -0 (x + (-0) == x for
+// every x): no select per tap.  Needs finite depthwise weights (checked when
+// the plan fuses the block).  Pixel p of a row is at MB_ZS + p.
+constexpr int MB_ZS = 16;
 __host__ __device__ inline int mb_chunk_floats(int cin, int mt) { return mb_ge(cin) * 256 + 16 + 144 + 16 + mt * 256; }
 
 __device__ __forceinline__ float mb_act(float v, int act, float lo, float hi) {
@@ -120,35 +126,34 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
       const int q = pin >> 2;
       stage_batched<8, float4>(
           total >> 2, [&](int e) { const int ci = e / q; return *reinterpret_cast<const float4*>(xb + ci * HW + 4 * (e - ci * q)); },
-          [&](int e, const float4& v) { const int ci = e / q; *reinterpret_cast<float4*>(X + ci * d.RX + 4 * (e - ci * q)) = v; });
+          [&](int e, const float4& v) { const int ci = e / q; *reinterpret_cast<float4*>(X + ci * d.RX + MB_ZS + 4 * (e - ci * q)) = v; });
     } else {
       stage_batched<8, float>(
           total, [&](int e) { const int ci = e / pin; return xb[ci * HW + (e - ci * pin)]; },
-          [&](int e, float v) { const int ci = e / pin; X[ci * d.RX + (e - ci * pin)] = v; });
+          [&](int e, float v) { const int ci = e / pin; X[ci * d.RX + MB_ZS + (e - ci * pin)] = v; });
     }
   }
 
   // This lane's output pixels (column c of each owned tile): the depthwise
   // tap base (E offset of tap (0, 0)) and the 9-bit tap mask.
-  int tbase[MAXT];
-  uint32_t tmask[MAXT];
+  int tidx[MAXT][9];  // plane-row offset read for tap k: the pixel, or slot k when skipped
 #pragma unroll
   for (int u = 0; u < MAXT; u++) {
     const int tile = wave + u * NW;
     const int o = tile * 16 + c;
     const int ol = min(o, pout - 1) / OW, ox = min(o, pout - 1) - (min(o, pout - 1) / OW) * OW;
     const int oy = oy0 + ol;
-    uint32_t m = 0;
+    const int base = MB_ZS + (oy * S - d.pt - ia) * W + ox * S - d.pl;
 #pragma unroll
     for (int ky = 0; ky < 3; ky++) {
       const int r = oy * S + ky - d.pt;
       const bool row_ok = r >= 0 && r < d.H;
 #pragma unroll
-      for (int kx = 0; kx < 3; kx++)
-        m |= (tile < tout && o < pout && row_ok && ox >= d.omin[kx] && ox < d.omax[kx]) ? 1u << (ky * 3 + kx) : 0u;
+      for (int kx = 0; kx < 3; kx++) {
+        const bool on = tile < tout && o < pout && row_ok && ox >= d.omin[kx] && ox < d.omax[kx];
+        tidx[u][ky * 3 + kx] = on ? base + ky * W + kx : ky * 3 + kx;
+      }
     }
-    tmask[u] = m;
-    tbase[u] = (oy * S - d.pt - ia) * W + ox * S - d.pl;  // may be negative: only masked taps go out of range
   }
 
   const int nchunks = d.hid >> 4;
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
       const float4 be = rec[GE * 64 + h];
       for (int tile = wave; tile < tin; tile += NW) {
         mb_f32x4 e = {0.f, 0.f, 0.f, 0.f};
-        const float* xc = X + h * d.RX + tile * 16 + c;
+        const float* xc = X + h * d.RX + MB_ZS + tile * 16 + c;
 #pragma unroll
         for (int s = 0; s < (RTENHIP_MB_EXPERIMENT == 2 ? 0 : KS); s++) {
           const float a = s % 4 == 0 ? wa[s / 4].x : s % 4 == 1 ? wa[s / 4].y : s % 4 == 2 ? wa[s / 4].z : wa[s / 4].w;
@@ -213,12 +218,18 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
           if (d.has_be) v[r] = __fadd_rn(v[r], bb[r]);
-          Eb[(4 * h + r) * d.RE + tile * 16 + c] = mb_act(v[r], d.act_e, d.lo_e, d.hi_e);
+          Eb[(4 * h + r) * d.RE + MB_ZS + tile * 16 + c] = mb_act(v[r], d.act_e, d.lo_e, d.hi_e);
         }
       }
     }
-    // Chunk ch's expand planes (and record ch + 1) complete; every wave is
-    // past chunk ch - 1, so its plane buffer is free.
+    // The chunk's 16 x 9 skip slots, copysign(0, -w) (see MB_ZS).
+    if (t < 144) {
+      const int cl = t / 9, k = t - cl * 9;  // channel cl = hh + 4 j of the chunk
+      const float w = reinterpret_cast<const float*>(rec + GE * 64 + 4)[((cl & 3) * 9 + k) * 4 + (cl >> 2)];
+      Eb[cl * re + k] = copysignf(0.f, -w);
+    }
+    // Chunk ch's expand planes, slots (and record ch + 1) complete; every
+    // wave is past chunk ch - 1, so its plane buffer is free.
     __syncthreads();
     held[0] = nxt[0];
     held[1] = nxt[1];
@@ -233,7 +244,6 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
       float4 wp[MT];
 #pragma unroll
       for (int m = 0; m < MT; m++) wp[m] = dwr[40 + m * 64 + lane];
-      const int ky_off[3] = {0, W, 2 * W};
 #pragma unroll
       for (int u = 0; u < MAXT; u++) {
         if (wave + u * NW >= tout || RTENHIP_MB_EXPERIMENT == 1) break;
@@ -246,17 +256,12 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
           const float* ep1 = ep0 + 4 * re;
           vm_f32x2 a = d.has_bd ? (jp == 0 ? (vm_f32x2){bd.x, bd.y} : (vm_f32x2){bd.z, bd.w}) : (vm_f32x2){0.f, 0.f};
 #pragma unroll
-          for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-            for (int kx = 0; kx < 3; kx++) {
-              const int k = ky * 3 + kx;
-              const bool on = (tmask[u] >> k) & 1u;
-              const int idx = on ? tbase[u] + ky_off[ky] + kx : 0;
-              const vm_f32x2 ev = {ep0[idx], ep1[idx]};
-              const vm_f32x2 w = jp == 0 ? (vm_f32x2){wd[k].x, wd[k].y} : (vm_f32x2){wd[k].z, wd[k].w};
-              const vm_f32x2 sp = a + ev * w;
-              a = on ? sp : a;
-            }
+          for (int k = 0; k < 9; k++) {
+            const int idx = tidx[u][k];
+            const vm_f32x2 ev = {ep0[idx], ep1[idx]};
+            const vm_f32x2 w = jp == 0 ? (vm_f32x2){wd[k].x, wd[k].y} : (vm_f32x2){wd[k].z, wd[k].w};
+            a = a + ev * w;  // a skipped tap adds -0
+          }
           dv[2 * jp] = mb_act(a[0], d.act_d, d.lo_d, d.hi_d);
           dv[2 * jp + 1] = mb_act(a[1], d.act_d, d.lo_d, d.hi_d);
         }
@@ -314,7 +319,7 @@ __global__ __launch_bounds__(NT, 2) void mbconv_block_kernel(MbBlockDesc d) {
         if (co >= d.cout || !ok) continue;
         float v = sum[u][m][r];
         if (d.res_lds)
-          v = __fadd_rn(v, X[co * d.RX + (oy - ia) * W + ox]);
+          v = __fadd_rn(v, X[co * d.RX + MB_ZS + (oy - ia) * W + ox]);
         else if (d.res)
           v = __fadd_rn(v, d.res[((int64_t)n * d.cout + co) * d.OH * OW + opix]);
         d.y[((int64_t)n * d.cout + co) * d.OH * OW + opix] = mb_act(v, d.act_p, d.lo_p, d.hi_p);
@@ -412,7 +417,7 @@ bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, M
   if (cf / 4 > 2 * nt) return false;  // a record is prefetched as two float4s per thread
   for (int tr = OH; tr >= 1; tr--) {
     const int rows = std::min(H, (tr - 1) * S + 3);  // input rows of the widest band
-    const int tin16 = (rows * W + 15) / 16 * 16;
+    const int tin16 = MB_ZS + (rows * W + 15) / 16 * 16;  // slots + pixels
     // (without the expand, the depthwise reads the band: its stride follows E's rule)
     int rx = tin16;
     if (exp || S == 1)

@@ -149,3 +149,21 @@ def test_mbconv_block_off_switch(rh, monkeypatch):
     torch.cuda.synchronize()
     assert _bits_equal(out[0].cpu().numpy(), exp)
     assert "Conv(mbconv_block)" not in g.timing_report()
+
+
+def test_mbconv_block_nonfinite_depthwise_weight_unfused(rh, monkeypatch):
+    """A non-finite depthwise weight keeps the block apart (the fused kernel's
+    skipped taps rely on w * copysign(0, -w) == -0)."""
+    import torch
+
+    monkeypatch.setenv("RTENHIP_MBCONV", "all")
+    case = CASES[2]
+    m, ins = _block_spec(case, np.random.default_rng(7))
+    wd = next(n for n in m.nodes if n.kind == "const" and n.name == "wd")
+    wd.data[0, 0, 0, 0] = np.inf
+    g = m.to_graph()
+    dev = {g.input_ids[0]: torch.from_numpy(ins["x"]).cuda()}
+    g.set_timing(True)
+    g.run(dev, g.output_ids)
+    torch.cuda.synchronize()
+    assert "Conv(mbconv_block)" not in g.timing_report()
