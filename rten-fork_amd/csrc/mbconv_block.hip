@@ -451,15 +451,13 @@ bool mb_geom(int cin, int cout, int H, int W, int OH, int OW, int S, bool exp, M
 // of 16, and a band that fits LDS.  RTENHIP_MBCONV=0 disables the fusion.
 bool mbconv_block_eligible(int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl, int pb,
                            int pr, bool expand) {
-  // Measured at MobileNetV2 batch 128 (per-op eager
-  // times, fused vs apart): only the stride-2 C_in = 24 block (features.4,
-  // 178 vs 224 us) beats the three kernels apart; the others are 1.1-1.6x
-  // slower fused.  RTENHIP_MBCONV=all fuses every instantiated shape
-  // (tests), 0 none.
+  // Opt-in (RTENHIP_MBCONV=all fuses every instantiated shape; unset or 0:
+  // none).  Measured at MobileNetV2 batch 128 (profiles/r4_mbconv_block.txt,
+  // kernel time per block run, fused vs the kernels apart): 1.0-1.8x slower
+  // on every block (features.4 200 vs 195 us, features.3 291 vs 277 us), so
+  // the plan keeps the convs apart by default.
   const char* e = getenv("RTENHIP_MBCONV");
-  if (e && strcmp(e, "0") == 0) return false;
-  const bool all = e && strcmp(e, "all") == 0;
-  if (!all && !(expand && S == 2 && cin == 24)) return false;
+  if (!e || strcmp(e, "all") != 0) return false;
   if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
   if (hid % 16 != 0 || hid <= 0 || cout <= 0 || (!expand && hid != cin)) return false;
   MbGeom g;

@@ -119,18 +119,17 @@ def test_mbconv_block_bitexact(rh, monkeypatch, case):
 
 
 def test_mbconv_block_default_policy(rh, monkeypatch):
-    """By default only the measured-faster shape (stride 2, C_in 24) fuses."""
+    """By default (measured slower) no block fuses."""
     import torch
 
     monkeypatch.delenv("RTENHIP_MBCONV", raising=False)
-    for case, fused in ((CASES[4], True), (CASES[2], False)):
-        m, ins = _block_spec(case, np.random.default_rng(6))
-        g = m.to_graph()
-        dev = {g.input_ids[0]: torch.from_numpy(ins["x"]).cuda()}
-        g.set_timing(True)
-        g.run(dev, g.output_ids)
-        torch.cuda.synchronize()
-        assert ("Conv(mbconv_block)" in g.timing_report()) == fused, g.timing_report()
+    m, ins = _block_spec(CASES[4], np.random.default_rng(6))
+    g = m.to_graph()
+    dev = {g.input_ids[0]: torch.from_numpy(ins["x"]).cuda()}
+    g.set_timing(True)
+    g.run(dev, g.output_ids)
+    torch.cuda.synchronize()
+    assert "Conv(mbconv_block)" not in g.timing_report(), g.timing_report()
 
 
 def test_mbconv_block_off_switch(rh, monkeypatch):
