@@ -107,13 +107,16 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
   dd.stamps = g_dma_stamps;
   if (g_dma_persist >= 0) dd.persist_k = g_dma_persist;
   {
-    // Tile-order experiments (DmaDesc::swz): RTENHIP_DMA_SWZ=g strips of g tile
-    // columns for every DMA GEMM; RTENHIP_DMA_SWZ_MM=g for dense MatMuls only
-    // (P == N: no image structure).
+    // Tile order (DmaDesc::swz).  Dense MatMuls (P == N: no image structure)
+    // run in strips of 8 tile columns: BERT-base b32 +1.4% in an interleaved
+    // A/B (4,925 / 4,916 -> 4,992 / 4,984 seq/s; strips of 4: +1%); the conv
+    // GEMMs keep the m-fastest order (ResNet-50 b64 strips of 8: -0.3%)
+    // (profiles/r4_tile_order_ab.txt).  Experiments: RTENHIP_DMA_SWZ=g for
+    // every DMA GEMM, RTENHIP_DMA_SWZ_MM=g for the dense ones (0: m fastest).
     static const int swz_all = [] { const char* e = getenv("RTENHIP_DMA_SWZ"); return e ? atoi(e) : -1; }();
-    static const int swz_mm = [] { const char* e = getenv("RTENHIP_DMA_SWZ_MM"); return e ? atoi(e) : -1; }();
+    static const int swz_mm = [] { const char* e = getenv("RTENHIP_DMA_SWZ_MM"); return e ? atoi(e) : 8; }();
     if (swz_all >= 0) dd.swz = swz_all;
-    if (swz_mm >= 0 && d.P == d.N) dd.swz = swz_mm;
+    if (d.P == d.N) dd.swz = swz_mm;
   }
   const DmaCfgInfo& ci = kDmaCfgs[cfg];
   const int tiles = ((d.M + ci.bm - 1) / ci.bm) * ((d.N + ci.bn - 1) / ci.bn);
