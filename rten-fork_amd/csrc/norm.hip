@@ -213,7 +213,11 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   const int ngroups = (len - 1) >> 2;  // >= nchunks for len >= 8
   const int ps = R + 1;                // [chunk][row] stride
   float* xs = reinterpret_cast<float*>(lds4);
-  float* part = xs + R * len;
+  // Rows are q + 1 float4s apart in LDS (one float4 of padding): the
+  // packed-A phase reads the same column of 8 consecutive rows, which at a
+  // stride of len (a multiple of 32 dwords) would share one bank.
+  const int qs = q + 1;
+  float* part = xs + R * (len + 4);
   float* stat = part + ngroups * ps;   // mean[R], inv[R]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = (int64_t)blockIdx.x * R;
@@ -249,14 +253,17 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         asm volatile("" ::"v"(v[u].x), "v"(v[u].y), "v"(v[u].z), "v"(v[u].w));
 #pragma unroll
       for (int u = 0; u < 8; u++)
-        if (t + u * 256 < n4) lds4[t + u * 256] = v[u];
+        if (t + u * 256 < n4) {
+          const int e = t + u * 256, rr = e / q;
+          lds4[rr * qs + (e - rr * q)] = v[u];
+        }
     }
   }
   __syncthreads();
   // slice_sum: chunk c = ((x0 + x4) + (x1 + x5)) + (x2 + x6)) + (x3 + x7)
   for (int r = wave; r < nr; r += 4)
     for (int c = lane; c < nchunks; c += 64) {
-      const float4 a = lds4[r * q + 2 * c], b = lds4[r * q + 2 * c + 1];
+      const float4 a = lds4[r * qs + 2 * c], b = lds4[r * qs + 2 * c + 1];
       const float z0 = __fadd_rn(a.x, b.x), z1 = __fadd_rn(a.y, b.y);
       const float z2 = __fadd_rn(a.z, b.z), z3 = __fadd_rn(a.w, b.w);
       part[c * ps + r] = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   for (int r = wave; r < nr; r += 4) {
     const float mean = stat[r];
     for (int g = lane; g < ngroups; g += 64) {
-      const float4 v = lds4[r * q + g];
+      const float4 v = lds4[r * qs + g];
       const float d0 = __fsub_rn(v.x, mean), d1 = __fsub_rn(v.y, mean);
       const float d2 = __fsub_rn(v.z, mean), d3 = __fsub_rn(v.w, mean);
       const float ab = __fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1));
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     else
       sum = strided_sum(part + r, ps, ngroups);
     for (int i = 4 * ngroups; i < len; i++) {
-      const float d = __fsub_rn(xs[r * len + i], mean);
+      const float d = __fsub_rn(xs[r * (len + 4) + i], mean);
       sum = __fadd_rn(sum, __fmul_rn(d, d));
     }
     const float ms = __fdiv_rn(sum, (float)len);
@@ -312,7 +319,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const float mean = stat[r], inv = stat[R + r];
     for (int i = 0; i < nc; i++) {
       const int c = c0 + 64 * i;
-      const float4 v = lds4[r * q + c];
+      const float4 v = lds4[r * qs + c];
       float4 o;
       o.x = __fmul_rn(__fmul_rn(__fsub_rn(v.x, mean), inv), sc[i].x);
       o.y = __fmul_rn(__fmul_rn(__fsub_rn(v.y, mean), inv), sc[i].y);
@@ -325,7 +332,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         o.w = __fadd_rn(o.w, bb[i].w);
       }
       if (RTENHIP_LN_EXPERIMENT != 3) y4[r * q + c] = o;
-      if (pk.p) lds4[r * q + c] = o;  // this thread's own element: no hazard
+      if (pk.p) lds4[r * qs + c] = o;  // this thread's own element: no hazard
     }
   };
   if constexpr (LEN > 0 && LEN % 256 == 0) {
@@ -354,7 +361,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
       const int r = rc ? i % (RC > 0 ? RC : 1) : i % nr, t2 = rc ? i / (RC > 0 ? RC : 1) : i / nr;
       const int qq = t2 & (nq - 1), tk = t2 >> (pk.lbk - 2);
       const int kb = tk * BK + 8 * (qq >> 1) + (qq & 1);
-      const float* xr = xs + r * len;
+      const float* xr = xs + r * (len + 4);
       const float4 v = make_float4(kb < len ? xr[kb] : 0.f, kb + 2 < len ? xr[kb + 2] : 0.f,
                                    kb + 4 < len ? xr[kb + 4] : 0.f, kb + 6 < len ? xr[kb + 6] : 0.f);
       const int64_t m = row0 + r;
@@ -370,7 +377,7 @@ bool layer_norm_rows_ok(const float* x, float* y, int64_t len, const float* scal
     return false;
   const int R = (int)std::max<int64_t>(1, std::min<int64_t>(16, 6144 / len));
   const int64_t ngroups = (len - 1) / 4;
-  return ((size_t)R * len + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float) <= 64 * 1024;
+  return ((size_t)R * (len + 4) + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float) <= 64 * 1024;
 }
 
 rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
@@ -390,7 +397,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
     const int R = env_rows > 0 ? std::min(env_rows, 64)
                                : (int)std::max<int64_t>(1, std::min<int64_t>(16, 6144 / len));
     const int64_t ngroups = (len - 1) / 4;
-    const size_t rshm = ((size_t)R * len + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float);
+    const size_t rshm = ((size_t)R * (len + 4) + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float);
     if (rshm <= 64 * 1024) {
       const int64_t rblocks = (rows + R - 1) / R;
       // BERT-base / BERT-large widths get the unrolled-fold instances.
