@@ -721,6 +721,7 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
     }
   }
   d.persist_k = a.persist_k;
+  d.swz = dma_dense_swz();  // strip tile order (dense MatMuls only)
   return launch_gemm_dma(d, cfg, s);
 }
 

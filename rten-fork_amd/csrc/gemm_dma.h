@@ -95,6 +95,9 @@ struct DmaSplit {
 };
 DmaSplit dma_split_plan(int M, int N, int K, int cfg);
 
+// Tile order of dense MatMul DMA GEMMs (DmaDesc::swz; gemm_dma.hip).
+int dma_dense_swz();
+
 // Kernel configurations (all bit-identical; see gemm_dma.hip).
 int dma_num_cfgs();
 bool dma_cfg_bvec(int cfg);

@@ -95,6 +95,12 @@ DmaSplit dma_split_plan(int M, int N, int K, int cfg) {
   return sp;
 }
 
+// Tile order of dense MatMul DMA GEMMs (DmaDesc::swz): RTENHIP_DMA_SWZ_MM, default 8.
+int dma_dense_swz() {
+  static const int v = [] { const char* e = getenv("RTENHIP_DMA_SWZ_MM"); return e ? atoi(e) : 8; }();
+  return v;
+}
+
 rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const DmaDesc* d2) {
   if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty DMA GEMM");
   if (cfg < 0 || cfg >= kNumDmaCfgs) return fail(RTENHIP_INVALID_VALUE, "unknown DMA config");
@@ -107,16 +113,15 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
   dd.stamps = g_dma_stamps;
   if (g_dma_persist >= 0) dd.persist_k = g_dma_persist;
   {
-    // Tile order (DmaDesc::swz).  Dense MatMuls (P == N: no image structure)
-    // run in strips of 8 tile columns: BERT-base b32 +1.4% in an interleaved
+    // Tile order (DmaDesc::swz).  Dense MatMuls run in strips of 8 tile
+    // columns: BERT-base b32 +1.4% in an interleaved
     // A/B (4,925 / 4,916 -> 4,992 / 4,984 seq/s; strips of 4: +1%); the conv
     // GEMMs keep the m-fastest order (ResNet-50 b64 strips of 8: -0.3%)
     // (profiles/r4_tile_order_ab.txt).  Experiments: RTENHIP_DMA_SWZ=g for
     // every DMA GEMM, RTENHIP_DMA_SWZ_MM=g for the dense ones (0: m fastest).
+    // (The dense-MatMul order is set by gemm_dense_dma, dma_dense_swz.)
     static const int swz_all = [] { const char* e = getenv("RTENHIP_DMA_SWZ"); return e ? atoi(e) : -1; }();
-    static const int swz_mm = [] { const char* e = getenv("RTENHIP_DMA_SWZ_MM"); return e ? atoi(e) : 8; }();
     if (swz_all >= 0) dd.swz = swz_all;
-    if (d.P == d.N) dd.swz = swz_mm;
   }
   const DmaCfgInfo& ci = kDmaCfgs[cfg];
   const int tiles = ((d.M + ci.bm - 1) / ci.bm) * ((d.N + ci.bn - 1) / ci.bn);
@@ -138,6 +143,7 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
     dd2 = *d2;
     dd2.dbg = dd.dbg;
     dd2.n_full = dd.n_full;
+    dd2.swz = dd.swz;  // both segments walk the same tiles
   }
   bool launched = false;
   const DmaDesc* p2 = d2 ? &dd2 : nullptr;
