@@ -60,10 +60,18 @@ def parse():
 
 
 def _git_head():
+    """HEAD of the tree, or the commit __graft_entry__.build() recorded in
+    BUILD_COMMIT when the tree arrived without .git (the GPU box)."""
     try:
-        return subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
-                              text=True, timeout=5).stdout.strip() or None
+        head = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=5).stdout.strip()
+        if head:
+            return head
     except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        return open(os.path.join(ROOT, "BUILD_COMMIT")).read().strip() + " (BUILD_COMMIT)"
+    except OSError:
         return None
 
 
