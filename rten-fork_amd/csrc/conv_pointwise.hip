@@ -117,11 +117,6 @@ __global__ __launch_bounds__(256) void conv_pw_valu_kernel(
 #pragma unroll
       for (int j = 0; j < KU; j++)
         xv[j] = *(const float4*)(xp + (int64_t)min(k0 + j, d.K - 1) * P);
-      // An unconditional use of every load: the KU loads stay in flight
-      // together (else each is issued just before its first use, one round
-      // trip per k).
-#pragma unroll
-      for (int j = 0; j < KU; j++) asm volatile("" ::"v"(xv[j].x), "v"(xv[j].y), "v"(xv[j].z), "v"(xv[j].w));
 #pragma unroll
       for (int j = 0; j < KU; j++) {
         if (k0 + j >= d.K) break;
@@ -137,47 +132,29 @@ __global__ __launch_bounds__(256) void conv_pw_valu_kernel(
     }
     float* __restrict__ yp = y + ((int64_t)img * d.M + o0) * P + p;
     const float* __restrict__ rp = residual ? residual + ((int64_t)img * d.M + o0) * P + p : nullptr;
-    // Bias values of the chunk loaded before its first store (a load issued
-    // behind a store waits for that store: vmcnt retires in order).
-    float bch[MC];
 #pragma unroll
-    for (int o = 0; o < MC; o++) bch[o] = bias ? bias[o0 + min(o, olim)] : 0.f;
-    // Residual rows in groups of 8, each group's loads issued before its
-    // stores (and kept together by the empty asm use).
-    constexpr int RG = MC < 8 ? MC : 8;
-#pragma unroll
-    for (int g0 = 0; g0 < MC; g0 += RG) {
-      float4 rr[RG];
+    for (int o = 0; o < MC; o++) {
+      if (o > olim) continue;
+      float4 v = make_float4(acc[o][0].x, acc[o][0].y, acc[o][1].x, acc[o][1].y);
+      if (bias) {
+        const float b = bias[o0 + o];
+        v.x = __fadd_rn(v.x, b);
+        v.y = __fadd_rn(v.y, b);
+        v.z = __fadd_rn(v.z, b);
+        v.w = __fadd_rn(v.w, b);
+      }
       if (rp) {
-#pragma unroll
-        for (int i = 0; i < RG; i++) rr[i] = *(const float4*)(rp + (int64_t)min(g0 + i, olim) * P);
-#pragma unroll
-        for (int i = 0; i < RG; i++) asm volatile("" ::"v"(rr[i].x), "v"(rr[i].y), "v"(rr[i].z), "v"(rr[i].w));
+        const float4 r = *(const float4*)(rp + (int64_t)o * P);
+        v.x = __fadd_rn(v.x, r.x);
+        v.y = __fadd_rn(v.y, r.y);
+        v.z = __fadd_rn(v.z, r.z);
+        v.w = __fadd_rn(v.w, r.w);
       }
-#pragma unroll
-      for (int i = 0; i < RG; i++) {
-        const int o = g0 + i;
-        if (o > olim) continue;
-        float4 v = make_float4(acc[o][0].x, acc[o][0].y, acc[o][1].x, acc[o][1].y);
-        if (bias) {
-          const float b = bch[o];
-          v.x = __fadd_rn(v.x, b);
-          v.y = __fadd_rn(v.y, b);
-          v.z = __fadd_rn(v.z, b);
-          v.w = __fadd_rn(v.w, b);
-        }
-        if (rp) {
-          v.x = __fadd_rn(v.x, rr[i].x);
-          v.y = __fadd_rn(v.y, rr[i].y);
-          v.z = __fadd_rn(v.z, rr[i].z);
-          v.w = __fadd_rn(v.w, rr[i].w);
-        }
-        v.x = pw_act(v.x, d.act, d.lo, d.hi);
-        v.y = pw_act(v.y, d.act, d.lo, d.hi);
-        v.z = pw_act(v.z, d.act, d.lo, d.hi);
-        v.w = pw_act(v.w, d.act, d.lo, d.hi);
-        *(float4*)(yp + (int64_t)o * P) = v;
-      }
+      v.x = pw_act(v.x, d.act, d.lo, d.hi);
+      v.y = pw_act(v.y, d.act, d.lo, d.hi);
+      v.z = pw_act(v.z, d.act, d.lo, d.hi);
+      v.w = pw_act(v.w, d.act, d.lo, d.hi);
+      *(float4*)(yp + (int64_t)o * P) = v;
     }
   }
 }
