@@ -192,6 +192,18 @@ static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaT
   }
 }
 
+// 16-byte B copies: pointwise stride-1 convs (B[k][n] = x[img][k][p],
+// linear in k) whose 4-pixel groups stay inside one image.
+static void set_conv_bvec(const ConvDmaArgs& a, int cfg, const DmaTile& tile, DmaDesc& d) {
+  const int64_t P = a.oh * a.ow;
+  const bool pointwise = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.Hp == a.oh && a.Wp == a.ow;
+  if (pointwise && dma_cfg_bvec(cfg) && P % 4 == 0 && d.K % tile.bk == 0 && (a.C * a.Hp * a.Wp) % 4 == 0 &&
+      ((uintptr_t)d.x % 16) == 0) {
+    d.bvec = 1;
+    d.kstride = (int)(a.Hp * a.Wp);
+  }
+}
+
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
   const int64_t opg = a.O / a.groups, ipg = a.C / a.groups;
   const int64_t K = ipg * a.kh * a.kw, P = a.oh * a.ow;
@@ -221,14 +233,7 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
       if (st) return st;
       continue;
     }
-    // 16-byte B copies: pointwise stride-1 convs (B[k][n] = x[img][k][p],
-    // linear in k) whose 4-pixel groups stay inside one image.
-    const bool pointwise = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.Hp == a.oh && a.Wp == a.ow;
-    if (pointwise && dma_cfg_bvec(cfg) && P % 4 == 0 && K % tile.bk == 0 && (a.C * a.Hp * a.Wp) % 4 == 0 &&
-        ((uintptr_t)d.x % 16) == 0) {
-      d.bvec = 1;
-      d.kstride = (int)(a.Hp * a.Wp);
-    }
+    set_conv_bvec(a, cfg, tile, d);
     if (a.split) {
       const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
       if (sp.split_tiles > 0 && a.ws && a.counters && sp.ws_floats <= a.ws_cap && sp.counters <= a.cnt_cap) {
@@ -266,6 +271,8 @@ rtenhip_status conv_dma_dual(Ctx* c, const ConvDmaArgs& a3, const ConvDmaArgs& a
   DmaDesc d3, dd;
   fill_conv_desc(a3, 0, false, tile, t3, d3);
   fill_conv_desc(ad, 0, false, tile, td, dd);
+  set_conv_bvec(a3, cfg, tile, d3);  // (kept only when both segments qualify, launch_gemm_dma)
+  set_conv_bvec(ad, cfg, tile, dd);
   d3.residual = nullptr;
   d3.persist_k = a3.persist_k;
   return launch_gemm_dma(d3, cfg, c->stream, &dd);

@@ -70,6 +70,10 @@ struct DmaDesc {
   // consecutive tiles -- what one XCD's resident blocks work on together --
   // is a compact block of A rows and B columns in that XCD's L2.
   int swz;
+  // Dual GEMM (set by launch_gemm_dma): 1 = one continuous K loop over both
+  // segments (segment 2's first tiles stream in while segment 1 finishes),
+  // 0 = two passes with a drain between them.
+  int dual_one;
   int bvec;                 // B copied 16 bytes per lane (dma_cfg_bvec(cfg) and pointwise:
                             // koff(k) = k * kstride, P % 4 == 0, K % BK == 0)
   int kstride;              // elements between consecutive k rows of B (bvec)

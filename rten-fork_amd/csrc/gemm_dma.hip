@@ -138,12 +138,19 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
     // Dual GEMM: same output tiles, no KC split, both segments through the
     // multi-block fold with 4-byte B copies.
     if (d2->M != d.M || d2->N != d.N || d2->K <= 0 || !(d2->tile == d.tile) || d.split_tiles || d.residual ||
-        d.cin || d2->cin || d.bvec || d2->bvec || d.pk_out)
+        d.cin || d2->cin || d.pk_out)
       return fail(RTENHIP_INVALID_VALUE, "bad dual DMA GEMM");
     dd2 = *d2;
     dd2.dbg = dd.dbg;
     dd2.n_full = dd.n_full;
     dd2.swz = dd.swz;  // both segments walk the same tiles
+    // One K loop needs segment 1 to end on an even tile (register-set
+    // parity) with no partial tile.  RTENHIP_DMA_DUAL1=0: two passes.
+    static const int dual1 = [] { const char* e = getenv("RTENHIP_DMA_DUAL1"); return e ? atoi(e) : 1; }();
+    dd.dual_one = dual1 && d2->K % (2 * ci.bk) == 0;
+    // 16-byte B copies only when both segments allow them, in one K loop
+    // (otherwise both take 4-byte copies, always valid).
+    if (!(dd.bvec && dd2.bvec && dd.dual_one && dma_cfg_bvec(cfg))) dd.bvec = dd2.bvec = 0;
   }
   bool launched = false;
   const DmaDesc* p2 = d2 ? &dd2 : nullptr;

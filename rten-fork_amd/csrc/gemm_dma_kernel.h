@@ -105,7 +105,7 @@ __device__ __forceinline__ float f4_at(const float4& v, int j) {
 template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES, int HEAD_,
           bool MULTI_KB, bool BVEC, bool DUAL = false>
 __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d2, int tiles_m, int tiles_n) {
-  static_assert(!DUAL || (MULTI_KB && !BVEC), "dual GEMMs fold through the multi-block path, 4-byte B copies");
+  static_assert(!DUAL || MULTI_KB, "dual GEMMs fold through the multi-block path");
   static_assert(STAGES >= 2 && STAGES <= 4, "2..4 stages");
   constexpr int NW = NT / 64;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;
@@ -166,7 +166,12 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   f32x16 carry[DUAL ? MI : 1][DUAL ? NI : 1];
   // mode 0: one GEMM; 1: dual segment 1 (fold into carry, no epilogue);
   // 2: dual segment 2 (epilogue adds carry).
-  auto process = [&](const KDesc& d, const int wg, const int kb_split, const int split_idx, const int mode) __attribute__((always_inline)) {
+  // mode 3 (DUAL): both segments in one pipelined K loop -- segment 1's
+  // tiles (desc e: the downsample) then segment 2's (desc d: conv3), the
+  // refill DMAs running on across the boundary, so segment 2's first tiles
+  // are in flight while segment 1 finishes; segment 1's fold is the carry.
+  auto process = [&](const KDesc& d, const int wg, const int kb_split, const int split_idx, const int mode,
+                     const KDesc& e) __attribute__((always_inline)) {
   // Lane-derived values are recomputed per item: hoisted out of the item loop
   // they would stay live across it and spill.
   int tid = tid_o;
@@ -191,8 +196,12 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   const int tn = tni * BN;
   const int tiles_k = (K + BK - 1) / BK;
   constexpr int TPB = DKC / BK;  // K tiles per KC block
+  // Dual, mode 3: segment 1 (e) occupies virtual K tiles [0, tk1), segment 2
+  // (d) [tk1, tk1 + tiles_k).  (Same M, N and tile; both 4-byte B copies.)
+  const bool seg2 = DUAL && mode == 3;
+  const int tk1 = seg2 ? (e.K + BK - 1) / BK : 0;
   const int kt_lo = kb_split >= 0 ? kb_split * TPB : 0;
-  const int kt_hi = kb_split >= 0 ? min(tiles_k, kt_lo + TPB) : tiles_k;
+  const int kt_hi = kb_split >= 0 ? min(tiles_k, kt_lo + TPB) : tk1 + tiles_k;
 
   const u32x4 ra = make_rsrc(d.apk, 0x7fffffffu);
   const u32x4 rb = make_rsrc(d.x, d.x_bytes);
@@ -239,6 +248,48 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   const uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
   const_int_t* ktab4 = (const_int_t*)d.ktab4;
   const uint32_t lds0 = lds_addr(lds);
+  u32x4 ra1 = ra, rb1 = rb;  // segment 1's resources (mode 3)
+  uint32_t vb1[DUAL ? NG : 1];
+  uint32_t a_row_base1 = 0;
+  const_int_t* ktab41 = ktab4;
+  uint32_t vb41[BVEC && DUAL ? B_PER_W : 1];
+  if constexpr (DUAL) {
+    if (seg2) {
+      ra1 = make_rsrc(e.apk, 0x7fffffffu);
+      rb1 = make_rsrc(e.x, e.x_bytes);
+      a_row_base1 = (uint32_t)tmi * (uint32_t)tk1 * (BM * BK * 4);
+      ktab41 = (const_int_t*)e.ktab4;
+      if constexpr (BVEC) {
+#pragma unroll
+        for (int i = 0; i < B_PER_W; i++) {
+          const int kk = (wave * B_PER_W + i) * 4 + (lane >> 4);
+          const int n = tn + (lane & 15) * 4;
+          uint32_t off = DMA_OOB;
+          if (n < N) {
+            const int img = fdiv(n, e.fdP);
+            const int p = n - img * e.P;
+            off = (uint32_t)(((int64_t)img * e.x_img + p) * 4 + (int64_t)kk * e.kstride * 4);
+          }
+          vb41[i] = off;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        const int pos = g * 64 + lane;
+        const int q = pos % WN;
+        const int n = tn + (pos - q) + (q % NI) * 32 + q / NI;
+        uint32_t off = DMA_OOB;
+        if (n < N) {
+          const int img = fdiv(n, e.fdP);
+          const int p = n - img * e.P;
+          const int oy = fdiv(p, e.fdOW);
+          const int ox = p - oy * e.OW;
+          off = (uint32_t)(((int64_t)img * e.x_img + (int64_t)oy * e.ystride + (int64_t)ox * e.xstride) * 4);
+        }
+        vb1[g] = off;
+      }
+    }
+  }
 
   // K-table offsets of the tile about to be issued, loaded at the start of
   // the tile body that issues it, so the scalar load's latency hides under
@@ -250,7 +301,12 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   uint32_t kpre[2][KPRE];
   auto load_k = [&](int kt, int slot) __attribute__((always_inline)) {
     if constexpr (!BVEC) {
-      kt = min(kt, tiles_k - 1);
+      if (DUAL && kt < tk1) {  // (tk1 = 0 unless mode 3)
+#pragma unroll
+        for (int i = 0; i < B_PER_W; i++) kpre[slot][i] = (uint32_t)ktab41[kt * BK + (wave * B_PER_W + i) / NG];
+        return;
+      }
+      kt = min(kt - tk1, tiles_k - 1);
 #pragma unroll
       for (int i = 0; i < B_PER_W; i++) kpre[slot][i] = (uint32_t)ktab4[kt * BK + (wave * B_PER_W + i) / NG];
     }
@@ -270,24 +326,35 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   auto issue_j = [&](int stage, int kt, int j, int slot) __attribute__((always_inline)) {
     const uint32_t As = lds0 + (uint32_t)(stage * STAGE * 4);
     const uint32_t Bs = As + BM * BK * 4;
+    const bool s1 = DUAL && kt < tk1;  // wave-uniform
     if (j < A_PER_W) {
-      const uint32_t a_soff = a_row_base + (uint32_t)kt * (BM * BK * 4);
+      const uint32_t a_soff = s1 ? a_row_base1 + (uint32_t)kt * (BM * BK * 4)
+                                 : a_row_base + (uint32_t)(kt - tk1) * (BM * BK * 4);
       const uint32_t dst = As + (uint32_t)((wave * A_PER_W + j) * A_CHUNK);
       if constexpr (A_LB == 16)
-        lds_dma16(ra, dst, va + j * A_CHUNK, a_soff);
+        lds_dma16(s1 ? ra1 : ra, dst, va + j * A_CHUNK, a_soff);
       else
-        lds_dma4(ra, dst, va + j * A_CHUNK, a_soff);
+        lds_dma4(s1 ? ra1 : ra, dst, va + j * A_CHUNK, a_soff);
       return;
     }
     const int i = j - A_PER_W;
     if constexpr (BVEC) {
-      const uint32_t b_soff = (uint32_t)kt * (uint32_t)(BK * d.kstride * 4);
       const int gi = wave * B_PER_W + i;  // rows 4*gi .. 4*gi+3: 1 KB of LDS
-      lds_dma16(rb, Bs + gi * 1024, vb4[i], b_soff);
+      if constexpr (DUAL) {
+        const uint32_t b_soff = s1 ? (uint32_t)kt * (uint32_t)(BK * e.kstride * 4)
+                                   : (uint32_t)(kt - tk1) * (uint32_t)(BK * d.kstride * 4);
+        lds_dma16(s1 ? rb1 : rb, Bs + gi * 1024, s1 ? vb41[i] : vb4[i], b_soff);
+      } else {
+        const uint32_t b_soff = (uint32_t)kt * (uint32_t)(BK * d.kstride * 4);
+        lds_dma16(rb, Bs + gi * 1024, vb4[i], b_soff);
+      }
     } else {
       const int gi = wave * B_PER_W + i;  // wave-uniform
       const int kl = gi / NG, g = gi % NG;
-      lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[slot][i]);
+      if constexpr (DUAL)
+        lds_dma4(s1 ? rb1 : rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), s1 ? vb1[g] : vb[g], kpre[slot][i]);
+      else
+        lds_dma4(rb, Bs + (uint32_t)((kl * BN + g * 64) * 4), vb[g], kpre[slot][i]);
     }
   };
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
@@ -634,6 +701,64 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     }
     if (tid == 0)
       __hip_atomic_store(d.counters + split_idx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (DUAL && seg2) {
+    // Segment 1's KC blocks (virtual tiles [0, tk1)): block 0 + e's bias,
+    // later blocks added in K order -> the carry; then segment 2's blocks
+    // from tile tk1, folded as one GEMM (the epilogue adds the carry).
+    // tk1 and TPB are even (register-set parity) and multiples of STAGES for
+    // the fast path (K1 a multiple of 64: the ResNet downsample widths).
+    run(0, min(TPB, tk1));
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          float x = e.alpha == 1.f ? acc[mi][ni][j] : __fmul_rn(acc[mi][ni][j], e.alpha);
+          if (e.bias) {
+            cfloat_t* cb = (cfloat_t*)e.bias;
+            const int r = tm + wm + mi * 32 + (j & 3) + 8 * (j >> 2);
+            const float lo = cb[min(r, M - 1)], hi = cb[min(r + 4, M - 1)];
+            x = __fadd_rn(x, half ? hi : lo);
+          }
+          sum[mi][ni][j] = x;
+        }
+        acc[mi][ni] = (f32x16){0};
+      }
+    for (int kt = TPB; kt < tk1; kt += TPB) {
+      run(kt, min(kt + TPB, tk1));
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++) {
+#pragma unroll
+          for (int j = 0; j < 16; j++) sum[mi][ni][j] = __fmaf_rn(acc[mi][ni][j], e.alpha, sum[mi][ni][j]);
+          acc[mi][ni] = (f32x16){0};
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++) carry[mi][ni] = sum[mi][ni];
+    run(tk1, tk1 + min(TPB, tiles_k));
+#pragma unroll
+    for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+      for (int ni = 0; ni < NI; ni++) {
+        first_block(sum[mi][ni], acc[mi][ni], mi, ni);
+        acc[mi][ni] = (f32x16){0};
+      }
+    for (int kt = TPB; kt < tiles_k; kt += TPB) {
+      run(tk1 + kt, tk1 + min(kt + TPB, tiles_k));
+#pragma unroll
+      for (int mi = 0; mi < MI; mi++)
+#pragma unroll
+        for (int ni = 0; ni < NI; ni++) {
+#pragma unroll
+          for (int j = 0; j < 16; j++) sum[mi][ni][j] = __fmaf_rn(acc[mi][ni][j], d.alpha, sum[mi][ni][j]);
+          acc[mi][ni] = (f32x16){0};
+        }
+    }
   } else {
     // K > DKC: block 0 is peeled so the bias/beta fold sits outside the loop.
     static_assert(TPB % 2 == 0, "register-set parity across K blocks");
@@ -937,13 +1062,19 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     // across it, they spill).
     const KDesc* dp = (const KDesc*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(dp));
-    if constexpr (DUAL) {
-      process(dp[1], wg, -1, -1, 1);  // d2 (the second kernel argument): segment 1
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // segment 1's LDS stages are free
-      process(dp[0], wg, -1, -1, 2);
+    if constexpr (DUAL && BVEC) {
+      process(dp[0], wg, -1, -1, 3, dp[1]);  // (16-byte B copies: one K loop only)
+    } else if constexpr (DUAL) {
+      if (dp[0].dual_one) {
+        process(dp[0], wg, -1, -1, 3, dp[1]);  // d2 (the second kernel argument): segment 1
+      } else {
+        process(dp[1], wg, -1, -1, 1, dp[1]);  // segment 1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // segment 1's LDS stages are free
+        process(dp[0], wg, -1, -1, 2, dp[1]);
+      }
     } else {
-      process(*dp, wg, kbs, si, 0);
+      process(*dp, wg, kbs, si, 0, *dp);
     }
     if (!persistent) break;
     // Every wave is done with this item's LDS before the next item's DMAs.
@@ -1011,6 +1142,12 @@ static bool launch_dma_cfg(const DmaDesc& d, hipStream_t s, const DmaDesc* d2) {
   const int tiles_m = (d.M + BM - 1) / BM, tiles_n = (d.N + BN - 1) / BN;
   if (d2) {
     if constexpr (dma_dual_ok<NT, BM, BN, BK, WM_, WN_>()) {
+      if constexpr (dma_bvec_ok<NT, BM, BN, BK, WM_, WN_>()) {
+        if (d.bvec) {  // (both segments; launch_gemm_dma checked)
+          launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, true, true>(d, tiles_m, tiles_n, s, d2);
+          return true;
+        }
+      }
       launch_dma_variant<NT, BM, BN, BK, WM_, WN_, MINW, STAGES, HD, true, false, true>(d, tiles_m, tiles_n, s, d2);
       return true;
     }

@@ -384,7 +384,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
                                  const float* scale, const float* bias, float eps,
                                  hipStream_t s, const PackedOut* pk) {
   if (rows == 0 || len == 0) return RTENHIP_OK;
-  if (pk && (!layer_norm_rows_ok(x, y, len, scale, bias) || getenv("RTENHIP_LN_ROWS")))
+  if (pk && !layer_norm_rows_ok(x, y, len, scale, bias))
     return fail(RTENHIP_UNSUPPORTED_VALUE, "LayerNorm: packed output needs the rows kernel");
   const PackedOut pko = pk ? *pk : PackedOut{};
   const bool rows_ok = len % 8 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&

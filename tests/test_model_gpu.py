@@ -592,6 +592,8 @@ DUAL_BLOCKS = [
     (2, 256, 18, 18, 128, 512, 2),   # layer2.0: strided downsample, K = 128 + 256
     (1, 512, 9, 9, 256, 1024, 2),    # layer3.0: K = 256 + 512 (downsample folds 2 KC blocks)
     (1, 96, 7, 11, 48, 136, 1),      # ragged M (136), K not a multiple of 16, N = 77
+    (2, 48, 12, 12, 32, 128, 1),     # K1 = 48: no single K loop, so 4-byte B copies
+    (1, 512, 8, 8, 256, 512, 1),     # 16-byte B copies, K = 256 + 512 (segment 1 folds 2 KC blocks)
 ]
 
 
