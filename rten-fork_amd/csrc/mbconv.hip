@@ -186,6 +186,27 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
     // buffer, and the ones after that are only written once every thread has
     // passed the next barrier, i.e. finished reading these.
     __syncthreads();
+    // Depthwise products and sums as packed pairs (v_pk_mul / v_pk_add: each
+    // component rounds exactly as the scalar op): two outputs of a channel
+    // when a thread has several (stride 1), else the pass's two channels.
+    if constexpr (NQ == 1 && CP == 2) {
+      const int cl0 = c0 - c_begin;
+      if (c0 + 1 < c_end && fin[cl0] && fin[cl0 + 1]) {
+        if (tmask[0] >> 9) {
+          vm_f32x2 acc = {b_d[cl0], b_d[cl0 + 1]};
+#pragma unroll
+          for (int i = 0; i < 9; i++) {
+            const vm_f32x2 v = {ebuf[taddr[0][i]], ebuf[plane + taddr[0][i]]};
+            const vm_f32x2 w = {w_d[cl0 * 9 + i], w_d[cl0 * 9 + 9 + i]};
+            acc = acc + v * w;
+          }
+          float* y0 = d.y + ((int64_t)n * d.hidden + c0) * d.OH * d.OW + (int64_t)oy0 * d.OW + t;
+          y0[0] = act(acc.x, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+          y0[(int64_t)d.OH * d.OW] = act(acc.y, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+        }
+        return;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < CP; j++) {
       const int c = c0 + j;
@@ -199,12 +220,26 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
       float* yc = d.y + ((int64_t)n * d.hidden + c) * d.OH * d.OW + (int64_t)oy0 * d.OW;
       if (fin[cl]) {
 #pragma unroll
-        for (int q = 0; q < NQ; q++) {
-          if (!(tmask[q] >> 9)) continue;  // not an output of this band
-          float acc = b0;
+        for (int q = 0; q + 1 < NQ; q += 2) {
+          if (!((tmask[q] | tmask[q + 1]) >> 9)) continue;  // neither is an output of this band
+          // (a non-output's taps all point at zero slots: harmless reads)
+          vm_f32x2 acc = {b0, b0};
 #pragma unroll
-          for (int i = 0; i < 9; i++) acc = __fadd_rn(acc, __fmul_rn(eb[taddr[q][i]], wk[i]));
-          yc[t + 256 * q] = act(acc, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+          for (int i = 0; i < 9; i++) {
+            const vm_f32x2 v = {eb[taddr[q][i]], eb[taddr[q + 1][i]]};
+            acc = acc + v * (vm_f32x2){wk[i], wk[i]};
+          }
+          if (tmask[q] >> 9) yc[t + 256 * q] = act(acc.x, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+          if (tmask[q + 1] >> 9) yc[t + 256 * (q + 1)] = act(acc.y, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+        }
+        if constexpr (NQ % 2 == 1) {
+          constexpr int q = NQ - 1;
+          if (tmask[q] >> 9) {
+            float acc = b0;
+#pragma unroll
+            for (int i = 0; i < 9; i++) acc = __fadd_rn(acc, __fmul_rn(eb[taddr[q][i]], wk[i]));
+            yc[t + 256 * q] = act(acc, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+          }
         }
       } else {
 #pragma unroll
@@ -331,11 +366,10 @@ static bool flat_ok(int cin, int H, int W) {
 // (banded kernel, the x band in VGPRs) or a plane of at most 256 pixels whose
 // channels fit LDS (flat kernel).
 //
-// Measured at MobileNetV2 batch 128 (profiles/r3_mbconv_fused_vs_split.txt)
-// the expand's VALU fma chains run far below the MFMA pointwise conv, so only
-// the pair where the saved HBM round trip outweighs that is fused by default:
-// C_in = 16 (features.2, a 616 MB intermediate per batch).  RTENHIP_EXPAND_DW
-// = "all" takes every eligible pair (tests), "0" none.
+// Fused by default where the saved HBM round trip outweighs the kernel's VALU
+// cost (measured at MobileNetV2 batch 128): the banded kernel for C_in = 16 / 24
+// (features.2-4).  RTENHIP_EXPAND_DW = "all" takes every eligible pair (tests),
+// "0" none.
 bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, int pr) {
   if (S != 1 && S != 2) return false;
   if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
@@ -343,7 +377,10 @@ bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, in
   const bool all = e && strcmp(e, "all") == 0;
   if (e && strcmp(e, "0") == 0) return false;
   const bool banded = (cin == 16 || cin == 24 || cin == 32) && W % 4 == 0 && W / 4 <= 256 / 3;
-  if (!all) return banded && cin == 16;
+  // Default: the banded kernel for C_in = 16 / 24 (features.2-4: 0.197 / 0.173 / 0.122 ms fused vs
+  // 0.21+ / 0.206 / 0.156 ms apart); C_in = 32 at 28x28 is even or slower, the whole-plane
+  // kernel much slower (profiles/r4_expand_dw_policy.txt).
+  if (!all) return banded && (cin == 16 || cin == 24);
   return banded || flat_ok(cin, H, W);
 }
 

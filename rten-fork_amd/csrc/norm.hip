@@ -201,6 +201,10 @@ __device__ __forceinline__ float strided_sum_n(const float* p, int s) {
 #ifndef RTENHIP_LN_EXPERIMENT
 #define RTENHIP_LN_EXPERIMENT 0
 #endif
+// Rows per workgroup: min(16, RTENHIP_LN_ROWS_NUM / len) (8 at BERT's 768).
+#ifndef RTENHIP_LN_ROWS_NUM
+#define RTENHIP_LN_ROWS_NUM 6144
+#endif
 
 template <int LEN>
 __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
@@ -355,7 +359,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     // (A full block of an instance has nr = R known at compile time (the host
     // picks R the same way): the index split below is then shifts and
     // multiplies instead of two integer divisions per chunk.)
-    constexpr int RC = LEN > 0 ? (6144 / LEN < 16 ? 6144 / LEN : 16) : 0;
+    constexpr int RC = LEN > 0 ? (RTENHIP_LN_ROWS_NUM / LEN < 16 ? RTENHIP_LN_ROWS_NUM / LEN : 16) : 0;
     const bool rc = RC > 0 && nr == RC;
     for (int i = threadIdx.x; i < total; i += 256) {
       const int r = rc ? i % (RC > 0 ? RC : 1) : i % nr, t2 = rc ? i / (RC > 0 ? RC : 1) : i / nr;
@@ -375,7 +379,7 @@ bool layer_norm_rows_ok(const float* x, float* y, int64_t len, const float* scal
   if (len % 8 != 0 || (uintptr_t)x % 16 || (uintptr_t)y % 16 || (uintptr_t)scale % 16 ||
       (bias && (uintptr_t)bias % 16))
     return false;
-  const int R = (int)std::max<int64_t>(1, std::min<int64_t>(16, 6144 / len));
+  const int R = (int)std::max<int64_t>(1, std::min<int64_t>(16, RTENHIP_LN_ROWS_NUM / len));
   const int64_t ngroups = (len - 1) / 4;
   return ((size_t)R * (len + 4) + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float) <= 64 * 1024;
 }
@@ -395,7 +399,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
       return e ? atoi(e) : 0;
     }();
     const int R = env_rows > 0 ? std::min(env_rows, 64)
-                               : (int)std::max<int64_t>(1, std::min<int64_t>(16, 6144 / len));
+                               : (int)std::max<int64_t>(1, std::min<int64_t>(16, RTENHIP_LN_ROWS_NUM / len));
     const int64_t ngroups = (len - 1) / 4;
     const size_t rshm = ((size_t)R * (len + 4) + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float);
     if (rshm <= 64 * 1024) {
