@@ -667,9 +667,12 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
       const int PB = 256 / OW;
       auto rows_for = [&](int th) { return (th - 1) * sh + (kh - 1) * dh + 1; };
       int TH = OH;
+      // 8192 floats: MobileNetV2's 14 -> 7 stride-2 layer then stages whole
+      // planes (0.054 -> 0.022 ms); the other layers are unchanged and 16384
+      // slows the 28 -> 14 one (profiles/r4_dw_budget.txt).
       static const int budget = [] {
         const char* e = getenv("RTENHIP_DW_LDS_FLOATS");  // tuning experiments
-        return e ? atoi(e) : 4096;
+        return e ? atoi(e) : 8192;
       }();
       while (TH > 1 && PB * rows_for(TH) * W > budget) TH = (TH + 1) / 2;
       const int rows_in = rows_for(TH);
