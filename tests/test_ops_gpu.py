@@ -211,6 +211,24 @@ def test_depthwise4_fused_residual_clip(rh, oracle):
     assert_bits(got, exp, "depthwise4 residual clip")
 
 
+@pytest.mark.parametrize("shape", [(2, 20, 14, 14, 1), (2, 38, 7, 7, 1), (2, 40, 14, 14, 2), (1, 7, 14, 14, 1)],
+                         ids=lambda s: "x".join(map(str, s)))
+def test_depthwise_flat_residual_clip(rh, oracle, shape):
+    """Whole-plane depthwise blocks (rows of 14 / 7 floats) with the fused
+    residual Add and Clip: outputs staged in LDS and stored as 16-byte runs
+    where a block's planes allow it, per element otherwise (ragged tails)."""
+    N, C, H, W, s = shape
+    x = rnd(oracle, 41, N, C, H, W)
+    w = rnd(oracle, 42, C, 1, 3, 3, scale=0.3)
+    b = rnd(oracle, 43, C)
+    oh = (H + 2 - 3) // s + 1
+    res = rnd(oracle, 44, N, C, oh, oh)
+    exp = oracle.clip(oracle.add(oracle.conv(x, w, b, pads=(1, 1, 1, 1), strides=(s, s), groups=C), res), 0.0, 0.4)
+    got = host(rh.conv(dev(x), dev(w), dev(b), padding=(1, 1, 1, 1), strides=(s, s), groups=C, residual=dev(res),
+                       act="clip", act_range=(0.0, 0.4)))
+    assert_bits(got, exp, "depthwise flat residual clip")
+
+
 def test_conv_fused_residual_relu(rh, oracle):
     """Conv -> Add(residual) -> Relu fused epilogue == the three reference ops."""
     x = rnd(oracle, 31, 2, 64, 14, 14)
