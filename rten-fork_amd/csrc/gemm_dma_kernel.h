@@ -101,7 +101,9 @@ __device__ __forceinline__ float f4_at(const float4& v, int j) {
 // keeps the folded value (bias included) in registers; segment 2 (d: conv3)
 // then runs its own K loop and adds it where the unfused graph adds the
 // residual: the same per-element operations as the two convs and the Add,
-// without the downsample output's round trip through HBM.
+// without the downsample output's round trip through HBM.  With d.dual_one
+// both segments run as one K loop (mode 3 below); with BVEC (both segments
+// pointwise stride-1) only that way.
 template <int NT, int BM, int BN, int BK, int WAVES_M, int WAVES_N, int MINW, int STAGES, int HEAD_,
           bool MULTI_KB, bool BVEC, bool DUAL = false>
 __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d2, int tiles_m, int tiles_n) {
