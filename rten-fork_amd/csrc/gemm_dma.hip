@@ -146,7 +146,9 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
     dd2.swz = dd.swz;  // both segments walk the same tiles
     // One K loop needs segment 1 to end on an even tile (register-set
     // parity) with no partial tile.  RTENHIP_DMA_DUAL1=0: two passes.
-    static const int dual1 = [] { const char* e = getenv("RTENHIP_DMA_DUAL1"); return e ? atoi(e) : 1; }();
+    // (read per launch, so tests can cover both forms in one process)
+    const char* dual1_env = getenv("RTENHIP_DMA_DUAL1");
+    const int dual1 = dual1_env ? atoi(dual1_env) : 1;
     dd.dual_one = dual1 && d2->K % (2 * ci.bk) == 0;
     // 16-byte B copies only when both segments allow them, in one K loop
     // (otherwise both take 4-byte copies, always valid).

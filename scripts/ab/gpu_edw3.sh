@@ -12,4 +12,4 @@ run() {
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'])" $O/$tag.json $tag
 }
 for r in 1 2 3; do run packed$r "" && run old$r rten-fork_amd/exp_edw/librten_hip_edwold.so || exit 1; done
-LN_EXPS=r16 bash scripts/gpu_ln.sh
+LN_EXPS=r16 bash scripts/ab/gpu_ln.sh

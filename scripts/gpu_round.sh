@@ -3,4 +3,4 @@
 # then the attention and LayerNorm timing experiments and the tile-order A/B.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-bash scripts/gpu_check.sh "${1:-now}" && bash scripts/gpu_attn.sh && bash scripts/gpu_ln.sh
+bash scripts/gpu_check.sh "${1:-now}" && bash scripts/ab/gpu_attn.sh && bash scripts/ab/gpu_ln.sh

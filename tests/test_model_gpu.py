@@ -598,12 +598,14 @@ DUAL_BLOCKS = [
 
 
 @pytest.mark.parametrize("case", DUAL_BLOCKS, ids=lambda c: "x".join(map(str, c)))
-@pytest.mark.parametrize("mode", ["force", "off"])
+@pytest.mark.parametrize("mode", ["force", "force-two-pass", "off"])
 def test_bottleneck_dual_gemm_bitexact(rh, monkeypatch, case, mode):
     """ResNet bottleneck with a downsample branch: relu(conv3(h) + b3 +
     downsample(x)) with conv3 and the downsample in one dual GEMM launch
-    (RTENHIP_DUAL=1 forces it; the default takes it when faster) or apart
-    (RTENHIP_NO_DUAL=1).  Bit-exact against the oracle, eager and replayed."""
+    (RTENHIP_DUAL=1 forces it; the default takes it when faster) -- one K
+    loop over both segments by default, two passes with
+    RTENHIP_DMA_DUAL1=0 -- or apart (RTENHIP_NO_DUAL=1).  Bit-exact against
+    the oracle, eager and replayed."""
     import torch
     import graph_runner
     from rten_hip.graph import ModelSpec
@@ -611,8 +613,11 @@ def test_bottleneck_dual_gemm_bitexact(rh, monkeypatch, case, mode):
     N, C, H, W, Cm, Co, s = case
     monkeypatch.delenv("RTENHIP_DUAL", raising=False)
     monkeypatch.delenv("RTENHIP_NO_DUAL", raising=False)
-    if mode == "force":
+    monkeypatch.delenv("RTENHIP_DMA_DUAL1", raising=False)
+    if mode.startswith("force"):
         monkeypatch.setenv("RTENHIP_DUAL", "1")
+        if mode == "force-two-pass":
+            monkeypatch.setenv("RTENHIP_DMA_DUAL1", "0")
     else:
         monkeypatch.setenv("RTENHIP_NO_DUAL", "1")
     rng = np.random.default_rng(C + Cm + Co)
@@ -644,7 +649,7 @@ def test_bottleneck_dual_gemm_bitexact(rh, monkeypatch, case, mode):
     g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
     torch.cuda.synchronize()
     rep = g.timing_report()
-    assert ("Conv(dual)" in rep) == (mode == "force"), rep
+    assert ("Conv(dual)" in rep) == mode.startswith("force"), rep
 
 
 @pytest.mark.parametrize("group", ["on", "off"])
