@@ -544,13 +544,16 @@ def test_matmul_chain_packed_a_bitexact(rh, monkeypatch, case, pk_out):
         assert _bits_equal(got, exp), f"run {r}: max abs {np.abs(got - exp).max():.3g}"
 
 
+@pytest.mark.parametrize("K", [256, 768])
 @pytest.mark.parametrize("pk_out", ["1", "0"])
-def test_layernorm_packed_a_bitexact(rh, monkeypatch, pk_out):
+def test_layernorm_packed_a_bitexact(rh, monkeypatch, pk_out, K):
     """LayerNormalization -> two MatMuls reading it as A (BERT's LN -> Q / K)
     with the LN output also the second MatMul's fused residual: from the
     second run on the LN stores its rows both row-major and in the MatMuls'
     packed-A layout, and neither MatMul packs A (Plan::pk_cons).  Ragged M
-    (300 rows).  Bit-exact, eager, captured and replayed."""
+    (300 rows: a partial last block of rows, for the runtime-length kernel
+    and for BERT's 768-wide instance).  Bit-exact, eager, captured and
+    replayed."""
     import torch
     import graph_runner
     from rten_hip.graph import ModelSpec
@@ -560,7 +563,7 @@ def test_layernorm_packed_a_bitexact(rh, monkeypatch, pk_out):
     else:
         monkeypatch.delenv("RTENHIP_NO_PK_OUT", raising=False)
     rng = np.random.default_rng(5)
-    M, K, N = 300, 256, 256
+    M, N = 300, K  # (N = K: the second MatMul adds h as its residual)
     m = ModelSpec("lnmm")
     x = m.value("x")
     m.inputs = ["x"]
