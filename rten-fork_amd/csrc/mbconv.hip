@@ -368,8 +368,8 @@ static bool flat_ok(int cin, int H, int W) {
 //
 // Fused by default where the saved HBM round trip outweighs the kernel's VALU
 // cost (measured at MobileNetV2 batch 128): the banded kernel for C_in = 16 / 24
-// (features.2-4).  RTENHIP_EXPAND_DW = "all" takes every eligible pair (tests),
-// "0" none.
+// (features.2-4) and C_in = 32 at stride 2 (features.7).  RTENHIP_EXPAND_DW =
+// "all" takes every eligible pair (tests), "0" none.
 bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, int pr) {
   if (S != 1 && S != 2) return false;
   if (pt > 1 || pl > 1 || pb > 1 || pr > 1) return false;
@@ -378,9 +378,10 @@ bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, in
   if (e && strcmp(e, "0") == 0) return false;
   const bool banded = (cin == 16 || cin == 24 || cin == 32) && W % 4 == 0 && W / 4 <= 256 / 3;
   // Default: the banded kernel for C_in = 16 / 24 (features.2-4: 0.197 / 0.173 / 0.122 ms fused vs
-  // 0.21+ / 0.206 / 0.156 ms apart); C_in = 32 at 28x28 is even or slower, the whole-plane
-  // kernel much slower (profiles/r4_expand_dw_policy.txt).
-  if (!all) return banded && (cin == 16 || cin == 24);
+  // 0.21+ / 0.206 / 0.156 ms apart) and C_in = 32 at stride 2 (features.7: 0.052 vs 0.063 ms);
+  // C_in = 32 at stride 1 is even or slower, the whole-plane kernel much slower
+  // (profiles/r4_expand_dw_policy.txt).
+  if (!all) return banded && (cin == 16 || cin == 24 || (cin == 32 && S == 2));
   return banded || flat_ok(cin, H, W);
 }
 

@@ -260,7 +260,8 @@ def test_expand_depthwise_fused_bitexact(rh, monkeypatch, case, policy):
     (conv_2d_pointwise then conv_2d_depthwise_block, with the graph's Clip /
     Relu after each), eager and replayed; shapes it does not take run unfused.
     RTENHIP_EXPAND_DW=all fuses every pair a fused kernel can take; the
-    default only the C_in = 16 / 24 pairs (see expand_dw_eligible)."""
+    default the C_in = 16 / 24 pairs and C_in = 32 at stride 2 (see
+    expand_dw_eligible)."""
     import torch
     import graph_runner
     from rten_hip.graph import ModelSpec
@@ -303,6 +304,6 @@ def test_expand_depthwise_fused_bitexact(rh, monkeypatch, case, policy):
     if policy == "all":
         assert fused == ((C in (16, 24, 32) and W % 4 == 0) or H * W <= 256), g.timing_report()
     else:
-        assert fused == (C in (16, 24) and W % 4 == 0), g.timing_report()
+        assert fused == ((C in (16, 24) or (C == 32 and s == 2)) and W % 4 == 0), g.timing_report()
 
 
