@@ -56,6 +56,11 @@ def parse():
                    help="skip the other single-GPU configs (b1, MobileNetV2 b128, BERT b32)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--timing-report", action="store_true")
+    p.add_argument("--host-input", action="store_true",
+                   help="headline with host-resident inputs/outputs (pinned staging, rten_hip/staging.py)")
+    p.add_argument("--cpu-logic-test", action="store_true",
+                   help="tests only: run the launch / sharding / timing / JSON logic with a torch CPU "
+                        "stand-in forward under gloo (no GPU, not a measurement)")
     return p.parse_args()
 
 
@@ -108,9 +113,15 @@ def cpu_baseline(spec, seconds: float, batch: int, feed_fn):
     med = times[len(times) // 2]
     # Per-core rate of the oracle's GEMM micro-kernel at the reference's
     # bench_gemm shapes (src/gemm.rs:1782-1903), one thread.
-    gflops_1t = None
+    gflops_1t = gflops_mt = None
     try:
         gflops_1t = round(rten_oracle.gemm_gflops_1t(1024, 1024, 1024, 0.5), 1)
+        gflops_mt = round(rten_oracle.gemm_gflops(1024, 1024, 1024, 0.5, threads=threads), 1)
+    except Exception:  # noqa: BLE001 -- informative only
+        pass
+    topo = {}
+    try:
+        topo = rten_oracle.cpu_topology()
     except Exception:  # noqa: BLE001 -- informative only
         pass
     cpu_model = "unknown"
@@ -130,12 +141,18 @@ def cpu_baseline(spec, seconds: float, batch: int, feed_fn):
         "logical_cpus": logical,
         "physical_cores": physical,
         "gemm_gflops_per_core": gflops_1t,
+        "gemm_gflops_all_threads": gflops_mt,
+        "topology": topo,
         "sample": f"{spec.name} batch {batch} (the benchmark config), {len(times)} runs in ~{seconds:.0f}s, "
                   f"median {med * 1e3:.1f} ms per batch; restated RTen algorithm (C++ BLIS 6x16 "
                   f"AVX2-FMA with x4 unroll + B prefetch, KC=256, im2col offset tables + masked gathers), "
                   f"not the Rust binary; {threads} threads (RTEN_NUM_THREADS = the box's CPU share; RTen's own "
                   f"rule, num_cpus::get_physical(), would start {physical} on this {logical}-CPU lease); "
-                  f"1-thread GEMM 1024^3: {gflops_1t} GFLOP/s; host: {cpu_model}",
+                  f"GEMM 1024^3: {gflops_1t} GFLOP/s on 1 thread, {gflops_mt} GFLOP/s on {threads} "
+                  f"({(gflops_mt or 0) / max(gflops_1t or 1, 1e-9):.1f}x); the {topo.get('affinity_cpus')} "
+                  f"CPUs of this lease are {topo.get('physical_cores_in_affinity')} physical cores "
+                  f"(SMT {'on' if topo.get('smt_active') else 'off' if topo.get('smt_active') is False else 'unknown'}); "
+                  f"host: {cpu_model}",
     }
 
 
@@ -167,6 +184,31 @@ def traffic_bytes(model, batch):
         return round(sum(v for k, v in by.items() if any(f in k for f in fams))), \
             f"profiles/{os.path.basename(path)} (commit {js.get('commit', 'unrecorded')})"
     return None, None
+
+
+def rocprof_kernel_ms(model, batch):
+    """Dominant-kernel time per forward from the newest committed rocprofv3
+    per-forward summary of this workload (scripts/gpu_evidence.sh ->
+    tools/rocprof_per_forward.py): the sum of the _ROOF_KERNELS families'
+    ms/forward, the commit the summary was taken at, and its path.  None when
+    no summary exists."""
+    import re
+
+    for rnd in ("r5", "r4"):
+        path = os.path.join(ROOT, "profiles", f"{rnd}_rocprof_{model}_b{batch}_per_forward.txt")
+        if not os.path.exists(path):
+            continue
+        commit, ms = None, 0.0
+        for line in open(path):
+            if line.startswith("# commit"):
+                commit = line.split()[2]
+            m = re.match(r"\s+(\S+)\s+([0-9.]+) ms/forward", line)
+            if m and any(f in m.group(1) for f in _ROOF_KERNELS[model]):
+                ms += float(m.group(2))
+        if ms > 0:
+            return {"kernel_ms_per_step": round(ms, 4), "commit": commit,
+                    "source": f"profiles/{os.path.basename(path)}"}
+    return None
 
 
 class Workload:
@@ -210,33 +252,95 @@ class Workload:
         # Rank r holds images [r*B, (r+1)*B) of the world*B job; the only
         # exchange is the all-gather of logits (RCCL) inside runner.run.
         self.runner = BatchShardRunner(forward)
+        self.staging = None
 
     def step(self):
         self.runner.run(self.x, self.world * self.B)
 
-    def timed(self, steps, warmup, dist):
+    def enable_host_input(self):
+        """Host-resident inputs and outputs (the drop-in Model::run case,
+        src/model.rs:580-592): every step uploads this rank's images from
+        pinned host memory and downloads the (gathered) logits, pipelined by
+        rten_hip/staging.py -- step k+1's upload overlaps step k's forward."""
         import torch
 
-        for _ in range(warmup):
-            self.step()
+        from rten_hip.staging import HostStaging
+
+        if self.extra:
+            raise ValueError("host-input mode covers single-input image models")
+        g = self.g
+        outs = [self.out, torch.empty_like(self.out)]
+        total = self.world * self.B
+
+        def fwd(xb, slot):
+            g.run({g.input_ids[0]: xb}, g.output_ids, out=[outs[slot]])
+            return self.runner.gather(outs[slot], total)
+
+        self.staging = HostStaging(fwd, tuple(self.x.shape), self.x.device, slots=2)
+        self.host_in = torch.from_numpy(self.feed_np["input"]).pin_memory()
+        out_shape = (total,) + tuple(self.out.shape[1:])
+        self.host_out = [HostStaging.pinned(out_shape), HostStaging.pinned(out_shape)]
+        self.k_host = 0
+
+    def host_step(self):
+        self.staging.submit(self.host_in, self.host_out[self.k_host % 2])
+        self.k_host += 1
+
+    def sync(self):
+        import torch
+
+        if self.staging is not None:
+            self.staging.synchronize()
         torch.cuda.synchronize()
+
+    def timed(self, steps, warmup, dist, host=False):
+        """Wall time of `steps` steps between barriers: the max over ranks,
+        and every rank's own time (rank order)."""
+        import torch
+
+        step = self.host_step if host else self.step
+        for _ in range(warmup):
+            step()
+        self.sync()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        self.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
-            self.step()
-        torch.cuda.synchronize()
+            step()
+        self.sync()
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize()
+        self.sync()
         elapsed = time.perf_counter() - t0
+        per_rank = [elapsed]
         if dist is not None:
-            t = torch.tensor([elapsed], device=self.x.device if self.backend == "nccl" else "cpu",
-                             dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-        return elapsed
+            dev = self.x.device if self.backend == "nccl" else "cpu"
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            parts = [torch.zeros_like(t) for _ in range(self.world)]
+            dist.all_gather(parts, t)
+            per_rank = [float(p.item()) for p in parts]
+        return max(per_rank), per_rank
+
+    def gather_us(self, reps, dist):
+        """Mean time of the logits all-gather alone (µs, max over ranks);
+        None with one rank."""
+        import torch
+
+        if dist is None:
+            return None
+        total = self.world * self.B
+        self.runner.gather(self.out, total)
+        self.sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.runner.gather(self.out, total)
+        self.sync()
+        us = (time.perf_counter() - t0) / reps * 1e6
+        t = torch.tensor([us], device=self.x.device if self.backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return round(float(t.item()), 1)
 
     def kernel_ms(self, runs):
         """Per-op hipEvent time of the dominant family per step (eager runs of
@@ -284,6 +388,12 @@ class Workload:
         return metric, workload, kernel_desc, data
 
     def roofline(self, kernel_ms_eager, ms_per_step, value):
+        # The eager per-op event pairs bracket each op's launches (the stream
+        # is held until the whole plan is queued, graph.cpp launch_hold, so
+        # host launch pace is not in them, but each pair still spans its
+        # op's dispatch); when their sum exceeds the replayed step the step
+        # time is used instead and the line says so ("capped").
+        capped = kernel_ms_eager > ms_per_step
         kms = min(kernel_ms_eager, ms_per_step)
         _, _, kernel_desc, _ = self.describe()
         gemm_flops = self.flops_per_img * self.B
@@ -291,7 +401,21 @@ class Workload:
         traffic, traffic_src = traffic_bytes(self.model, self.B)
         common = {"traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_desc,
                   "kernel_ms_per_step": round(kms, 4), "kernel_ms_eager_events": round(kernel_ms_eager, 4),
-                  "timing": "per-op hipEvents on the executor stream over eager runs, capped at ms_per_step"}
+                  "capped": capped,
+                  "timing": "per-op hipEvents on the executor stream over eager runs (stream held until the "
+                            "plan is queued), capped at ms_per_step when larger (capped: true)"}
+        rp = rocprof_kernel_ms(self.model, self.B)
+        if rp:
+            head = (_git_head() or "").split()[0]
+            rp["matches_head"] = bool(head and rp["commit"] and (head.startswith(rp["commit"]) or
+                                                                 rp["commit"].startswith(head)))
+            if self.model == "mobilenet_v2":
+                rp["achieved_gbs"] = round(self.io_bytes / (rp["kernel_ms_per_step"] * 1e-3) / 1e9, 1)
+                rp["frac"] = round(rp["achieved_gbs"] / HBM_PEAK_GBPS, 4)
+            else:
+                rp["achieved"] = round(gemm_flops / (rp["kernel_ms_per_step"] * 1e-3) / 1e12, 2)
+                rp["frac"] = round(rp["achieved"] / F32_MFMA_PEAK_TFLOPS, 4)
+            common["rocprof"] = rp
         if self.model == "mobilenet_v2":
             gbs = self.io_bytes / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
             return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -308,9 +432,9 @@ def secondary_entry(ctx, model, B, seq, steps, warmup):
     steps, then K steps between synchronisations (K raised so the timed
     region is >= ~0.15 s for short steps)."""
     w = Workload(ctx, model, B, seq, 0, 1, "nccl")
-    est = w.timed(3, 1, None) / 3
+    est = w.timed(3, 1, None)[0] / 3
     k = max(steps, min(2000, int(0.15 / max(est, 1e-5))))
-    elapsed = w.timed(k, warmup, None)
+    elapsed, _ = w.timed(k, warmup, None)
     ms = elapsed / k * 1e3
     value = B * k / elapsed
     kms, _ = w.kernel_ms(max(1, min(steps, 10)))
@@ -325,13 +449,88 @@ def secondary_entry(ctx, model, B, seq, steps, warmup):
     return ent
 
 
+def host_input_entry(ctx, steps, warmup, headline_ms):
+    """ResNet-50 b64 with host-resident inputs and outputs (pinned staging,
+    rten_hip/staging.py), timed like the headline, with the PCIe copy rates
+    measured in the same run at the staging sizes."""
+    from rten_hip.staging import pcie_rates
+
+    w = Workload(ctx, "resnet50", 64, 128, 0, 1, "nccl")
+    w.enable_host_input()
+    elapsed, _ = w.timed(steps, warmup, None, host=True)
+    ms = elapsed / steps * 1e3
+    pcie = pcie_rates(w.host_in.numel() * 4, w.host_out[0].numel() * 4, w.x.device)
+    ent = {"metric": "images/sec ResNet-50 f32 batch=64, host-resident input and logits",
+           "value": round(64 * steps / elapsed, 2), "unit": "images/s", "ms_per_step": round(ms, 4),
+           "steps": steps, "warmup": warmup, "dtype": "f32",
+           "config": {"workload": "resnet50 f32 batch=64, images in pinned host memory uploaded every step "
+                                  "(38.5 MB H2D on a copy stream, overlapped with the previous step's forward), "
+                                  "logits downloaded every step (256 KB D2H); the drop-in Model::run case "
+                                  "(src/model.rs:580-592)", "model": w.spec.name, "global_batch": 64},
+           "pcie": pcie,
+           "vs_device_resident": round(headline_ms / ms, 4) if headline_ms else None}
+    del w
+    return ent
+
+
+class CpuLogicWorkload:
+    """--cpu-logic-test only: the N>1 launch / shard / timing / JSON logic with
+    a torch CPU stand-in forward (a small conv net) under gloo.  Not a
+    measurement of anything; no GPU and no rten_hip involved."""
+
+    def __init__(self, B, rank, world):
+        import torch
+
+        self.B, self.world, self.backend, self.model = B, world, "gloo", "resnet50"
+        torch.manual_seed(1234 + rank)
+        self.x = torch.rand(B, 3, 32, 32)
+        self.wc = torch.rand(8, 3, 3, 3) - 0.5
+        self.wf = torch.rand(10, 8) - 0.5
+        self.staging = None
+
+        from rten_hip.parallel import BatchShardRunner
+
+        def forward(xb):
+            h = torch.relu(torch.nn.functional.conv2d(xb, self.wc, padding=1))
+            return h.mean(dim=(2, 3)) @ self.wf.t()
+
+        self.out = forward(self.x)
+        self.runner = BatchShardRunner(forward)
+
+    step = Workload.step
+    timed = Workload.timed
+    gather_us = Workload.gather_us
+
+    def sync(self):
+        pass
+
+
+def device_identity(local):
+    """Host name and GPU identity of this rank's device (UUID where torch
+    exposes it), for the one-rank-per-GPU check."""
+    import socket
+
+    import torch
+
+    ident = None
+    try:
+        props = torch.cuda.get_device_properties(local)
+        ident = str(getattr(props, "uuid", "") or "") or f"{getattr(props, 'name', 'gpu')}#{local}"
+    except Exception:  # noqa: BLE001
+        ident = f"gpu#{local}"
+    return f"{socket.gethostname()}/{ident}"
+
+
 def main():
     args = parse()
+    if args.cpu_logic_test:
+        return cpu_logic_main(args)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(args, world)
     dist = None
     backend = os.environ.get("RTENHIP_DIST_BACKEND", "nccl")  # "gloo": one-GPU multi-rank rehearsal
     if world > 1:
@@ -348,16 +547,28 @@ def main():
     else:
         torch.cuda.set_device(0)
 
+    devices = [device_identity(local)]
+    if dist is not None:
+        devices = [None] * world
+        dist.all_gather_object(devices, device_identity(local))
+        if backend == "nccl" and len(set(devices)) != world:
+            raise SystemExit(f"bench.py: ranks share a GPU ({devices}); one rank per GPU is required")
+
     import rten_hip
 
     ctx = rten_hip.Context(torch.cuda.current_device())
     w = Workload(ctx, args.model, args.batch, args.seq, rank, world, backend)
-    elapsed = w.timed(args.steps, args.warmup, dist)
+    if args.host_input:
+        w.enable_host_input()
+    elapsed, per_rank = w.timed(args.steps, args.warmup, dist, host=args.host_input)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * args.batch * args.steps / elapsed
+    gather_us = w.gather_us(max(5, args.steps), dist)
     kms, report = w.kernel_ms(max(1, min(args.steps, 10)))
     roofline = w.roofline(kms, ms_per_step, value)
     metric, workload, _, data = w.describe()
+    if args.host_input:
+        data = data.replace("resident in HBM", "in pinned host memory, uploaded every step")
 
     if rank == 0:
         line = {
@@ -379,15 +590,23 @@ def main():
                        "parallelism": f"batch-shard x{world} (replicated weights, "
                                           f"{'RCCL' if backend == 'nccl' else backend} all-gather of logits)"},
             "roofline": roofline,
+            "ranks": {"ms_per_step": [round(t / args.steps * 1e3, 4) for t in per_rank],
+                      "devices": devices, "allgather_us": gather_us},
             "commit": _git_head(),
         }
-        if world == 1 and not args.no_secondary and args.model == "resnet50" and args.batch == 64:
+        if world == 1 and not args.no_secondary and args.model == "resnet50" and args.batch == 64 \
+                and not args.host_input:
             sec = []
             for model, B in (("resnet50", 1), ("mobilenet_v2", 128), ("bert", 32)):
                 try:
                     sec.append(secondary_entry(ctx, model, B, args.seq, args.steps, args.warmup))
                 except Exception as e:  # noqa: BLE001 -- reported in the line, never hides the headline
                     sec.append({"model": model, "batch": B, "error": f"{type(e).__name__}: {e}"})
+            try:
+                sec.append(host_input_entry(ctx, args.steps, args.warmup, ms_per_step))
+            except Exception as e:  # noqa: BLE001
+                sec.append({"model": "resnet50", "batch": 64, "host_input": True,
+                            "error": f"{type(e).__name__}: {e}"})
             line["secondary"] = sec
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(w.spec, args.cpu_seconds, args.batch, lambda: w.feed_np)
@@ -397,6 +616,50 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def check_world(args, world):
+    """bench.py --gpus N runs as N ranks, one per GPU (the driver launches it
+    under torch.distributed.run); anything else is a launch error."""
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N > 1 as "
+                         f"python -m torch.distributed.run --nproc-per-node {args.gpus} --master-addr 127.0.0.1 "
+                         f"bench.py --gpus {args.gpus}")
+
+
+def cpu_logic_main(args):
+    """--cpu-logic-test: the same world checks, barriers, max-over-ranks
+    timing, per-rank fields and all-gather timing as main(), over gloo with a
+    CPU stand-in forward.  Prints one JSON line marked as a logic test."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    check_world(args, world)
+    d = None
+    if world > 1:
+        dist.init_process_group("gloo")
+        d = dist
+    w = CpuLogicWorkload(args.batch, rank, world)
+    elapsed, per_rank = w.timed(args.steps, args.warmup, d)
+    gather_us = w.gather_us(max(5, args.steps), d)
+    gathered = w.runner.run(w.x, world * args.batch)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "logic test (CPU stand-in forward, gloo): not a measurement",
+            "value": round(world * args.batch * args.steps / elapsed, 2), "unit": "images/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic, CPU stand-in forward",
+            "config": {"workload": "cpu logic test", "global_batch": world * args.batch,
+                       "parallelism": f"batch-shard x{world} (gloo all-gather of logits)"},
+            "ranks": {"ms_per_step": [round(t / args.steps * 1e3, 4) for t in per_rank],
+                      "allgather_us": gather_us},
+            "gathered_shape": list(gathered.shape),
+        }), flush=True)
+    if d is not None:
+        d.barrier()
+        d.destroy_process_group()
 
 
 if __name__ == "__main__":

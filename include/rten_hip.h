@@ -295,10 +295,11 @@ int32_t rtenhip_graph_add_constant_i32(rtenhip_graph* g, const char* name, const
  * Where, shape ops carry int32; the f32 kernels reject int32 inputs with
  * RTENHIP_INCORRECT_INPUT_TYPE).  output_dtypes (may be NULL) receives the
  * outputs' types.  A plan with a Gather on non-constant indices checks its
- * indices on the device (gather.rs:52-60) without a host round trip: an
- * out-of-range index ("Entry in `indices` is out of range", INVALID_VALUE) is
- * reported by rtenhip_graph_synchronize, or by the next run of the same plan
- * (before that run is queued), whichever comes first. */
+ * indices on the device (gather.rs:52-60): by default the run waits for that
+ * check and returns an out-of-range index ("Entry in `indices` is out of
+ * range", INVALID_VALUE) itself, as Model::run does.  With
+ * rtenhip_graph_set_deferred_checks(g, 1) the run is queued without a host
+ * round trip and the error is reported by rtenhip_graph_synchronize only. */
 rtenhip_status rtenhip_graph_run_typed(rtenhip_graph* g, const int32_t* input_ids,
                                        const rtenhip_tensor* inputs, const int32_t* input_dtypes,
                                        int32_t n_inputs, const int32_t* output_ids,
@@ -308,10 +309,16 @@ rtenhip_status rtenhip_graph_plan_typed(rtenhip_graph* g, const int32_t* input_i
                                         int32_t n_inputs, const int32_t* output_ids,
                                         int32_t n_outputs, int64_t* shapes, int32_t* ndims,
                                         int32_t* output_dtypes);
-/* Wait for every queued run of the graph and report a deferred Gather index
- * error (see rtenhip_graph_run_typed).  Stands in for the point where RTen's
+/* Wait for every queued run of the graph and report the deferred Gather index
+ * error of the earliest run that had one (see rtenhip_graph_run_typed); the
+ * error is cleared once reported.  Stands in for the point where RTen's
  * synchronous Model::run returns (src/model.rs:580-592). */
 rtenhip_status rtenhip_graph_synchronize(rtenhip_graph* g);
+/* enabled = 1: Gather index checks of later runs are deferred to
+ * rtenhip_graph_synchronize (runs queue back to back); 0 (default): every run
+ * returns its own index error (gather.rs:52-60).  No counterpart in RTen, whose
+ * Model::run is synchronous. */
+rtenhip_status rtenhip_graph_set_deferred_checks(rtenhip_graph* g, int enabled);
 /* Output shape of a value after the last run (or -1). */
 int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape);
 /* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled. */

@@ -123,10 +123,44 @@ def gemm_gflops_1t(m: int, n: int, k: int, seconds: float = 0.5) -> float:
     """Single-thread GFLOP/s of gemm() at one of the reference's bench_gemm
     shapes (src/gemm.rs:1782-1903 times m = n = k square products): best of
     the runs made within `seconds`.  The thread count is restored after."""
+    return gemm_gflops(m, n, k, seconds, threads=1)
+
+
+def cpu_topology() -> dict:
+    """What the CPUs this process may run on are (sched_getaffinity, sysfs):
+    logical CPUs, the distinct physical cores and packages under them, and
+    whether SMT is on -- so a thread count can be read as cores or
+    hyperthreads."""
+    import os
+
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    cores, pkgs = set(), set()
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+        try:
+            core = open(base + "core_id").read().strip()
+            pkg = open(base + "physical_package_id").read().strip()
+        except OSError:
+            core, pkg = str(c), "0"
+        cores.add((pkg, core))
+        pkgs.add(pkg)
+    smt = None
+    try:
+        smt = open("/sys/devices/system/cpu/smt/active").read().strip() == "1"
+    except OSError:
+        pass
+    return {"affinity_cpus": len(cpus), "physical_cores_in_affinity": len(cores), "packages": len(pkgs),
+            "smt_active": smt}
+
+
+def gemm_gflops(m: int, n: int, k: int, seconds: float = 0.5, threads: int = 1) -> float:
+    """GFLOP/s of gemm() on `threads` threads (the pool the reference's
+    GEMM parallelises its column blocks over, src/gemm.rs:733-930); best of
+    the runs made within `seconds`.  The thread count is restored after."""
     import time
 
     prev = num_threads()
-    set_num_threads(1)
+    set_num_threads(int(threads))
     try:
         a = ((xorshift(11, m * k) - 0.5).reshape(m, k))
         b = ((xorshift(12, k * n) - 0.5).reshape(k, n))

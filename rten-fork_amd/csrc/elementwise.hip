@@ -322,6 +322,27 @@ rtenhip_status launch_fill(void* y, int64_t n, uint32_t bits, hipStream_t s) {
   return RTENHIP_OK;
 }
 
+// Timing runs only (Graph::run with timing on): one wave that holds the
+// stream until the host has queued the whole eager plan, so the per-op event
+// pairs time the kernels back to back instead of the host's launch pace.  It
+// polls a word of pinned, uncached host memory the host sets after queueing
+// (a load over PCIe each time, so never stale) and gives up after max_ticks
+// of s_memrealtime (100 MHz) whatever happens: it cannot hang the queue.
+__global__ void hold_kernel(const volatile int* release, uint64_t max_ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < max_ticks) {
+    if (__hip_atomic_load(const_cast<const int*>(release), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+    __builtin_amdgcn_s_sleep(64);
+  }
+}
+
+rtenhip_status launch_hold(const int* release, double max_ms, hipStream_t s) {
+  const uint64_t ticks = (uint64_t)(max_ms * 1e5);  // s_memrealtime runs at 100 MHz
+  hipLaunchKernelGGL(hold_kernel, dim3(1), dim3(64), 0, s, release, ticks);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 // col2im (src/ops/conv.rs:329-375), one thread per output element: the
 // reference fills the plane with the bias and adds each (ky, kx) column image
 // in turn, so an output receives bias + its columns in (ky, kx) order.

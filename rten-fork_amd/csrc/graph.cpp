@@ -67,6 +67,7 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 }
 
 Plan::~Plan() {
+  drop_captures();
   if (gather_flag) (void)hipFree(gather_flag);
   for (auto& c : gchk) {
     if (c.ev) {
@@ -148,8 +149,11 @@ static ConvAttrs conv_attrs(const Node& n, bool one_d) {
 }
 
 Graph::~Graph() {
-  for (auto& pl : plans)
-    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  for (auto& pl : plans) pl->drop_captures();
+  if (hold_word) {
+    if (exec_stream) (void)hipStreamSynchronize(exec_stream);
+    (void)hipHostFree(hold_word);
+  }
   for (auto& n : nodes) {
     if (n.kind == NodeKind::Constant && n.dev && n.owns_dev) (void)hipFree(n.dev);
     if (n.bn_dev) (void)hipFree(n.bn_dev);
@@ -171,8 +175,7 @@ int Graph::add_node(Node n) {
   if (!n.name.empty()) by_name[n.name] = id;
   nodes.push_back(std::move(n));
   // Any structural change invalidates cached plans.
-  for (auto& pl : plans)
-    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  for (auto& pl : plans) pl->drop_captures();
   plans.clear();
   return id;
 }
@@ -2767,10 +2770,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   {
     rtenhip_status st = find_plan(in_ids, ins, n_in, in_dt, out_ids, n_out, &plan);
     if (st) return st;
-    // An index error an earlier run recorded and nobody has read yet is
-    // reported now, before this run is queued.
-    if (plan->gather_flag && (st = collect_gather_checks(*plan, false))) return st;
   }
+  const uint64_t this_run = ++run_seq;
   std::vector<int> ov(out_ids, out_ids + n_out);
   // Check the caller's output buffers (RunError::OutputMismatch).
   for (int i = 0; i < n_out; i++) {
@@ -2789,11 +2790,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   if (plan->arena_bytes > arena_cap) {
     RTENHIP_HIP_CHECK(hipStreamSynchronize(caller));
     RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
-    for (auto& pl : plans)
-      if (pl->exec) {
-        (void)hipGraphExecDestroy(pl->exec);
-        pl->exec = nullptr;
-      }
+    for (auto& pl : plans) pl->drop_captures();
     if (arena) RTENHIP_HIP_CHECK(hipFree(arena));
     arena = nullptr;
     RTENHIP_HIP_CHECK(hipMalloc(&arena, plan->arena_bytes));
@@ -2819,8 +2816,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   std::vector<float*> bin, bout;
   for (int i = 0; i < n_in; i++) bin.push_back(ins[i].data);
   for (int i = 0; i < n_out; i++) bout.push_back(outs[i].data);
-  bool same_binding = plan->exec && bin == plan->bound_in && bout == plan->bound_out &&
-                      plan->scratch_gen == ctx->scratch_gen;
+  Plan::Capture* cap = nullptr;
+  for (auto& c : plan->captures)
+    if (c.exec && c.in == bin && c.out == bout && c.scratch_gen == ctx->scratch_gen) cap = &c;
   plan->bound_in = bin;
   plan->bound_out = bout;
 
@@ -2851,11 +2849,21 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
   plan->pk_ready.clear();
   if (replay) {
-    if (!same_binding) {
-      if (plan->exec) {
-        (void)hipGraphExecDestroy(plan->exec);
-        plan->exec = nullptr;
+    if (!cap) {
+      // A new binding: capture into a free slot, or replace the least
+      // recently used capture (or a stale one of an older scratch generation).
+      if ((int)plan->captures.size() < Plan::kMaxCaptures) {
+        plan->captures.emplace_back();
+        cap = &plan->captures.back();
+      } else {
+        cap = &plan->captures[0];
+        for (auto& c : plan->captures)
+          if (c.scratch_gen != ctx->scratch_gen || c.last_use < cap->last_use) cap = &c;
+        if (cap->exec) (void)hipGraphExecDestroy(cap->exec);
+        *cap = Plan::Capture{};
       }
+      cap->in = bin;
+      cap->out = bout;
       hipGraph_t g = nullptr;
       hipError_t e = hipStreamBeginCapture(exec_stream, hipStreamCaptureModeThreadLocal);
       if (e == hipSuccess) {
@@ -2864,22 +2872,34 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (!st) st = copy_static_outputs();
         ctx->stream = exec_stream;
         hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
-        if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&plan->exec, g, nullptr, nullptr, 0);
-        plan->scratch_gen = ctx->scratch_gen;
+        if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&cap->exec, g, nullptr, nullptr, 0);
+        cap->scratch_gen = ctx->scratch_gen;
         if (g) (void)hipGraphDestroy(g);
         if (!st && e2 != hipSuccess) st = hip_fail(e2, "hipGraph capture");
       } else {
         st = hip_fail(e, "hipStreamBeginCapture");
       }
     }
+    if (!st && !cap->exec) st = fail(RTENHIP_HIP_ERROR, "hipGraph capture produced no executable graph");
     if (!st) {
-      hipError_t e = hipGraphLaunch(plan->exec, exec_stream);
+      cap->last_use = this_run;
+      hipError_t e = hipGraphLaunch(cap->exec, exec_stream);
       if (e != hipSuccess) st = hip_fail(e, "hipGraphLaunch");
     }
   } else {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
     ctx->scratch_log = &plan->scratch_need;
+    // Timing run of a tuned plan: hold the stream until every op is queued,
+    // so the event pairs measure the kernels, not the host's launch rate.
+    // (Not on the plan's first run: its tuner synchronizes inside the ops.)
+    const bool hold = timing && plan->eager_runs >= 1;
+    if (hold) {
+      if (!hold_word) RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hold_word), sizeof(int), hipHostMallocCoherent));
+      __atomic_store_n(hold_word, 0, __ATOMIC_SEQ_CST);
+      st = launch_hold(hold_word, 100.0, exec_stream);
+    }
     for (int op : plan->ops) {
+      if (st) break;
       hipEvent_t a = nullptr, b = nullptr;
       // (a downsample computed by its conv3's dual GEMM launches nothing: no events)
       const bool timed = timing && !plan->dual_skip.count(op);
@@ -2899,6 +2919,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         break;
       }
     }
+    if (hold) __atomic_store_n(hold_word, 1, __ATOMIC_SEQ_CST);  // release the queued plan
     ctx->scratch_log = nullptr;
     ctx->stream = exec_stream;
     if (!st) st = copy_static_outputs();
@@ -3001,18 +3022,15 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   }
   ctx->stream = caller;
   if (plan->gather_flag) {
-    // Gather's index check (gather.rs:52-60), without a host round trip: the
-    // flag the kernels set on an out-of-range index goes to a pinned word of
-    // the check ring and is cleared whatever the run's status; an event marks
-    // the copy.  A later run or synchronize() reads it (collect_gather_checks).
+    // Gather's index check (gather.rs:52-60): the flag the kernels set on an
+    // out-of-range index goes to a pinned word of a check slot and is cleared
+    // whatever the run's status; an event marks the copy.
     Plan::GatherCheck& c = plan->gchk[plan->gchk_next];
     if (c.pending) {
-      // The ring is full: this slot's run must have finished before reuse.
-      rtenhip_status cs = RTENHIP_OK;
-      if (hipEventSynchronize(c.ev) != hipSuccess) cs = fail(RTENHIP_HIP_ERROR, "gather check event");
-      else if (*c.host) cs = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
-      c.pending = false;
-      if (!st) st = cs;
+      // (deferred mode) The ring is full: the slot's run must have finished
+      // before reuse; its error is kept for synchronize(), not given to this run.
+      rtenhip_status cs = collect_gather_checks(*plan, true);
+      if (!st) st = cs;  // a HIP error only
     }
     if (!c.host) {
       RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.host), sizeof(int), hipHostMallocDefault));
@@ -3024,8 +3042,16 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     const hipError_t e2 = hipEventRecord(c.ev, exec_stream);
     if (e0 != hipSuccess || e1 != hipSuccess || e2 != hipSuccess) {
       if (!st) st = hip_fail(e0 != hipSuccess ? e0 : e1 != hipSuccess ? e1 : e2, "gather flag");
+    } else if (!deferred_checks) {
+      // The reference's behaviour: this run returns its own index error.
+      if (hipEventSynchronize(c.ev) != hipSuccess) {
+        if (!st) st = fail(RTENHIP_HIP_ERROR, "gather check event");
+      } else if (*c.host && !st) {
+        st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+      }
     } else {
       c.pending = true;
+      c.run = this_run;
       plan->gchk_next = (plan->gchk_next + 1) % Plan::kGatherChecks;
     }
   }
@@ -3036,7 +3062,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
 
 rtenhip_status Graph::collect_gather_checks(Plan& p, bool wait) {
   rtenhip_status st = RTENHIP_OK;
-  // Oldest first, so the error reported is the earliest run's.
   for (int i = 0; i < Plan::kGatherChecks; i++) {
     Plan::GatherCheck& c = p.gchk[(p.gchk_next + i) % Plan::kGatherChecks];
     if (!c.pending) continue;
@@ -3045,8 +3070,8 @@ rtenhip_status Graph::collect_gather_checks(Plan& p, bool wait) {
     c.pending = false;
     if (e != hipSuccess) {
       if (!st) st = hip_fail(e, "gather check event");
-    } else if (*c.host && !st) {
-      st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+    } else if (*c.host && (deferred_error_run == 0 || c.run < deferred_error_run)) {
+      deferred_error_run = c.run;  // the earliest failing run is the one reported
     }
   }
   return st;
@@ -3060,6 +3085,10 @@ rtenhip_status Graph::synchronize() {
       const rtenhip_status s2 = collect_gather_checks(*pl, true);
       if (!st) st = s2;
     }
+  if (deferred_error_run) {
+    deferred_error_run = 0;
+    if (!st) st = fail(RTENHIP_INVALID_VALUE, "Entry in `indices` is out of range");
+  }
   return st;
 }
 
@@ -3436,8 +3465,7 @@ rtenhip_status Graph::optimize() {
       }
     }
   }
-  for (auto& pl : plans)
-    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  for (auto& pl : plans) pl->drop_captures();
   plans.clear();
   (void)fused;
   return RTENHIP_OK;
@@ -3625,6 +3653,21 @@ int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape) 
 }
 
 rtenhip_status rtenhip_graph_synchronize(rtenhip_graph* g) { return G_(g)->synchronize(); }
+
+rtenhip_status rtenhip_graph_set_deferred_checks(rtenhip_graph* g, int enabled) {
+  Graph* gr = G_(g);
+  if (!enabled && gr->deferred_checks) {
+    // Leaving deferred mode: settle the queued checks first, so none is lost
+    // (their error stays for synchronize()).
+    for (auto& pl : gr->plans)
+      if (pl->gather_flag) {
+        const rtenhip_status st = gr->collect_gather_checks(*pl, true);
+        if (st) return st;
+      }
+  }
+  gr->deferred_checks = enabled != 0;
+  return RTENHIP_OK;
+}
 
 rtenhip_status rtenhip_graph_set_timing(rtenhip_graph* g, int enabled) {
   G_(g)->timing = enabled != 0;

@@ -259,22 +259,41 @@ struct Plan {
   std::map<int, float*> host_dev;
   // Gathers with non-constant indices record an out-of-range index here
   // (graph-capturable: no sync inside the ops).  The end of each run copies
-  // the flag into a pinned host word, clears it and records an event, all
-  // asynchronously (a ring of kGatherChecks, so several runs can be queued);
-  // the check is read at the start of a later run of the plan or by
-  // Graph::synchronize (rtenhip_graph_synchronize).
+  // the flag into a pinned host word of a check slot, clears it and records
+  // an event.  By default the run then waits for that event and returns the
+  // error itself, as the reference's Model::run does (gather.rs:52-60).
+  // With Graph::deferred_checks the slots form a ring of kGatherChecks, so
+  // several runs can be queued; each slot carries its run's sequence number
+  // and its error is reported only by Graph::synchronize
+  // (rtenhip_graph_synchronize), never by a later, unrelated run.
   int* gather_flag = nullptr;
   static constexpr int kGatherChecks = 4;
   struct GatherCheck {
     int* host = nullptr;       // pinned
     hipEvent_t ev = nullptr;
     bool pending = false;
+    uint64_t run = 0;          // Graph::run_seq of the run that queued it
   } gchk[kGatherChecks];
   int gchk_next = 0;
-  // hipGraph replay state: valid for these exact input/output pointers.
-  hipGraphExec_t exec = nullptr;
-  std::vector<float*> bound_in, bound_out;
-  uint64_t scratch_gen = 0;                // Ctx::scratch_gen when exec was captured
+  // hipGraph replay state: each capture is valid for its exact input / output
+  // pointers (and the ctx scratch generation it baked in).  Up to
+  // kMaxCaptures bindings are kept (least recently used replaced), so a
+  // caller that alternates between staging buffers (double-buffered host
+  // input, rten_hip/staging.py) replays without re-capturing.
+  struct Capture {
+    hipGraphExec_t exec = nullptr;
+    std::vector<float*> in, out;
+    uint64_t scratch_gen = 0;   // Ctx::scratch_gen when captured
+    uint64_t last_use = 0;      // Graph::run_seq
+  };
+  static constexpr int kMaxCaptures = 4;
+  std::vector<Capture> captures;
+  void drop_captures() {
+    for (auto& c : captures)
+      if (c.exec) (void)hipGraphExecDestroy(c.exec);
+    captures.clear();
+  }
+  std::vector<float*> bound_in, bound_out;  // this run's binding (ptr_of)
   std::map<size_t, size_t> scratch_need;   // ctx scratch slot -> floats (eager runs)
   int eager_runs = 0;
 };
@@ -298,7 +317,14 @@ struct Graph {
   hipStream_t exec_stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
+  int* hold_word = nullptr;  // pinned coherent host word releasing launch_hold (timing runs)
   bool use_hip_graph = true;
+  // Gather index checks (Plan::gchk): false = each run waits for its own
+  // check and returns its error; true = checks are queued and reported by
+  // synchronize() only (rtenhip_graph_set_deferred_checks).
+  bool deferred_checks = false;
+  uint64_t run_seq = 0;             // runs started
+  uint64_t deferred_error_run = 0;  // earliest run with an unreported index error (0: none)
   bool autotune = true;  // time DMA conv configurations on a plan's first run
   int persist_mode = -1; // DMA GEMM launches: -1 tuned, 0 never persistent, k: always, k blocks/CU
   int lat_mode = -1;     // latency GEMM convs (gemm_lat.hip): -1 tuned, 0 never, v > 0 forced variant
@@ -316,7 +342,8 @@ struct Graph {
   // Waits for the queued runs and reports a Gather index error any of them
   // recorded (see Plan::gchk).
   rtenhip_status synchronize();
-  // Reads the completed Gather checks of p (all pending ones when wait).
+  // Reads the completed Gather checks of p (all pending ones when wait) into
+  // deferred_error_run.
   rtenhip_status collect_gather_checks(Plan& p, bool wait);
   // RTen's own passes (src/optimize.rs:286-518, graph_optimize.cpp), run
   // first by optimize(): constant propagation, Silu / Gelu / LayerNorm fusion.

@@ -233,8 +233,7 @@ rtenhip_status Graph::propagate_constants() {
     }
   }
   for (int op : evaluable_ops) nodes[op].removed = true;
-  for (auto& pl : plans)
-    if (pl->exec) (void)hipGraphExecDestroy(pl->exec);
+  for (auto& pl : plans) pl->drop_captures();
   plans.clear();
   return RTENHIP_OK;
 }

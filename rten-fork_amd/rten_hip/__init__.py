@@ -82,6 +82,7 @@ def lib():
                 L.rtenhip_graph_timing_report.restype = C.c_char_p
                 L.rtenhip_graph_timing_report.argtypes = [C.c_void_p]
                 L.rtenhip_graph_synchronize.argtypes = [C.c_void_p]
+                L.rtenhip_graph_set_deferred_checks.argtypes = [C.c_void_p, C.c_int]
             L.rtenhip_last_error_code.restype = C.c_int32
             L.rtenhip_model_load.restype = C.c_void_p
             L.rtenhip_model_load.argtypes = [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t]
@@ -121,7 +122,7 @@ EXPORTED_SYMBOLS = [
     "rtenhip_cast_i32_to_f32", "rtenhip_graph_add_constant_i32", "rtenhip_graph_run_typed",
     "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts", "rtenhip_reduce_mean_f32",
     "rtenhip_graph_describe", "rtenhip_log_softmax_f32", "rtenhip_instance_norm_f32",
-    "rtenhip_graph_synchronize",
+    "rtenhip_graph_synchronize", "rtenhip_graph_set_deferred_checks",
 ]
 
 # rtenhip_dtype (sg::DataType order, include/rten_hip.h)

@@ -168,15 +168,24 @@ class Graph:
         return [s for s, _ in self.output_info(inputs, outputs)]
 
     def synchronize(self):
-        """Wait for the queued runs; raises the deferred Gather index error
-        ("Entry in `indices` is out of range") a run recorded."""
+        """Wait for the queued runs; raises the Gather index error
+        ("Entry in `indices` is out of range") of the earliest deferred run
+        that recorded one (see set_deferred_checks)."""
         check(lib().rtenhip_graph_synchronize(C.c_void_p(self.ptr)))
+
+    def set_deferred_checks(self, enabled: bool):
+        """False (default): a run whose Gather indices are out of range raises
+        from that run, like Model::run (gather.rs:52-60); the run waits for its
+        own check.  True: runs queue without a host round trip and the error is
+        raised by synchronize() only -- never by a later run."""
+        check(lib().rtenhip_graph_set_deferred_checks(C.c_void_p(self.ptr), C.c_int(int(enabled))))
 
     def run(self, inputs: Dict[int, object], outputs: Sequence[int], out=None):
         """Graph::run: inputs {value id: float32 or int32 device tensor};
         returns device tensors (int32 where the graph's value is int32).
-        Queued on the device without a host round trip: a Gather index error
-        is raised by synchronize() or by the next run of the same plan."""
+        A plan with a Gather on non-constant indices checks them on the device
+        and raises their error from this run (set_deferred_checks changes
+        that)."""
         torch = _torch()
         self.ctx.sync_stream()
         in_ids = list(inputs.keys())

@@ -53,7 +53,11 @@ class BatchShardRunner:
     def run(self, full_batch_local_view, total: int):
         """full_batch_local_view: this rank's slice of the inputs (already
         resident on its device).  Returns the gathered [total, ...] output."""
-        out = self.fn(full_batch_local_view)
+        return self.gather(self.fn(full_batch_local_view), total)
+
+    def gather(self, out, total: int):
+        """All-gather this rank's output slice in rank order (identity with
+        one rank)."""
         if self.dist is None:
             return out
         if out.is_cuda and self.dist.get_backend(self.group) == "gloo":

@@ -17,7 +17,11 @@ python3 - "$O/bench.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print("head", d["metric"], d["value"], d["ms_per_step"], d["roofline"]["frac"])
+r = d["roofline"]; print("   roofline capped", r.get("capped"), "eager", r.get("kernel_ms_eager_events"), "rocprof", r.get("rocprof"))
 for s in d.get("secondary", []):
-    print("  ", s.get("metric", s), s.get("value"), s.get("ms_per_step"), (s.get("roofline") or {}).get("frac"), s.get("error", ""))
-if "cpu_baseline" in d: print("  cpu", d["cpu_baseline"]["value"], d["cpu_baseline"].get("gemm_gflops_per_core"))
+    print("  ", s.get("metric", s), s.get("value"), s.get("ms_per_step"), (s.get("roofline") or {}).get("frac"),
+          (s.get("roofline") or {}).get("capped"), (s.get("roofline") or {}).get("kernel_ms_eager_events"),
+          s.get("pcie", ""), s.get("vs_device_resident", ""), s.get("error", ""))
+if "cpu_baseline" in d: print("  cpu", d["cpu_baseline"]["value"], d["cpu_baseline"].get("gemm_gflops_per_core"),
+                              d["cpu_baseline"].get("gemm_gflops_all_threads"), d["cpu_baseline"].get("topology"))
 PY

@@ -224,10 +224,10 @@ def _gather_graph(width=3):
 @pytest.mark.parametrize("width", [3, 8])  # 8: the float4 row-gather path (embeddings)
 def test_graph_gather_index_error_and_types(rh, width):
     """Gather in the captured plan reports an out-of-range index with the
-    reference's error (gather.rs:52-60) without a host round trip per run:
-    at synchronize(), or at the next run of the plan (before it is queued);
-    later valid runs succeed; negative indices count from the end; Cast of an
-    int32 value; int32 data into an f32-only operator is IncorrectInputType."""
+    reference's error (gather.rs:52-60) from the run that had it (eager,
+    captured and replayed runs); the next valid run succeeds; negative indices
+    count from the end; Cast of an int32 value; int32 data into an f32-only
+    operator is IncorrectInputType."""
     import torch
     from rten_hip import OpError
     from rten_hip.graph import ModelSpec
@@ -238,20 +238,15 @@ def test_graph_gather_index_error_and_types(rh, width):
     table = np.arange(4 * width, dtype=np.float32).reshape(4, width)
     exp = table[np.array([[0, 3], [3, 2]])]
     outs = None
-    # eager, capture, replays; "bad+next": the error surfaces at the next run
-    for feed in (good, good, good, "bad", good, "bad+next", good, good):
+    # eager (bad first), capture, replays
+    for feed in ("bad", good, good, good, "bad", good, "bad", "bad", good):
         if isinstance(feed, str):
-            g.run({g.input_ids[0]: bad}, g.output_ids, out=outs)
             with pytest.raises(OpError, match="Entry in `indices` is out of range") as e:
-                if feed == "bad":
-                    g.synchronize()
-                else:
-                    torch.cuda.synchronize()
-                    g.run({g.input_ids[0]: good}, g.output_ids, out=outs)
+                g.run({g.input_ids[0]: bad}, g.output_ids, out=outs)
             assert e.value.kind == "InvalidValue"
+            g.synchronize()  # nothing left to report
             continue
         outs = g.run({g.input_ids[0]: feed}, g.output_ids, out=outs)
-        g.synchronize()
         torch.cuda.synchronize()
         assert _bits_equal(outs[0].cpu().numpy(), exp)
         assert outs[1].dtype == torch.float32
@@ -265,6 +260,46 @@ def test_graph_gather_index_error_and_types(rh, width):
     with pytest.raises(OpError) as e:
         g2.run({g2.input_ids[0]: good}, g2.output_ids)
     assert e.value.kind == "IncorrectInputType"
+
+
+@pytest.mark.parametrize("width", [3, 8])
+def test_graph_gather_deferred_checks(rh, width):
+    """rtenhip_graph_set_deferred_checks: runs queue without a host round trip;
+    an index error is raised by synchronize() only (the earliest failing run's),
+    never by a later run -- also when more runs than the check ring holds (4)
+    follow the bad one, and when the later runs' own indices are valid."""
+    import torch
+    from rten_hip import OpError
+
+    g = _gather_graph(width).to_graph()
+    good = torch.tensor([[0, 3], [-1, 2]], dtype=torch.int32).cuda()
+    bad = torch.tensor([[0, 4], [1, 2]], dtype=torch.int32).cuda()
+    table = np.arange(4 * width, dtype=np.float32).reshape(4, width)
+    exp = table[np.array([[0, 3], [3, 2]])]
+    outs = g.run({g.input_ids[0]: good}, g.output_ids)  # eager, synchronous
+    g.set_deferred_checks(True)
+    for n_after in (0, 1, 6):
+        g.run({g.input_ids[0]: bad}, g.output_ids, out=outs)  # no raise
+        for _ in range(n_after):
+            outs = g.run({g.input_ids[0]: good}, g.output_ids, out=outs)  # no raise
+        with pytest.raises(OpError, match="Entry in `indices` is out of range") as e:
+            g.synchronize()
+        assert e.value.kind == "InvalidValue"
+        g.synchronize()  # reported once
+        outs = g.run({g.input_ids[0]: good}, g.output_ids, out=outs)
+        g.synchronize()
+        torch.cuda.synchronize()
+        assert _bits_equal(outs[0].cpu().numpy(), exp)
+    # back to synchronous checks: a pending deferred error is kept for synchronize()
+    g.run({g.input_ids[0]: bad}, g.output_ids, out=outs)
+    g.set_deferred_checks(False)
+    with pytest.raises(OpError, match="out of range"):
+        g.synchronize()
+    with pytest.raises(OpError, match="out of range"):
+        g.run({g.input_ids[0]: bad}, g.output_ids, out=outs)
+    outs = g.run({g.input_ids[0]: good}, g.output_ids, out=outs)
+    torch.cuda.synchronize()
+    assert _bits_equal(outs[0].cpu().numpy(), exp)
 
 
 def test_bert_base_seq128_bitexact(rh):

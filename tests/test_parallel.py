@@ -113,3 +113,40 @@ def test_gloo_world2_matches_single_process(total):
         assert p.exitcode == 0
     assert got.shape == expect.shape
     assert (got.view(np.uint32) == np.ascontiguousarray(expect).view(np.uint32)).all()
+
+
+def _bench_cmd(world, extra=()):
+    port = _free_port()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+            "--steps", "3", "--warmup", "1", "--batch", "5", "--cpu-logic-test", *extra]
+
+
+def test_bench_world2_launch_logic_gloo():
+    """bench.py as the driver launches it for N > 1 (torch.distributed.run, one
+    process per rank), with the CPU stand-in forward over gloo: one JSON line
+    from rank 0 with n_gpus = world, per-rank step times, the all-gather time,
+    and the gathered [world * B, ...] logits."""
+    import json
+    import subprocess
+
+    r = subprocess.run(_bench_cmd(2, ("--gpus", "2")), capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["config"]["global_batch"] == 10
+    assert len(js["ranks"]["ms_per_step"]) == 2
+    assert js["ms_per_step"] == max(js["ranks"]["ms_per_step"])
+    assert js["ranks"]["allgather_us"] > 0
+    assert js["gathered_shape"] == [10, 10]
+
+
+def test_bench_rejects_world_mismatch():
+    """--gpus must equal the launched WORLD_SIZE (a driver misconfiguration
+    must fail loudly, not print a line for the wrong N)."""
+    import subprocess
+
+    r = subprocess.run(_bench_cmd(2, ("--gpus", "4")), capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr + r.stdout
