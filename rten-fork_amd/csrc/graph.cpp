@@ -68,6 +68,7 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 
 Plan::~Plan() {
   drop_captures();
+  for (auto& c : chains) c.release();
   if (gather_flag) (void)hipFree(gather_flag);
   for (auto& c : gchk) {
     if (c.ev) {
@@ -1411,6 +1412,10 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     if (to == RTENHIP_DTYPE_INT32)
       return rtenhip_cast_f32_to_i32(c, &x, reinterpret_cast<rtenhip_tensor_i32*>(&y));
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
+  }
+  if (t == "Conv" && p.chain_of.count(op_id)) {
+    Plan::ConvChain& c = p.chains[p.chain_of[op_id]];
+    return c.ops[0] == op_id ? exec_chain(p, c) : RTENHIP_OK;  // members run inside the chain's launch
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv" && p.block_fused.count(op_id)) return exec_mbconv_block(p, op_id);
@@ -2796,6 +2801,24 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     RTENHIP_HIP_CHECK(hipMalloc(&arena, plan->arena_bytes));
     arena_cap = plan->arena_bytes;
   }
+  // Conv chains are built once the plan's convs are tuned (after its first,
+  // eager run), outside any capture; rebuilt when the arena moved.
+  if (plan->eager_runs >= 1 && chain_mode != 0 && (!plan->chains_built || plan->chains_arena != arena)) {
+    RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
+    for (auto& c : plan->chains) c.release();
+    plan->chains.clear();
+    plan->chain_of.clear();
+    plan->drop_captures();
+    hipStream_t saved = ctx->stream;
+    ctx->stream = exec_stream;
+    plan->bound_in.assign(ins ? n_in : 0, nullptr);
+    for (int i = 0; i < n_in; i++) plan->bound_in[i] = ins[i].data;
+    plan->bound_out.assign(n_out, nullptr);
+    for (int i = 0; i < n_out; i++) plan->bound_out[i] = outs[i].data;
+    rtenhip_status cst = build_chains(*plan);
+    ctx->stream = saved;
+    if (cst) return cst;
+  }
   const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
   if (replay) {
     // The ctx scratch buffers a capture bakes in must not move afterwards:
@@ -2943,6 +2966,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
+        if (plan->chain_of.count(plan->ops[i]))
+          key = plan->chains[plan->chain_of[plan->ops[i]]].ops[0] == plan->ops[i] ? "Conv(chain)" : "Conv(in_chain)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -2980,7 +3005,16 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         // GEMM shape and the tuned DMA configuration of GEMM-backed ops.
         auto ce = plan->convs.find(plan->ops[i]);
         auto du = plan->dual_on.find(plan->ops[i]);
-        if (plan->dual_skip.count(plan->ops[i])) {
+        if (plan->chain_of.count(plan->ops[i])) {
+          const Plan::ConvChain& ch = plan->chains[plan->chain_of[plan->ops[i]]];
+          if (ch.ops[0] == plan->ops[i]) {
+            snprintf(buf, sizeof buf, "  chain of %zu convs, %d phases, grid %d (built: chain %.4f ms vs %.4f ms one by one)",
+                     ch.ops.size(), ch.n_phases, ch.grid, ch.chain_ms, ch.ops_ms);
+            os << buf;
+          } else {
+            os << "  (in its chain's launch)";
+          }
+        } else if (plan->dual_skip.count(plan->ops[i])) {
           os << "  (in its conv3's dual GEMM)";
         } else if (du != plan->dual_on.end()) {
           // FLOPs of both convs of the pair.
@@ -3489,6 +3523,7 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   if (const char* s = getenv("RTENHIP_LAT")) g->lat_mode = atoi(s);
+  if (const char* s = getenv("RTENHIP_CHAIN")) g->chain_mode = atoi(s);
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 
