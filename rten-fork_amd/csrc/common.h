@@ -167,17 +167,6 @@ rtenhip_status launch_copy_view(const float* src, const int64_t* shape, const in
 rtenhip_status launch_fill(void* y, int64_t n, uint32_t bits, hipStream_t s);
 // Fused 1x1 expand (+bias, act) -> 3x3 depthwise (+bias, act) (mbconv.hip).
 bool expand_dw_eligible(int cin, int H, int W, int S, int pt, int pl, int pb, int pr);
-// MobileNetV2 inverted residual block in one kernel (mbconv_block.hip).
-bool mbconv_block_eligible(int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl, int pb,
-                           int pr, bool expand);
-int mbconv_block_pack_floats(int cin, int hid, int cout);
-void mbconv_block_pack(const float* we, const float* be, const float* wd, const float* bd, const float* wp,
-                       const float* bp, int cin, int hid, int cout, float* out);
-rtenhip_status launch_mbconv_block(const float* x, const float* pk, const float* res, bool res_is_x, float* y, int N,
-                                   int cin, int hid, int cout, int H, int W, int OH, int OW, int S, int pt, int pl,
-                                   int act_e, float lo_e, float hi_e, int act_d, float lo_d, float hi_d, int act_p,
-                                   float lo_p, float hi_p, bool has_be, bool has_bd, bool has_bp, bool expand,
-                                   hipStream_t s);
 rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be, const float* wd, const float* bd,
                                 float* y, int N, int cin, int hidden, int H, int W, int OH, int OW, int S, int pt,
                                 int pl, int act_e, float lo_e, float hi_e, int act_d, float lo_d, float hi_d,

@@ -164,8 +164,6 @@ Graph::~Graph() {
     if (kv.second.first) (void)hipFree(kv.second.first);
     if (kv.second.second) (void)hipFree(kv.second.second);
   }
-  for (auto& kv : mb_pack)
-    if (kv.second) (void)hipFree(kv.second);
   if (exec_stream) (void)hipStreamDestroy(exec_stream);
   if (ev_in) (void)hipEventDestroy(ev_in);
   if (ev_out) (void)hipEventDestroy(ev_out);
@@ -782,8 +780,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (nodes[op].fused_residual >= 0) uses[nodes[op].fused_residual]++;
     auto ef = p.expand_fused.find(op);
     if (ef != p.expand_fused.end()) uses[ef->second]++;
-    auto bf = p.block_fused.find(op);
-    if (bf != p.block_fused.end()) uses[bf->second]++;
   }
   std::set<int> outset(out_ids.begin(), out_ids.end());
 
@@ -802,59 +798,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       return cnt;
     };
     std::vector<int> drop;
-    // Whole inverted residual blocks (Node::fb_op) first: the project op runs
-    // the expand and depthwise ops too, which leave the plan.
-    for (int op : p.ops) {
-      const Node& pn = nodes[op];
-      if (pn.op_type != "Conv" || pn.fb_op < 0 || !in_plan.count(pn.fb_op)) continue;
-      const Node& dn = nodes[pn.fb_op];
-      // With the expand (fe_op in this plan) or as depthwise -> project.
-      const bool expand = dn.fe_op >= 0 && in_plan.count(dn.fe_op);
-      if (dn.fe_op >= 0 && !expand) continue;
-      const Node& en = nodes[expand ? dn.fe_op : pn.fb_op];  // without an expand: the depthwise op reads x
-      const int xv = en.inputs[0];
-      if (outset0.count(dn.outputs[0]) || uses_of_value(p.ops, dn.outputs[0]) != 1 || pn.inputs[0] != dn.outputs[0])
-        continue;
-      if (expand && (outset0.count(en.outputs[0]) || uses_of_value(p.ops, en.outputs[0]) != 1 ||
-                     dn.inputs[0] != en.outputs[0]))
-        continue;
-      const Shape* xs = shape_of(xv);
-      const Shape* ys = shape_of(pn.outputs[0]);
-      if (!xs || !ys || xs->size() != 4 || ys->size() != 4 || p.dtypes[xv] == RTENHIP_DTYPE_INT32) continue;
-      const Shape& wes = nodes[dn.inputs[1]].shape;  // [hidden, 1, 3, 3]
-      const Shape& wps = nodes[pn.inputs[1]].shape;
-      ConvAttrs ca = conv_attrs(dn, false);
-      int64_t ohw[2], fp[4];
-      const bool ok = ca.mode == 0 && ca.dil == std::vector<int64_t>{1, 1} && ca.strides.size() == 2 &&
-                      ca.strides[0] == ca.strides[1] &&
-                      (expand ? nodes[en.inputs[1]].shape[1] == (*xs)[1] : wes[0] == (*xs)[1]) &&
-                      output_size_and_padding((*xs)[2], (*xs)[3], 3, 3, ca.strides[0], ca.strides[1], 0,
-                                              ca.pads.data(), 1, 1, ohw, fp) == RTENHIP_OK &&
-                      (*ys)[0] == (*xs)[0] && (*ys)[1] == wps[0] && (*ys)[2] == ohw[0] && (*ys)[3] == ohw[1] &&
-                      mbconv_block_eligible((int)(*xs)[1], (int)wes[0], (int)wps[0], (int)(*xs)[2], (int)(*xs)[3],
-                                            (int)ohw[0], (int)ohw[1], (int)ca.strides[0], (int)fp[0], (int)fp[1],
-                                            (int)fp[2], (int)fp[3], expand);
-      if (!ok) continue;
-      if (pn.fused_residual >= 0 && pn.fused_residual != xv) {
-        const Shape* rs = shape_of(pn.fused_residual);
-        if (!rs || *rs != *ys) continue;
-      }
-      if (pn.fused_residual == xv && (ca.strides[0] != 1 || (*xs)[1] != wps[0] || *xs != *ys)) continue;
-      {
-        // The kernel's skipped taps add w * copysign(0, -w) = -0: finite
-        // depthwise weights only (mbconv_block.hip MB_ZS).
-        std::vector<float> wdh((size_t)wes[0] * 9);
-        if (hipMemcpy(wdh.data(), nodes[dn.inputs[1]].dev, wdh.size() * sizeof(float), hipMemcpyDeviceToHost) !=
-            hipSuccess)
-          continue;
-        bool finite = true;
-        for (float w : wdh) finite = finite && std::isfinite(w);
-        if (!finite) continue;
-      }
-      p.block_fused[op] = xv;
-      drop.push_back(pn.fb_op);
-      if (expand) drop.push_back(dn.fe_op);
-    }
     for (int op : p.ops) {
       const Node& n = nodes[op];
       if (n.op_type != "Conv" || n.fe_op < 0 || !in_plan.count(n.fe_op) ||
@@ -889,7 +832,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   }
   for (int op : p.ops) {
     const Node& n = nodes[op];
-    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op) || p.block_fused.count(op)) continue;
+    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op)) continue;
     const Shape* xs = shape_of(n.inputs[0]);
     const Shape* ws = shape_of(n.inputs[1]);
     if (!xs || !ws || nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
@@ -1118,8 +1061,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       // (fused expand ops read their input through these maps, not inputs)
       auto ef = p.expand_fused.find(op);
       if (ef != p.expand_fused.end()) readers[ef->second].push_back(op);
-      auto bf = p.block_fused.find(op);
-      if (bf != p.block_fused.end()) readers[bf->second].push_back(op);
     }
     for (auto& kv : p.convs) {
       if (kv.second.fc) continue;
@@ -1177,7 +1118,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       auto cd = p.convs.find(ds);
       if (dn.op_type != "Conv" || cd == p.convs.end() || cd->second.fc || cd->second.g.groups != 1 ||
           dn.fused_residual >= 0 || dn.fused_act || dn.fused_bn >= 0 || outset.count(v) || uses[v] != 1 ||
-          p.conv_unfused.count(ds) || p.expand_fused.count(ds) || p.block_fused.count(ds) || p.padded.count(v))
+          p.conv_unfused.count(ds) || p.expand_fused.count(ds) || p.padded.count(v))
         continue;
       const ConvPlan& gd = cd->second.g;
       const bool ds_pad = gd.pads[0] || gd.pads[1] || gd.pads[2] || gd.pads[3];
@@ -1314,8 +1255,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (n.fused_residual >= 0) drop_use(n.fused_residual);
     auto ef = p.expand_fused.find(op);
     if (ef != p.expand_fused.end()) drop_use(ef->second);
-    auto bfu = p.block_fused.find(op);
-    if (bfu != p.block_fused.end()) drop_use(bfu->second);
     auto cdu = p.conv_dual.find(op);
     if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
     // An output nobody reads is released right after its producer.
@@ -1418,7 +1357,6 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     return c.ops[0] == op_id ? exec_chain(p, c) : RTENHIP_OK;  // members run inside the chain's launch
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
-  if (t == "Conv" && p.block_fused.count(op_id)) return exec_mbconv_block(p, op_id);
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
   if (t == "MatMul" && p.mm_group_skip.count(op_id)) return RTENHIP_OK;  // computed by its group's leader
   if (t == "Conv" && p.conv_dual.count(op_id)) {
@@ -1677,57 +1615,6 @@ rtenhip_status Graph::exec_expand_dw(Plan& p, int op_id) {
                           ptr_of(p, n.outputs[0]), (int)xs[0], (int)xs[1], (int)ys[1], (int)xs[2], (int)xs[3],
                           (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0], (int)fp[1], e.fused_act, e.act_lo,
                           e.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
-}
-
-// Whole inverted residual block (Node::fb_op) as one mbconv_block.hip launch,
-// reading the expand's input; the three convs' weights are repacked into the
-// kernel's operand order once per graph (Graph::mb_pack).
-rtenhip_status Graph::exec_mbconv_block(Plan& p, int op_id) {
-  const Node& pn = nodes[op_id];
-  const Node& dn = nodes[pn.fb_op];
-  const int xv = p.block_fused[op_id];
-  const bool expand = dn.inputs[0] != xv;  // else depthwise -> project (no expand conv)
-  const Node& en = nodes[expand ? dn.fe_op : pn.fb_op];
-  const Shape* xsp = plan_shape(*this, p, xv);
-  const Shape* ysp = plan_shape(*this, p, pn.outputs[0]);
-  if (!xsp || !ysp) return fail(RTENHIP_HIP_ERROR, "inverted residual block: missing shapes");
-  const Shape& xs = *xsp;
-  const Shape& ys = *ysp;
-  const int cin = (int)xs[1], hid = (int)nodes[dn.inputs[1]].shape[0], cout = (int)ys[1];
-  auto bias_of = [&](const Node& n) -> int { return n.inputs.size() > 2 && n.inputs[2] >= 0 ? n.inputs[2] : -1; };
-  const int be = expand ? bias_of(en) : -1, bd = bias_of(dn), bp = bias_of(pn);
-  auto pk = mb_pack.find(op_id);
-  if (pk == mb_pack.end()) {
-    // Plan-time work on the first (eager) run of this block.
-    auto host = [&](int v, size_t n) {
-      std::vector<float> h(n);
-      if (v >= 0 && n) (void)hipMemcpy(h.data(), nodes[v].dev, n * sizeof(float), hipMemcpyDeviceToHost);
-      return h;
-    };
-    const std::vector<float> we = host(expand ? en.inputs[1] : -1, expand ? (size_t)hid * cin : 0),
-                             hbe = host(be, be >= 0 ? hid : 0),
-                             wd = host(dn.inputs[1], (size_t)hid * 9), hbd = host(bd, bd >= 0 ? hid : 0),
-                             wp = host(pn.inputs[1], (size_t)cout * hid), hbp = host(bp, bp >= 0 ? cout : 0);
-    const int cin_e = expand ? cin : 0;  // packed without expand operands
-    std::vector<float> packed((size_t)mbconv_block_pack_floats(cin_e, hid, cout));
-    mbconv_block_pack(we.data(), be >= 0 ? hbe.data() : nullptr, wd.data(), bd >= 0 ? hbd.data() : nullptr, wp.data(),
-                      bp >= 0 ? hbp.data() : nullptr, cin_e, hid, cout, packed.data());
-    float* dev = nullptr;
-    RTENHIP_HIP_CHECK(hipMalloc(&dev, packed.size() * sizeof(float)));
-    RTENHIP_HIP_CHECK(hipMemcpy(dev, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice));
-    pk = mb_pack.emplace(op_id, dev).first;
-  }
-  ConvAttrs ca = conv_attrs(dn, false);
-  int64_t ohw[2], fp[4];
-  rtenhip_status st = output_size_and_padding(xs[2], xs[3], 3, 3, ca.strides[0], ca.strides[1], 0, ca.pads.data(), 1,
-                                              1, ohw, fp);
-  if (st) return st;
-  const bool res_x = pn.fused_residual == xv;
-  const float* res = pn.fused_residual >= 0 && !res_x ? ptr_of(p, pn.fused_residual) : nullptr;
-  return launch_mbconv_block(ptr_of(p, xv), pk->second, res, res_x, ptr_of(p, pn.outputs[0]), (int)xs[0], cin, hid,
-                             cout, (int)xs[2], (int)xs[3], (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0],
-                             (int)fp[1], en.fused_act, en.act_lo, en.act_hi, dn.fused_act, dn.act_lo, dn.act_hi,
-                             pn.fused_act, pn.act_lo, pn.act_hi, be >= 0, bd >= 0, bp >= 0, expand, ctx->stream);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -2962,7 +2849,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
             (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0 || n.fused_bn >= 0))
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
-        if (plan->block_fused.count(plan->ops[i])) key = "Conv(mbconv_block)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
@@ -3306,48 +3192,6 @@ rtenhip_status Graph::optimize() {
                                                          nodes[dn.inputs[2]].kind != NodeKind::Constant))
       continue;
     dn.fe_op = i;
-    fused++;
-  }
-  // MobileNetV2's whole inverted residual: a 1x1 project Conv whose input is
-  // the output of a depthwise Conv carrying fe_op, read by nothing else ->
-  // Node::fb_op (the plan decides whether the fused kernel takes the shapes).
-  for (int i = 0; i < (int)nodes.size(); i++) {
-    Node& pn = nodes[i];
-    if (pn.kind != NodeKind::Operator || pn.removed || pn.op_type != "Conv" || pn.fused_bn >= 0 ||
-        pn.fe_op >= 0 || pn.outputs.size() != 1 || pn.inputs.size() < 2 || !pn.input_perm.empty())
-      continue;
-    const int wv = pn.inputs[1];
-    if (wv < 0 || nodes[wv].kind != NodeKind::Constant || nodes[wv].shape.size() != 4 || nodes[wv].shape[2] != 1 ||
-        nodes[wv].shape[3] != 1)
-      continue;
-    const int bv = pn.inputs.size() > 2 ? pn.inputs[2] : -1;
-    if (bv >= 0 && nodes[bv].kind != NodeKind::Constant) continue;
-    ConvAttrs pa = conv_attrs(pn, false);
-    if (pa.mode != 0 || pa.groups != 1 || pa.pads != std::vector<int64_t>{0, 0, 0, 0} ||
-        pa.strides != std::vector<int64_t>{1, 1} || pa.dil != std::vector<int64_t>{1, 1})
-      continue;
-    // The producer: a depthwise 3x3 Conv (constant [C, 1, 3, 3] weights,
-    // groups C), with its expand (fe_op) or without one (features.1).
-    int d_op = -1;
-    for (int j = 0; j < (int)nodes.size(); j++) {
-      const Node& dn = nodes[j];
-      if (dn.kind == NodeKind::Operator && !dn.removed && dn.op_type == "Conv" && dn.outputs.size() == 1 &&
-          dn.outputs[0] == pn.inputs[0]) {
-        d_op = j;
-        break;
-      }
-    }
-    if (d_op < 0 || sole(pn.inputs[0]) != i) continue;
-    const Node& dn = nodes[d_op];
-    if (dn.fused_residual >= 0 || dn.fused_bn >= 0 || dn.inputs.size() < 2 || !dn.input_perm.empty()) continue;
-    const int dwv = dn.inputs[1];
-    if (dwv < 0 || nodes[dwv].kind != NodeKind::Constant) continue;
-    const int64_t hidden = nodes[dwv].shape.empty() ? -1 : nodes[dwv].shape[0];
-    if (nodes[dwv].shape != Shape{hidden, 1, 3, 3} || (int64_t)dn.attrs.num("groups", 1) != hidden ||
-        (dn.inputs.size() > 2 && dn.inputs[2] >= 0 && nodes[dn.inputs[2]].kind != NodeKind::Constant))
-      continue;
-    if (nodes[wv].shape[1] != hidden) continue;  // project K = hidden
-    pn.fb_op = d_op;
     fused++;
   }
   // FusedTranspose (optimize.rs:329-378): a MatMul reads a Transpose's input

@@ -110,12 +110,6 @@ struct Node {
   // fused kernel takes (mbconv.hip) drops that op and runs both here, reading
   // the expand's input; otherwise both run as they are.
   int fe_op = -1;
-  // MobileNetV2's whole inverted residual (Graph::optimize): on the 1x1
-  // project Conv, the depthwise Conv (itself carrying fe_op) whose only
-  // consumer it is.  A plan whose shapes the fused kernel takes
-  // (mbconv_block.hip) drops the expand and depthwise ops and runs all three
-  // here, reading the expand's input.
-  int fb_op = -1;
   // MatMul epilogue: constant [N] added per column after the K fold
   // (MatMul -> Add(bias)), before the residual and the activation.
   int fused_colbias = -1;
@@ -202,9 +196,6 @@ struct Plan {
   // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
   // the expand's input value, which the depthwise op then reads.
   std::map<int, int> expand_fused;
-  // Project convs running the whole inverted residual block (Node::fb_op):
-  // op id -> the expand's input value.
-  std::map<int, int> block_fused;
   // Grouped MatMuls (MatMulExec::nseg): leader op -> members (leader first),
   // members run by their leader; the members' outputs are segments of one
   // arena block of [nseg][M][N].
@@ -334,9 +325,6 @@ struct Graph {
   // [nseg][N]), keyed by the members' (weight, bias) node ids; shared by
   // every plan of the graph.
   std::map<std::vector<int>, std::pair<float*, float*>> mm_cat;
-  // Inverted residual blocks' weights repacked for mbconv_block.hip, keyed by
-  // the project op id; shared by every plan of the graph.
-  std::map<int, float*> mb_pack;
   void* arena = nullptr;
   size_t arena_cap = 0;
   hipStream_t exec_stream = nullptr;
@@ -409,7 +397,6 @@ struct Graph {
   // Conv chains (graph_chain.cpp).
   rtenhip_status build_chains(Plan& p);
   rtenhip_status exec_chain(Plan& p, Plan::ConvChain& c);
-  rtenhip_status exec_mbconv_block(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   // The packed-A store a producer of value v makes this run, or false.

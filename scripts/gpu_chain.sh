@@ -18,3 +18,9 @@ done
 RTENHIP_CHAIN=1 RTENHIP_CHAIN_STAMPS=$O/stamps.bin timeout -k 10 300 python -u rten-fork_amd/tools/model_once.py 2 resnet50 1 --report > $O/once.txt 2>&1 || { echo "stamped run failed"; tail $O/once.txt; exit 1; }
 grep "chain of" $O/once.txt
 python3 rten-fork_amd/tools/chain_stamps.py $O/stamps.bin > $O/stamps.txt && head -60 $O/stamps.txt
+# Host-resident input: copy / kernel overlap of the pipelined staging.
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/hostin -o run --output-format csv \
+  -- python3 bench.py --host-input --no-secondary --no-cpu-baseline --steps 20 --warmup 5 > $O/hostin.json 2> $O/hostin.err \
+  || { echo "host-input trace failed"; tail $O/hostin.err; exit 1; }
+python3 rten-fork_amd/tools/copy_overlap.py $O/hostin 12 > $O/hostin_overlap.txt; cat $O/hostin_overlap.txt
+rm -rf $O/hostin

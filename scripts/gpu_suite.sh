@@ -1,13 +1,12 @@
 #!/bin/bash
 # GPU session after kernel changes: the new parity tests first, then the whole
 # -m gpu suite without stopping at the first failure, smoke(), the bench line
-# (headline + secondaries) and a MobileNetV2 b128 A/B of the fused inverted
-# residual block (RTENHIP_MBCONV=0 runs the three convs apart).
+# (headline + secondaries).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/suite_${1:-now}; mkdir -p $O
 PYT="python -u -m pytest -q --timeout 300 --timeout-method thread"
-timeout -k 10 300 $PYT -x tests/test_vecmath_gpu.py tests/test_mbconv_block_gpu.py > $O/new.log 2>&1; rc=$?
+timeout -k 10 300 $PYT -x tests/test_vecmath_gpu.py tests/test_chain_gpu.py > $O/new.log 2>&1; rc=$?
 tail -3 $O/new.log; grep -E "FAILED|Error" $O/new.log | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || { echo "new tests aborted rc=$rc"; exit 1; }
 timeout -k 10 900 $PYT tests -m gpu > $O/suite.log 2>&1; rc=$?
@@ -23,5 +22,3 @@ print("head", d["metric"], d["value"], d["ms_per_step"], d["roofline"]["frac"])
 for s in d.get("secondary", []):
     print("  ", s.get("metric", s), s.get("value"), s.get("ms_per_step"), (s.get("roofline") or {}).get("frac"), s.get("error", ""))
 PY
-RTENHIP_MBCONV=0 timeout -k 10 300 python -u bench.py --model mobilenet_v2 --batch 128 --no-secondary --no-cpu-baseline > $O/mnv2_off.json 2> $O/mnv2_off.err \
-  && python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('mnv2 MBCONV=0', d['value'], d['ms_per_step'])" $O/mnv2_off.json
