@@ -16,6 +16,7 @@ constexpr int kChainPanels = 5;        // LDS panels per workgroup: RW A panels 
 struct ChainLayer {
   DmaDesc d;
   int rw, cw;            // rw * cw == 4: one 16x16 chain per wave
+  int bvec;              // pointwise stride-1, P % 4 == 0: 16-byte B copies (conv_chain.hip chain_item)
   int wg_m, wg_n, nkb, subs;
   int items;             // wg_m * wg_n * nkb, ordered (kb, tm, tn), tn fastest
   int item_base;         // first item of the layer within its phase

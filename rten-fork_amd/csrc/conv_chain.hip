@@ -86,13 +86,19 @@ __device__ __forceinline__ void chain_load_a(const ChainLayer& ly, const ItemPos
 // stores): B gathered by all 256 threads with sc1 loads, A from av (loaded
 // by the caller, possibly before the phase barrier), both staged in LDS; one
 // chain per wave; fold and epilogue with sc1 stores.
-template <int RW>
+// BVEC (pointwise stride-1 convs with P % 4 == 0, ChainLayer::bvec): B is
+// copied 16 bytes per lane -- 4 adjacent columns of one k row, never across
+// an image -- into a [CW][256 k][16 columns] LDS tile, and the chain reads
+// its B operands from it one float per step (4x fewer global loads than the
+// per-element gather).
+template <int RW, bool BVEC>
 __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& ip, float4* lds,
                                            const chain_u32x4 (&av)[16]) {
   constexpr int CW = 4 / RW;
   const DmaDesc& d = ly.d;
   float4(*lds_a)[LGROUPS][64] = reinterpret_cast<float4(*)[LGROUPS][64]>(lds);
   float4(*lds_b)[LGROUPS][64] = reinterpret_cast<float4(*)[LGROUPS][64]>(lds + RW * LGROUPS * 64);
+  float* ldsk = reinterpret_cast<float*>(lds + RW * LGROUPS * 64);  // BVEC: [CW][LKC][16]
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int K = d.K;
@@ -123,24 +129,44 @@ __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& 
       k3off[s9] = (uint32_t)((c0 + q) * d.kt_plane + ky * d.kt_row + kx * d.kt_col) * 4u;
     }
   }
-  uint32_t koff[16];
-#pragma unroll
-  for (int st = 0; st < 16; st++) {
-    const int k = k0 + 64 * wave + 4 * st + h;
-    const uint32_t lin = (uint32_t)k * (uint32_t)d.kstride * 4u;
-    const uint32_t win = k3off[st % 9] + (uint32_t)(st / 9) * k3step;
-    koff[st] = k < K ? (linear ? lin : win) : DMA_OOB;
-  }
   float bv[CW][4][4];
+  chain_u32x4 bq[CW][4];
+  const int q4 = threadIdx.x & 3, kr = threadIdx.x >> 2;  // BVEC: column quad, k row (+ 64 i)
+  if constexpr (BVEC) {
 #pragma unroll
-  for (int cw = 0; cw < CW; cw++) {
-    const LatCol col = lat_col(d, (ip.tn * CW + cw) * 16);
+    for (int cw = 0; cw < CW; cw++) {
+      const int n = (ip.tn * CW + cw) * 16 + 4 * q4;
+      uint32_t cb = DMA_OOB;
+      if (n < d.N) {
+        const int img = fdiv(n, d.fdP);
+        cb = (uint32_t)(((int64_t)img * d.x_img + (n - img * d.P)) * 4);
+      }
 #pragma unroll
-    for (int gi = 0; gi < 4; gi++)
+      for (int i = 0; i < 4; i++) {
+        const int k = k0 + kr + 64 * i;
+        const uint32_t off = (k < K && cb != DMA_OOB) ? cb + (uint32_t)k * (uint32_t)d.kstride * 4u : DMA_OOB;
+        bq[cw][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, kLoadSc1);
+      }
+    }
+  } else {
+    uint32_t koff[16];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        bv[cw][gi][j] =
-            __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + koff[4 * gi + j], 0, kLoadSc1));
+    for (int st = 0; st < 16; st++) {
+      const int k = k0 + 64 * wave + 4 * st + h;
+      const uint32_t lin = (uint32_t)k * (uint32_t)d.kstride * 4u;
+      const uint32_t win = k3off[st % 9] + (uint32_t)(st / 9) * k3step;
+      koff[st] = k < K ? (linear ? lin : win) : DMA_OOB;
+    }
+#pragma unroll
+    for (int cw = 0; cw < CW; cw++) {
+      const LatCol col = lat_col(d, (ip.tn * CW + cw) * 16);
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          bv[cw][gi][j] =
+              __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + koff[4 * gi + j], 0, kLoadSc1));
+    }
   }
   const bool live = sub0 < ly.subs && n0 < d.N;
   const LatCol col = lat_col(d, n0);
@@ -152,11 +178,21 @@ __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& 
     lds_a[idx >> 10][(idx >> 6) & 15][idx & 63] =
         make_float4(__uint_as_float(av[i].x), __uint_as_float(av[i].y), __uint_as_float(av[i].z), __uint_as_float(av[i].w));
   }
+  if constexpr (BVEC) {
 #pragma unroll
-  for (int cw = 0; cw < CW; cw++)
+    for (int cw = 0; cw < CW; cw++)
 #pragma unroll
-    for (int gi = 0; gi < 4; gi++)
-      lds_b[cw][4 * wave + gi][lane] = make_float4(bv[cw][gi][0], bv[cw][gi][1], bv[cw][gi][2], bv[cw][gi][3]);
+      for (int i = 0; i < 4; i++)
+        *reinterpret_cast<float4*>(ldsk + (cw * LKC + kr + 64 * i) * 16 + 4 * q4) =
+            make_float4(__uint_as_float(bq[cw][i].x), __uint_as_float(bq[cw][i].y), __uint_as_float(bq[cw][i].z),
+                        __uint_as_float(bq[cw][i].w));
+  } else {
+#pragma unroll
+    for (int cw = 0; cw < CW; cw++)
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++)
+        lds_b[cw][4 * wave + gi][lane] = make_float4(bv[cw][gi][0], bv[cw][gi][1], bv[cw][gi][2], bv[cw][gi][3]);
+  }
   __syncthreads();
   if (!live) return;
 
@@ -166,7 +202,13 @@ __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& 
   for (int g = 0; g < LGROUPS; g++) {
     if (g < ng) {
       const float4 a4 = lds_a[wr][g][lane];
-      const float4 b4 = lds_b[wc][g][lane];
+      float4 b4;
+      if constexpr (BVEC) {
+        const float* bp = ldsk + (wc * LKC + 16 * g + h) * 16 + (lane & 15);
+        b4 = make_float4(bp[0], bp[64], bp[128], bp[192]);  // k = 16g + 4j + h, j = 0..3
+      } else {
+        b4 = lds_b[wc][g][lane];
+      }
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[0], 0, 0, 0);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[0], 0, 0, 0);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[0], 0, 0, 0);
@@ -236,9 +278,15 @@ __global__ __launch_bounds__(256) void conv_chain_kernel(const ChainLayer* __res
       if (!(first && have_a)) chain_load_a(ly, ip, av);
       if (!first) chain_lds_barrier();  // the previous item's chains are done with LDS
       first = false;
-      if (ly.rw == 1) chain_item<1>(ly, ip, lds, av);
-      else if (ly.rw == 2) chain_item<2>(ly, ip, lds, av);
-      else chain_item<4>(ly, ip, lds, av);
+      if (ly.bvec) {
+        if (ly.rw == 1) chain_item<1, true>(ly, ip, lds, av);
+        else if (ly.rw == 2) chain_item<2, true>(ly, ip, lds, av);
+        else chain_item<4, true>(ly, ip, lds, av);
+      } else {
+        if (ly.rw == 1) chain_item<1, false>(ly, ip, lds, av);
+        else if (ly.rw == 2) chain_item<2, false>(ly, ip, lds, av);
+        else chain_item<4, false>(ly, ip, lds, av);
+      }
     }
     have_a = false;
     if (ph + 1 == nph) break;

@@ -160,6 +160,14 @@ rtenhip_status Graph::build_chains(Plan& p) {
       if ((st = lat_conv_desc(a, ly.d))) break;
       ly.rw = rw;
       ly.cw = 4 / rw;
+      {
+        static const bool no_bvec = getenv("RTENHIP_CHAIN_NO_BVEC") != nullptr;  // A/B experiments
+        const bool pw = g.kh == 1 && g.kw == 1 && g.sh == 1 && g.sw == 1 && a.Hp == g.oh && a.Wp == g.ow;
+        ly.bvec = (!no_bvec && pw && ly.d.P % 4 == 0 && ly.d.x_img % 4 == 0 && ly.d.kstride % 4 == 0 &&
+                   (uintptr_t)ly.d.x % 16 == 0)
+                      ? 1
+                      : 0;
+      }
       ly.subs = (ly.d.M + 15) / 16;
       ly.wg_m = (ly.subs + rw - 1) / rw;
       ly.wg_n = ((ly.d.N + 15) / 16 + ly.cw - 1) / ly.cw;

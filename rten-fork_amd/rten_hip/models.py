@@ -179,10 +179,19 @@ def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
     return total
 
 
-def _expand_dw_fused(cin: int, h: int, w: int) -> bool:
+def _expand_dw_fused(cin: int, h: int, w: int, stride: int = 1) -> bool:
     """Whether csrc/mbconv.hip runs an expand -> depthwise pair of these
-    shapes as one kernel by default (expand_dw_eligible: C_in = 16 banded)."""
-    return cin == 16 and w % 4 == 0
+    shapes as one kernel by default (expand_dw_eligible's default policy: the
+    banded kernel for C_in 16 / 24, and 32 at stride 2).  Kept in step with
+    the executor by tests/test_conv_pointwise_gpu.py (fused pairs counted in
+    the timing report)."""
+    banded = w % 4 == 0 and w // 4 <= 256 // 3
+    return banded and (cin in (16, 24) or (cin == 32 and stride == 2))
+
+
+def expand_dw_pairs(spec: ModelSpec, batch: int = 1, hw: int = 224) -> int:
+    """Expand -> depthwise pairs of ``spec`` the executor fuses by default."""
+    return int(conv_io_bytes(spec, batch, hw, count_pairs=True))
 
 
 def _expand_dw_fusable(cin: int, h: int, w: int) -> bool:
@@ -194,7 +203,7 @@ def _expand_dw_fusable(cin: int, h: int, w: int) -> bool:
     return banded or flat
 
 
-def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
+def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224, count_pairs: bool = False) -> float:
     """Algorithmic HBM bytes of every Conv (and the classifier Gemm) in
     ``spec`` at input [batch, 3, hw, hw], as the fused graph moves them: each
     conv reads its input and weights (+ bias) once and writes its output once;
@@ -218,6 +227,7 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
 
     fused_e, fused_d = set(), set()
     total = 0.0
+    pairs = 0
     for n in spec.nodes:
         if n.kind != "op":
             continue
@@ -232,7 +242,8 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
             e = source_conv(n.inputs[0])
             if n.attrs.get("groups", 1) == C and (kh, kw) == (3, 3) and e is not None:
                 ex = shapes[e.inputs[0]]
-                if _expand_dw_fused(ex[1], ex[2], ex[3]):
+                if _expand_dw_fused(ex[1], ex[2], ex[3], s[0]):
+                    pairs += 1
                     rd = 0  # the expand output never reaches HBM
                     total -= 4.0 * N * C * H * W  # nor is written by the expand
             total += 4.0 * (rd + wr + o * ci * kh * kw + o)
@@ -255,7 +266,7 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224) -> float:
             shapes[n.outputs[0]] = (xs[0], o)
         else:
             shapes[n.outputs[0]] = xs
-    return total
+    return pairs if count_pairs else total
 
 
 BERT_BASE_GFLOP_PER_SEQ128 = 22.347  # SURVEY.md App. A.3 (encoder, seq 128)

@@ -120,6 +120,9 @@ def test_mobilenet_v2_pointwise_valu(rh, monkeypatch, mode):
         rep = g.timing_report()
         m = re.search(r"Conv\(expand\+dw\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
         fused = int(m.group(1)) if m else 0
+        # bench.py's HBM bytes (models.conv_io_bytes) assume the executor's pairs
+        from rten_hip import models as _m
+        assert fused == _m.expand_dw_pairs(spec), (fused, _m.expand_dw_pairs(spec))
         assert rep.count("cfg=valu16") + fused >= 20, rep
 
 
