@@ -40,6 +40,10 @@ hipStream_t stream_of(rtenhip_ctx* ctx) { return reinterpret_cast<Ctx*>(ctx)->st
 Ctx::Ctx(int dev) : device(dev), ref_threads(rten_num_threads()) {}
 
 Ctx::~Ctx() {
+  if (exec_stream) {
+    (void)hipStreamSynchronize(exec_stream);
+    (void)hipStreamDestroy(exec_stream);
+  }
   for (auto& kv : ktabs) (void)hipFree(kv.second);
   for (auto& kv : dtabs) (void)hipFree(kv.second);
   for (auto& kv : packed_cache) (void)hipFree(kv.second);

@@ -91,9 +91,12 @@ __device__ __forceinline__ void chain_load_a(const ChainLayer& ly, const ItemPos
 // an image -- into a [CW][256 k][16 columns] LDS tile, and the chain reads
 // its B operands from it one float per step (4x fewer global loads than the
 // per-element gather).
+// ist (timing experiments only, null otherwise): {start, operands in LDS,
+// chain done, stored and drained} of this item, s_memrealtime.
 template <int RW, bool BVEC>
 __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& ip, float4* lds,
-                                           const chain_u32x4 (&av)[16]) {
+                                           const chain_u32x4 (&av)[16], unsigned long long* ist) {
+  if (ist && threadIdx.x == 0) ist[0] = __builtin_amdgcn_s_memrealtime();
   constexpr int CW = 4 / RW;
   const DmaDesc& d = ly.d;
   float4(*lds_a)[LGROUPS][64] = reinterpret_cast<float4(*)[LGROUPS][64]>(lds);
@@ -194,6 +197,7 @@ __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& 
         lds_b[cw][4 * wave + gi][lane] = make_float4(bv[cw][gi][0], bv[cw][gi][1], bv[cw][gi][2], bv[cw][gi][3]);
   }
   __syncthreads();
+  if (ist && threadIdx.x == 0) ist[1] = __builtin_amdgcn_s_memrealtime();
   if (!live) return;
 
   lat_f32x4 acc[1];
@@ -216,8 +220,16 @@ __device__ __forceinline__ void chain_item(const ChainLayer& ly, const ItemPos& 
     }
   }
   const int wt = sub0 * (ly.wg_n * CW) + (n0 >> 4);
+  if (ist && threadIdx.x == 0) {
+    asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][3]));
+    ist[2] = __builtin_amdgcn_s_memrealtime();
+  }
   LatStamps stp;
   lat_fold_finish<1, true>(d, sub0, ip.kb, ly.nkb, wt, col, e, acc, stp);
+  if (ist && threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ist[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // Workgroup barrier that leaves global loads in flight (__syncthreads would
@@ -278,14 +290,17 @@ __global__ __launch_bounds__(256) void conv_chain_kernel(const ChainLayer* __res
       if (!(first && have_a)) chain_load_a(ly, ip, av);
       if (!first) chain_lds_barrier();  // the previous item's chains are done with LDS
       first = false;
+      // (timing experiments: the first item of the phase is stamped)
+      unsigned long long* ist =
+          stamps && i == o ? stamps + 2 * (size_t)G * nph + 4 * ((size_t)bid * nph + ph) : nullptr;
       if (ly.bvec) {
-        if (ly.rw == 1) chain_item<1, true>(ly, ip, lds, av);
-        else if (ly.rw == 2) chain_item<2, true>(ly, ip, lds, av);
-        else chain_item<4, true>(ly, ip, lds, av);
+        if (ly.rw == 1) chain_item<1, true>(ly, ip, lds, av, ist);
+        else if (ly.rw == 2) chain_item<2, true>(ly, ip, lds, av, ist);
+        else chain_item<4, true>(ly, ip, lds, av, ist);
       } else {
-        if (ly.rw == 1) chain_item<1, false>(ly, ip, lds, av);
-        else if (ly.rw == 2) chain_item<2, false>(ly, ip, lds, av);
-        else chain_item<4, false>(ly, ip, lds, av);
+        if (ly.rw == 1) chain_item<1, false>(ly, ip, lds, av, ist);
+        else if (ly.rw == 2) chain_item<2, false>(ly, ip, lds, av, ist);
+        else chain_item<4, false>(ly, ip, lds, av, ist);
       }
     }
     have_a = false;

@@ -15,6 +15,11 @@ namespace rtenhip {
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // The graphs' executor stream (Graph::run), one per context and shared by
+  // its graphs: a process gets few hardware queues (GPU_MAX_HW_QUEUES, 4 by
+  // default), and streams beyond that share them, serialising copies or
+  // kernels queued behind another graph's work.
+  hipStream_t exec_stream = nullptr;
   // Thread count RTen would run with (RTEN_NUM_THREADS semantics,
   // src/threading.rs:41-62).  It only changes numerics in the gemv path,
   // where the reference's column blocking depends on it (gemm.rs:673).

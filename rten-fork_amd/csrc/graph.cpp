@@ -164,7 +164,7 @@ Graph::~Graph() {
     if (kv.second.first) (void)hipFree(kv.second.first);
     if (kv.second.second) (void)hipFree(kv.second.second);
   }
-  if (exec_stream) (void)hipStreamDestroy(exec_stream);
+  if (exec_stream) (void)hipStreamSynchronize(exec_stream);  // the context's stream (Ctx::exec_stream)
   if (ev_in) (void)hipEventDestroy(ev_in);
   if (ev_out) (void)hipEventDestroy(ev_out);
 }
@@ -2675,7 +2675,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   }
   hipStream_t caller = ctx->stream;
   if (!exec_stream) {
-    RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&exec_stream, hipStreamNonBlocking));
+    if (!ctx->exec_stream) RTENHIP_HIP_CHECK(hipStreamCreateWithFlags(&ctx->exec_stream, hipStreamNonBlocking));
+    exec_stream = ctx->exec_stream;
     RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_in, hipEventDisableTiming));
     RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&ev_out, hipEventDisableTiming));
   }

@@ -312,7 +312,7 @@ rtenhip_status Graph::exec_chain(Plan& p, Plan::ConvChain& c) {
   if (!stamp_path || cs != hipStreamCaptureStatusNone)
     return launch_conv_chain(ld, pd, c.n_phases, c.ctrl, c.grid, ctx->stream);
   unsigned long long* st_dev = nullptr;
-  const size_t bytes = (size_t)c.grid * c.n_phases * 16;
+  const size_t bytes = (size_t)c.grid * c.n_phases * 48;  // barrier pairs, then 4 item stamps per block and phase
   RTENHIP_HIP_CHECK(hipMalloc(&st_dev, bytes));
   RTENHIP_HIP_CHECK(hipMemsetAsync(st_dev, 0, bytes, ctx->stream));
   rtenhip_status st = launch_conv_chain(ld, pd, c.n_phases, c.ctrl, c.grid, ctx->stream, st_dev);

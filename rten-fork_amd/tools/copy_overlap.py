@@ -25,7 +25,16 @@ def main():
         print("no memory copy trace")
         return
     cs.sort(key=lambda r: int(r["Start_Timestamp"]))
-    big = [r for r in cs if int(r.get("Size", 0) or 0) >= 1 << 16][-n:]
+    print("copy trace columns:", ",".join(cs[0].keys()), f"({len(cs)} copies)")
+
+    def size_of(r):
+        for k in ("Size", "Bytes", "Copy_Bytes", "Size_Bytes"):
+            if r.get(k):
+                return int(r[k])
+        return 0
+
+    big = [r for r in cs if size_of(r) >= 1 << 16 or (size_of(r) == 0 and
+                                                       int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > 50000)][-n:]
 
     def busy(a, b):
         t, cur = 0, a
@@ -40,8 +49,8 @@ def main():
 
     for r in big:
         a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        size = int(r.get("Size", 0) or 0)
-        dirn = r.get("Direction", r.get("Operation", "?"))
+        size = size_of(r)
+        dirn = r.get("Direction", r.get("Operation", r.get("Kind", "?")))
         print(f"{dirn:>28} {size / 1e6:8.2f} MB {(b - a) / 1e3:8.1f} us {size / max(b - a, 1):6.1f} GB/s "
               f"kernel-overlap {busy(a, b) / max(b - a, 1):.2f}")
     if big:

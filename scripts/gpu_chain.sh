@@ -15,6 +15,8 @@ for m in 0 -1 1; do
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('chain', sys.argv[2], d['value'], d['ms_per_step'])" $O/b1_$m.json $m
   grep "conv chain" $O/b1_$m.err | head -3
 done
+RTENHIP_CHAIN=1 RTENHIP_CHAIN_NO_BVEC=1 RTENHIP_CHAIN_STAMPS=$O/stamps_nobvec.bin timeout -k 10 300 python -u rten-fork_amd/tools/model_once.py 2 resnet50 1 > $O/once_nobvec.txt 2>&1 || { echo "stamped run failed"; tail $O/once_nobvec.txt; exit 1; }
+python3 rten-fork_amd/tools/chain_stamps.py $O/stamps_nobvec.bin > $O/stamps_nobvec.txt && tail -1 $O/stamps_nobvec.txt
 RTENHIP_CHAIN=1 RTENHIP_CHAIN_STAMPS=$O/stamps.bin timeout -k 10 300 python -u rten-fork_amd/tools/model_once.py 2 resnet50 1 --report > $O/once.txt 2>&1 || { echo "stamped run failed"; tail $O/once.txt; exit 1; }
 grep "chain of" $O/once.txt
 python3 rten-fork_amd/tools/chain_stamps.py $O/stamps.bin > $O/stamps.txt && head -60 $O/stamps.txt
@@ -24,3 +26,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/hostin -o r
   || { echo "host-input trace failed"; tail $O/hostin.err; exit 1; }
 python3 rten-fork_amd/tools/copy_overlap.py $O/hostin 12 > $O/hostin_overlap.txt; cat $O/hostin_overlap.txt
 rm -rf $O/hostin
+NO_SUITE=1 bash scripts/gpu_check.sh ${1:-now}_bench || exit 1
