@@ -66,11 +66,17 @@ __global__ __launch_bounds__(256) void gemm_lat_kernel(DmaDesc d, int wg_m, int 
 // both once per wave).  The chains then read their operands from LDS as
 // 16-byte groups in the same k order, so the bits are those of every other
 // variant; the fold and the epilogue are lat_fold_finish's.
-template <int RW, int CW>
+//
+// BVEC (pointwise stride-1 convs with P % 4 == 0, DmaDesc::bvec): B is copied
+// 16 bytes per lane -- 4 adjacent columns of one k row, inside one image --
+// into a [CW][256 k][16 columns] tile, and the chains read it one float per
+// MFMA step: a quarter of the gather's load instructions.
+template <int RW, int CW, bool BVEC>
 __global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
   static_assert(RW * CW == 4, "one chain per wave");
   __shared__ float4 lds_a[RW][LGROUPS][64];
   __shared__ float4 lds_b[CW][LGROUPS][64];
+  float* ldsk = reinterpret_cast<float*>(&lds_b[0][0][0]);  // BVEC: [CW][LKC][16]
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int G = gridDim.x, bid = blockIdx.x;
@@ -127,23 +133,44 @@ __global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int
       k3off[s9] = (uint32_t)((c0 + q) * d.kt_plane + ky * d.kt_row + kx * d.kt_col) * 4u;
     }
   }
-  uint32_t koff[16];
-#pragma unroll
-  for (int st = 0; st < 16; st++) {  // step within this thread's 16
-    const int k = k0 + 64 * wave + 4 * st + h;
-    const uint32_t lin = (uint32_t)k * (uint32_t)d.kstride * 4u;
-    const uint32_t win = k3off[st % 9] + (uint32_t)(st / 9) * k3step;
-    koff[st] = k < K ? (linear ? lin : win) : DMA_OOB;
-  }
   float bv[CW][4][4];
+  typedef unsigned int lat2_u32x4 __attribute__((ext_vector_type(4)));
+  lat2_u32x4 bq[CW][4];
+  const int q4 = threadIdx.x & 3, kr = threadIdx.x >> 2;  // BVEC: column quad, k row (+ 64 i)
+  if constexpr (BVEC) {
 #pragma unroll
-  for (int cw = 0; cw < CW; cw++) {
-    const LatCol col = lat_col(d, (tn * CW + cw) * 16);
+    for (int cw = 0; cw < CW; cw++) {
+      const int n = (tn * CW + cw) * 16 + 4 * q4;
+      uint32_t cb = DMA_OOB;
+      if (n < d.N) {
+        const int img = fdiv(n, d.fdP);
+        cb = (uint32_t)(((int64_t)img * d.x_img + (n - img * d.P)) * 4);
+      }
 #pragma unroll
-    for (int gi = 0; gi < 4; gi++)
+      for (int i = 0; i < 4; i++) {
+        const int k = k0 + kr + 64 * i;
+        const uint32_t off = (k < K && cb != DMA_OOB) ? cb + (uint32_t)k * (uint32_t)d.kstride * 4u : DMA_OOB;
+        bq[cw][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      }
+    }
+  } else {
+    uint32_t koff[16];
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        bv[cw][gi][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + koff[4 * gi + j], 0, 0));
+    for (int st = 0; st < 16; st++) {  // step within this thread's 16
+      const int k = k0 + 64 * wave + 4 * st + h;
+      const uint32_t lin = (uint32_t)k * (uint32_t)d.kstride * 4u;
+      const uint32_t win = k3off[st % 9] + (uint32_t)(st / 9) * k3step;
+      koff[st] = k < K ? (linear ? lin : win) : DMA_OOB;
+    }
+#pragma unroll
+    for (int cw = 0; cw < CW; cw++) {
+      const LatCol col = lat_col(d, (tn * CW + cw) * 16);
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          bv[cw][gi][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + koff[4 * gi + j], 0, 0));
+    }
   }
   if (stp.p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -155,11 +182,21 @@ __global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int
     lds_a[idx >> 10][(idx >> 6) & 15][idx & 63] =
         make_float4(__uint_as_float(av[i].x), __uint_as_float(av[i].y), __uint_as_float(av[i].z), __uint_as_float(av[i].w));
   }
+  if constexpr (BVEC) {
 #pragma unroll
-  for (int cw = 0; cw < CW; cw++)
+    for (int cw = 0; cw < CW; cw++)
 #pragma unroll
-    for (int gi = 0; gi < 4; gi++)
-      lds_b[cw][4 * wave + gi][lane] = make_float4(bv[cw][gi][0], bv[cw][gi][1], bv[cw][gi][2], bv[cw][gi][3]);
+      for (int i = 0; i < 4; i++)
+        *reinterpret_cast<float4*>(ldsk + (cw * LKC + kr + 64 * i) * 16 + 4 * q4) =
+            make_float4(__uint_as_float(bq[cw][i].x), __uint_as_float(bq[cw][i].y), __uint_as_float(bq[cw][i].z),
+                        __uint_as_float(bq[cw][i].w));
+  } else {
+#pragma unroll
+    for (int cw = 0; cw < CW; cw++)
+#pragma unroll
+      for (int gi = 0; gi < 4; gi++)
+        lds_b[cw][4 * wave + gi][lane] = make_float4(bv[cw][gi][0], bv[cw][gi][1], bv[cw][gi][2], bv[cw][gi][3]);
+  }
 
   // Epilogue operands of this wave's tile, in flight during the chain.
   const bool live = sub0 < subs && n0 < d.N;
@@ -176,7 +213,13 @@ __global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int
   for (int g = 0; g < LGROUPS; g++) {
     if (g < ng) {
       const float4 a4 = lds_a[wr][g][lane];
-      const float4 b4 = lds_b[wc][g][lane];
+      float4 b4;
+      if constexpr (BVEC) {
+        const float* bp = ldsk + (wc * LKC + 16 * g + h) * 16 + (lane & 15);
+        b4 = make_float4(bp[0], bp[64], bp[128], bp[192]);  // k = 16g + 4j + h, j = 0..3
+      } else {
+        b4 = lds_b[wc][g][lane];
+      }
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[0], 0, 0, 0);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[0], 0, 0, 0);
       acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[0], 0, 0, 0);
@@ -351,9 +394,15 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   if (v >= 70 && v < 80) {
     if (d.kstride <= 0 && !d.k3x3) return fail(RTENHIP_UNSUPPORTED_VALUE, "LDS latency GEMM: 1x1 or 3x3 windows only");
     const dim3 grid((unsigned)g.wgs), blk(256);
-    if (v == 71) hipLaunchKernelGGL((gemm_lat2_kernel<1, 4>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
-    else if (v == 72) hipLaunchKernelGGL((gemm_lat2_kernel<2, 2>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
-    else hipLaunchKernelGGL((gemm_lat2_kernel<4, 1>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+    if (d.bvec) {
+      if (v == 71) hipLaunchKernelGGL((gemm_lat2_kernel<1, 4, true>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+      else if (v == 72) hipLaunchKernelGGL((gemm_lat2_kernel<2, 2, true>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+      else hipLaunchKernelGGL((gemm_lat2_kernel<4, 1, true>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+    } else {
+      if (v == 71) hipLaunchKernelGGL((gemm_lat2_kernel<1, 4, false>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+      else if (v == 72) hipLaunchKernelGGL((gemm_lat2_kernel<2, 2, false>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+      else hipLaunchKernelGGL((gemm_lat2_kernel<4, 1, false>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);
+    }
     RTENHIP_LAUNCH_CHECK();
     return RTENHIP_OK;
   }
