@@ -93,7 +93,9 @@ rtenhip_status Graph::build_chains(Plan& p) {
   for (const std::vector<int>& run : runs) {
     int lat = 0;
     for (int op : run) lat += is_lat_cfg(p.convs[op].cfg) ? 1 : 0;
-    if (chain_mode != 1 && 2 * lat < (int)run.size()) continue;
+    // Auto mode: long runs only (a launch saved per conv is what the chain
+    // can win; a short run cannot repay its barriers).
+    if (chain_mode != 1 && (2 * lat < (int)run.size() || run.size() < 8)) continue;
     Plan::ConvChain c;
     c.ops = run;
     const std::set<int> in_run(run.begin(), run.end());
