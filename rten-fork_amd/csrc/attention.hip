@@ -31,7 +31,6 @@
 #include "vecmath.h"
 
 #include <cfloat>
-#include <cstdlib>
 #include <cmath>
 
 // Timing experiments only (never set in a product build): 1 = no exp / divide,
@@ -62,24 +61,14 @@ constexpr int AT_THREADS = 256;  // 4 waves
 // FULL: S == AT_S, every key and row guard folds away at compile time.
 // VEC: q, k and v rows are 16-byte aligned with unit element stride (checked
 // at launch, attention_vec_ok), so only the float4 staging paths are built.
-// QW: waves per workgroup.  QW = 4: one workgroup per (batch, head), K and V
-// side by side in LDS (65 KB, two workgroups per CU: 384 BERT-base b32
-// workgroups leave half the CUs running two and half one).  QW = 2: one
-// workgroup per (batch, head, 64 query rows); V is written over K once every
-// score is formed (33 KB, four workgroups per CU: 768 workgroups, three on
-// every CU), at the price of one more barrier and staging K / V twice per
-// (batch, head).
-template <bool FULL, bool VEC, int QW>
-__global__ __launch_bounds__(QW * 64, 2) void attention_kernel(AttnDesc d) {
-  constexpr int NT = QW * 64;
-  constexpr int PARTS = 4 / QW;  // workgroups per (batch, head)
+template <bool FULL, bool VEC>
+__global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   __shared__ float Ks[AT_S * KS];
-  __shared__ float Vs_own[QW == 4 ? AT_S * VS : 1];
-  float* Vs = QW == 4 ? Vs_own : Ks;
+  __shared__ float Vs[AT_S * VS];
   __shared__ float Ms[AT_S];  // the mask row when it does not depend on the query row (m_i == 0)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, l32 = lane & 31;
-  const int bh = blockIdx.x / PARTS, qpart = blockIdx.x - bh * PARTS;
+  const int bh = blockIdx.x;
   const int b = bh / d.H, hd = bh - b * d.H;
   const int S = FULL ? AT_S : d.S;
 
@@ -93,11 +82,11 @@ __global__ __launch_bounds__(QW * 64, 2) void attention_kernel(AttnDesc d) {
   // for the whole staging, not one per row group).
   const bool v4 = VEC || (((uintptr_t)v % 16 == 0) && d.v_s % 4 == 0);
   const bool k4 = VEC || (d.k_d == 1 && ((uintptr_t)kt % 16 == 0) && d.k_s % 4 == 0);
-  constexpr int ST = AT_S * (AT_D / 4) / NT;  // float4 positions per thread (8 / 16)
+  constexpr int ST = AT_S * (AT_D / 4) / AT_THREADS;  // float4 positions per thread (8)
   float4 kk[ST], vv[ST];
 #pragma unroll
   for (int u = 0; u < ST; u++) {
-    const int t = tid + u * NT;
+    const int t = tid + u * AT_THREADS;
     const int j = t >> 4, c = (t & 15) * 4;
     kk[u] = vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((FULL || j < S) && RTENHIP_ATT_EXPERIMENT != 4) {
@@ -119,7 +108,7 @@ __global__ __launch_bounds__(QW * 64, 2) void attention_kernel(AttnDesc d) {
   if (mask_lds && tid < S) mv = d.mask[b * d.m_b + hd * d.m_h + (int64_t)tid * d.m_j];
 #pragma unroll
   for (int u = 0; u < ST; u++) {
-    const int t = tid + u * NT;
+    const int t = tid + u * AT_THREADS;
     const int j = t >> 4, c = (t & 15) * 4;
     float* kd = Ks + j * KS + c;
     kd[0] = kk[u].x;
@@ -129,8 +118,7 @@ __global__ __launch_bounds__(QW * 64, 2) void attention_kernel(AttnDesc d) {
   }
   // (V stays in registers, still in flight, until the scores are done.)
   if (mask_lds && tid < S) Ms[tid] = mv;
-  static_assert(NT >= AT_S, "one mask entry per thread");
-  const int i0 = (qpart * QW + wave) * 32;
+  const int i0 = wave * 32;
   const int i = i0 + l32;  // this lane's query row
   const bool row_ok = FULL || i < S;
   // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand),
@@ -163,12 +151,10 @@ __global__ __launch_bounds__(QW * 64, 2) void attention_kernel(AttnDesc d) {
     }
   }
   // V to LDS now (its loads had the score MFMAs to land); read after the
-  // softmax, past the second barrier.  (QW = 2: over K, once every wave has
-  // read its last K row.)
-  if constexpr (QW == 2) __syncthreads();
+  // softmax, past the second barrier.
 #pragma unroll
   for (int u = 0; u < ST; u++) {
-    const int t = tid + u * NT;
+    const int t = tid + u * AT_THREADS;
     const int j = t >> 4, c = (t & 15) * 4;
     *(float4*)(Vs + j * VS + c) = vv[u];
   }
@@ -384,7 +370,7 @@ __global__ void vecmath_check_kernel(const float* a, const float* b, int64_t n, 
 
 bool attention_fast_ok(const AttnDesc& d) {
   return d.D == AT_D && d.S >= 2 && d.S <= AT_S && d.S % 2 == 0 && d.B > 0 && d.H > 0 &&
-         (int64_t)d.B * d.H < (int64_t(1) << 30);
+         (int64_t)d.B * d.H < (int64_t(1) << 31);
 }
 
 rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s) {
@@ -402,24 +388,15 @@ rtenhip_status launch_attention(const AttnDesc& d, hipStream_t s) {
   const bool vec = al16(d.q) && al16(d.k) && al16(d.v) && d.q_b % 4 == 0 && d.q_h % 4 == 0 &&
                    d.q_s % 4 == 0 && d.k_d == 1 && d.k_b % 4 == 0 && d.k_h % 4 == 0 && d.k_s % 4 == 0 &&
                    d.v_b % 4 == 0 && d.v_h % 4 == 0 && d.v_s % 4 == 0;
-  // Query halves (QW = 2) unless RTENHIP_ATT_QW=4 (A/B experiments).
-  static const int qw = [] {
-    const char* e = getenv("RTENHIP_ATT_QW");
-    return e && atoi(e) == 4 ? 4 : 2;
-  }();
-  if (qw == 2) {
-    const dim3 grid((unsigned)(d.B * d.H * 2)), block(128);
-    if (d.S == AT_S && vec) hipLaunchKernelGGL((attention_kernel<true, true, 2>), grid, block, 0, s, e);
-    else if (d.S == AT_S) hipLaunchKernelGGL((attention_kernel<true, false, 2>), grid, block, 0, s, e);
-    else if (vec) hipLaunchKernelGGL((attention_kernel<false, true, 2>), grid, block, 0, s, e);
-    else hipLaunchKernelGGL((attention_kernel<false, false, 2>), grid, block, 0, s, e);
-  } else {
-    const dim3 grid((unsigned)(d.B * d.H)), block(AT_THREADS);
-    if (d.S == AT_S && vec) hipLaunchKernelGGL((attention_kernel<true, true, 4>), grid, block, 0, s, e);
-    else if (d.S == AT_S) hipLaunchKernelGGL((attention_kernel<true, false, 4>), grid, block, 0, s, e);
-    else if (vec) hipLaunchKernelGGL((attention_kernel<false, true, 4>), grid, block, 0, s, e);
-    else hipLaunchKernelGGL((attention_kernel<false, false, 4>), grid, block, 0, s, e);
-  }
+  const dim3 grid((unsigned)(d.B * d.H)), block(AT_THREADS);
+  if (d.S == AT_S && vec)
+    hipLaunchKernelGGL((attention_kernel<true, true>), grid, block, 0, s, e);
+  else if (d.S == AT_S)
+    hipLaunchKernelGGL((attention_kernel<true, false>), grid, block, 0, s, e);
+  else if (vec)
+    hipLaunchKernelGGL((attention_kernel<false, true>), grid, block, 0, s, e);
+  else
+    hipLaunchKernelGGL((attention_kernel<false, false>), grid, block, 0, s, e);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

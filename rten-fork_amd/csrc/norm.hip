@@ -206,11 +206,6 @@ __device__ __forceinline__ float strided_sum_n(const float* p, int s) {
 #define RTENHIP_LN_ROWS_NUM 6144
 #endif
 
-// Value of lane l ^ 1 (DPP quad_perm [1, 0, 3, 2], no LDS trip).
-__device__ __forceinline__ float ln_xor1(float x) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));
-}
-
 template <int LEN>
 __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const float* __restrict__ x, float* __restrict__ y, int64_t rows, int len_arg, int R,
@@ -341,25 +336,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         o.w = __fadd_rn(o.w, bb[i].w);
       }
       if (RTENHIP_LN_EXPERIMENT != 3) y4[r * q + c] = o;
-      if constexpr (LEN > 0 && LEN % 256 == 0) {
-        if (pk.p && RTENHIP_LN_EXPERIMENT != 1) {
-          // The MatMul's packed A straight from registers (packed_a.h): lanes
-          // 2j and 2j + 1 hold columns 8p .. 8p + 7 (p = c / 2) as two
-          // float4s; one neighbour exchange gives the even lane k-quad
-          // {8p, +2, +4, +6} and the odd lane {8p + 1, +3, +5, +7}, each one
-          // 16-byte store (k tile tk, quad qq, row m).  Same values, new places.
-          const bool odd = lane & 1;
-          const float r0 = ln_xor1(odd ? o.x : o.y), r1 = ln_xor1(odd ? o.z : o.w);
-          const float4 chunk = odd ? make_float4(r0, r1, o.y, o.w) : make_float4(o.x, o.z, r0, r1);
-          const int k8 = 8 * (c >> 1);
-          const int tk = k8 >> pk.lbk, qq = 2 * ((k8 - (tk << pk.lbk)) >> 3) + (odd ? 1 : 0);
-          const int64_t m = row0 + r;
-          float* tb = pk.p + (((m >> pk.lbm) * pk.tiles_k + tk) << (pk.lbm + pk.lbk));
-          *(float4*)(tb + (((int64_t)qq << pk.lbm) + (m & ((1 << pk.lbm) - 1))) * 4) = chunk;
-        }
-      } else {
-        if (pk.p) lds4[r * qs + c] = o;  // this thread's own element: no hazard
-      }
+      if (pk.p) lds4[r * qs + c] = o;  // this thread's own element: no hazard
     }
   };
   if constexpr (LEN > 0 && LEN % 256 == 0) {
@@ -371,7 +348,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
         out_row(r, &sc, &bb, c, 1);
       }
   }
-  if (!(LEN > 0 && LEN % 256 == 0) && pk.p && RTENHIP_LN_EXPERIMENT != 1) {
+  if (pk.p && RTENHIP_LN_EXPERIMENT != 1) {
     // The MatMul's packed A (packed_a.h): one 16-byte chunk per (k tile,
     // plane, row) with the row fastest, so consecutive threads write
     // consecutive chunks of a plane (rows are 16 bytes apart in it).
