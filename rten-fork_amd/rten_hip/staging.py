@@ -11,21 +11,25 @@ the upload on top of the forward.
 
 ``HostStaging`` pipelines it instead.  Inputs come from pinned host memory
 (DMA straight from the pages, no bounce copy) into one of ``slots`` device
-buffers on an upload stream; the forward of step k runs on the compute
-stream as soon as its slot has landed, while step k+1's upload is already
-in flight on the SDMA engine; step k's outputs go back to pinned host memory
-on a download stream while step k+1 computes.  Events order the three
+buffers; the forward of step k runs on the compute stream as soon as its slot
+has landed, while step k+1's upload is already in flight; step k's outputs go
+back to pinned host memory while step k+1 computes.  ONE copy stream carries
+both directions, in the order upload(k), download(k - 1): the upload of step k
+only waits for the forward that last read its slot (k - 2), so it runs during
+forward k - 1, and the download of step k - 1 follows it.  Events order the
 streams per slot, so nothing waits on the host:
 
-    upload   : wait in_free[s]  -> H2D host_in -> dev_in[s]    -> in_ready[s]
-    compute  : wait in_ready[s], out_free[s] -> forward(dev_in[s]) -> dev_out[s]
-               -> in_free[s], out_ready[s]
-    download : wait out_ready[s] -> D2H dev_out[s] -> host_out  -> out_free[s]
+    copy    : wait in_free[s]   -> H2D host_in(k) -> dev_in[s]   -> in_ready[s]
+              wait out_ready[s'] -> D2H out(k - 1) -> host_out    -> out_free[s']
+    compute : wait in_ready[s], out_free[s] -> forward(dev_in[s]) -> in_free[s], out_ready[s]
 
-The graph keeps one captured hipGraph per (input, output) binding
-(``Plan::captures``, up to four), so alternating slots replay without
-re-capturing.  With the batch sharded over ranks (parallel.py) each rank
-stages its own slice.
+The copy stream is created at high priority: a process gets few hardware
+queues (GPU_MAX_HW_QUEUES, 4 by default) and a normal-priority stream can land
+on the queue of the graph executor's stream, where the copies would wait
+behind the forwards they are meant to overlap.  The graph keeps one captured
+hipGraph per (input, output) binding (``Plan::captures``, up to four), so
+alternating slots replay without re-capturing.  With the batch sharded over
+ranks (parallel.py) each rank stages its own slice.
 """
 from __future__ import annotations
 
@@ -50,8 +54,7 @@ class HostStaging:
         self.device = torch.device(device)
         dtype = dtype or torch.float32
         self.compute = torch.cuda.current_stream(self.device)
-        self.up = torch.cuda.Stream(self.device)
-        self.down = torch.cuda.Stream(self.device)
+        self.copy = torch.cuda.Stream(self.device, priority=-1)
         self.dev_in = [torch.empty(tuple(in_shape), dtype=dtype, device=self.device) for _ in range(self.slots)]
         E = torch.cuda.Event
         self.in_ready = [E() for _ in range(self.slots)]
@@ -59,6 +62,7 @@ class HostStaging:
         self.out_ready = [E() for _ in range(self.slots)]
         self.out_free = [E() for _ in range(self.slots)]
         self.k = 0
+        self.pending = None  # (slot, device output, host output) of the last step
 
     @staticmethod
     def pinned(shape, dtype=None):
@@ -66,6 +70,15 @@ class HostStaging:
         import torch
 
         return torch.empty(tuple(shape), dtype=dtype or torch.float32, pin_memory=True)
+
+    def _download(self):
+        s, out, host_out = self.pending
+        self.pending = None
+        with self.torch.cuda.stream(self.copy):
+            self.copy.wait_event(self.out_ready[s])
+            out.record_stream(self.copy)  # the allocator must not reuse it before the copy
+            host_out.copy_(out, non_blocking=True)
+            self.out_free[s].record(self.copy)
 
     def submit(self, host_in, host_out) -> None:
         """Queue one step: host_in (pinned, in_shape) -> forward -> host_out
@@ -76,24 +89,24 @@ class HostStaging:
             raise ValueError(f"input shape {tuple(host_in.shape)} != staged {tuple(self.dev_in[0].shape)}")
         s = self.k % self.slots
         self.k += 1
-        with torch.cuda.stream(self.up):
-            self.up.wait_event(self.in_free[s])  # the forward that read this slot is done
+        with torch.cuda.stream(self.copy):
+            self.copy.wait_event(self.in_free[s])  # the forward that read this slot is done
             self.dev_in[s].copy_(host_in, non_blocking=True)
-            self.in_ready[s].record(self.up)
+            self.in_ready[s].record(self.copy)
+        if self.pending is not None:
+            self._download()  # the previous step's outputs, behind this upload
         with torch.cuda.stream(self.compute):
             self.compute.wait_event(self.in_ready[s])
             self.compute.wait_event(self.out_free[s])  # this slot's last outputs are downloaded
             out = self.forward(self.dev_in[s], s)
             self.in_free[s].record(self.compute)
             self.out_ready[s].record(self.compute)
-        with torch.cuda.stream(self.down):
-            self.down.wait_event(self.out_ready[s])
-            out.record_stream(self.down)  # the allocator must not reuse it before the copy
-            host_out.copy_(out, non_blocking=True)
-            self.out_free[s].record(self.down)
+        self.pending = (s, out, host_out)
 
     def synchronize(self) -> None:
-        for st in (self.up, self.compute, self.down):
+        if self.pending is not None:
+            self._download()
+        for st in (self.copy, self.compute):
             st.synchronize()
 
 
