@@ -128,9 +128,5 @@ int64_t lat_packed_floats(int M, int K);
 rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float* out, hipStream_t s);
 DmaSplit lat_split_plan(int M, int N, int K, int variant);
 rtenhip_status launch_gemm_lat(const DmaDesc& d, int variant, hipStream_t s);
-// Variants 61 / 62 / 64 (gemm_pwb.hip): 1x1 convs (kstride > 0) with K <= 256,
-// the workgroup's B panel in LDS, mr chunks of 64 rows per workgroup.
-bool pwb_ok(const DmaDesc& d);
-rtenhip_status launch_gemm_pwb(const DmaDesc& d, int mr, hipStream_t s);
 
 }  // namespace rtenhip

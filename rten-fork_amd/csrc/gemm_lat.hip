@@ -319,7 +319,6 @@ rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float*
 bool lat_variant_ok(int v) {
   if (v == 91 || v == 92) return true;  // workgroup fold
   if (v == 71 || v == 72 || v == 74) return true;  // LDS-staged, RW = v - 70 rows x CW = 4 / RW columns
-  if (v == 61 || v == 62 || v == 64) return true;  // B-stationary pointwise (gemm_pwb.hip), v - 60 row chunks
   const int wmw = v / 10, mi = v % 10;
   return (wmw == 1 || wmw == 2 || wmw == 4) && (mi == 1 || mi == 2);
 }
@@ -344,8 +343,7 @@ static LatGrid lat_grid(int M, int N, int K, int v) {
 
 DmaSplit lat_split_plan(int M, int N, int K, int v) {
   DmaSplit sp{0, 0, 0, 0};
-  // (the workgroup-fold variants need no workspace; 6x take one KC block only)
-  if (!lat_variant_ok(v) || v >= 90 || (v >= 60 && v < 70)) return sp;
+  if (!lat_variant_ok(v) || v >= 90) return sp;  // the workgroup-fold variants need no workspace
   const LatGrid g = lat_grid(M, N, K, v);
   if (g.nkb < 2) return sp;
   sp.split_tiles = (int)g.tiles;
@@ -365,7 +363,7 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   DmaDesc d = d0;
   d.stamps = nullptr;
   if (g_lat_stamps) {
-    const int64_t waves = (v >= 90 || (v >= 60 && v < 70)) ? 0 : lat_grid(d.M, d.N, d.K, v).wgs * 4;
+    const int64_t waves = v >= 90 ? 0 : lat_grid(d.M, d.N, d.K, v).wgs * 4;
     if (waves > 0 && g_lat_stamps_used + waves <= g_lat_stamps_cap) {
       d.stamps = g_lat_stamps + kLatStampWords * g_lat_stamps_used;
       g_lat_stamps_used += waves;
@@ -376,7 +374,6 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   if (!lat_variant_ok(v)) return fail(RTENHIP_INVALID_VALUE, "unknown latency GEMM variant");
   if (d.cin) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM: beta * C not supported");
   if (d.kstride <= 0 && !d.ktab4) return fail(RTENHIP_INVALID_VALUE, "latency GEMM: no K table");
-  if (v >= 60 && v < 70) return launch_gemm_pwb(d, v - 60, s);
   if (v >= 90) {
     const int mi = v - 90;
     const int subs = (d.M + 15) / 16, n16 = (d.N + 15) / 16, nkb = (d.K + LKC - 1) / LKC;

@@ -2224,12 +2224,8 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
     // gemm_lat2_kernel (variants 7x) forms 1x1 and 3x3 window offsets only.
     const bool lds_ok = ((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3)) && !getenv("RTENHIP_LAT_KTAB");
-    // gemm_pwb (variants 6x): ungrouped 1x1 convs with one KC block.
-    const bool pwb_eligible = g.kh == 1 && g.kw == 1 && g.groups == 1 && K <= 256;
-    static const bool pwb_tuned = getenv("RTENHIP_PWB") && getenv("RTENHIP_PWB")[0] == '1';  // (pending GPU validation)
     const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode) &&
-                            (lds_ok || lat_mode < 70 || lat_mode >= 80) &&
-                            (pwb_eligible || lat_mode < 60 || lat_mode >= 70);
+                            (lds_ok || lat_mode < 70 || lat_mode >= 80);
     if (lat_forced) {
       chosen = kLatCfgBase + lat_mode;
       chosen_split = true;
@@ -2307,10 +2303,9 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Latency GEMM variants (small batches: one wave per 16x16 tile and KC
       // block); their K-block fold is part of the kernel (split always on).
       if (lat_mode != 0) {
-        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74, 61, 62, 64}) {
+        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74}) {
           if (lat_mode > 0 && v != lat_mode) continue;
           if (v >= 70 && v < 80 && !lds_ok) continue;
-          if (v >= 60 && v < 70 && (!pwb_eligible || !pwb_tuned)) continue;
           const int cfg = kLatCfgBase + v;
           float* pk = nullptr;
           RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
