@@ -263,9 +263,11 @@ int orc_unary(int op, const float* x, int64_t n, float* y, float p0, float p1) {
       case ORC_RELU:
         r = rust_max(v, 0.f);
         break;
-      case ORC_CLIP:  // f32::clamp (unary_elementwise.rs:314-323)
-        r = v < p0 ? p0 : (v > p1 ? p1 : v);
+      case ORC_CLIP: {  // Clamp::clamp = max(lo).min(hi), the trait's own max / min (unary_elementwise.rs:263-323)
+        const float m = v > p0 ? v : p0;
+        r = m < p1 ? m : p1;
         break;
+      }
       case ORC_GELU:
         r = vm_gelu(v);
         break;

@@ -244,12 +244,12 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
         d.counters = a.counters;
       }
       {
-        // gemm_lat2 (variants 7x): 16-byte B copies for pointwise stride-1
+        // gemm_lat2 / gemm_lat3 (variants 7x / 8x): 16-byte B copies for pointwise stride-1
         // convs whose 4-column groups stay inside one image.
         static const bool no_bvec = getenv("RTENHIP_LAT_NO_BVEC") != nullptr;  // A/B experiments
         const int v = cfg - kLatCfgBase;
         const bool pw = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.Hp == a.oh && a.Wp == a.ow;
-        if (!no_bvec && v >= 70 && v < 80 && pw && d.P % 4 == 0 && d.x_img % 4 == 0 && d.kstride % 4 == 0 &&
+        if (!no_bvec && v >= 70 && v < 90 && pw && d.P % 4 == 0 && d.x_img % 4 == 0 && d.kstride % 4 == 0 &&
             (uintptr_t)d.x % 16 == 0)
           d.bvec = 1;
       }

@@ -48,7 +48,7 @@ __device__ __forceinline__ float pw_act(float x, int act, float lo, float hi) {
   if (act == RTENHIP_ACT_RELU) {
     x = fmaxf(x, 0.f);
   } else if (act == RTENHIP_ACT_CLIP) {
-    x = x < lo ? lo : (x > hi ? hi : x);
+    x = rust_clamp(x, lo, hi);
   } else if (act == RTENHIP_ACT_GELU) {
     x = vm_gelu(x);
   }

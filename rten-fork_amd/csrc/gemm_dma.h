@@ -120,7 +120,10 @@ bool dma_cfg_dual(int cfg);
 // Latency GEMM (gemm_lat.hip): the same DmaDesc addressing and summation
 // order, one wave per 16x16 output tile and KC block (small-batch convs).
 // variant = 10 * (waves along M: 1, 2, 4) + (16-row tiles per wave: 1, 2),
-// or 90 + (16-row tiles per wave) for the workgroup-fold kernel;
+// 71 / 72 / 74 for the LDS-staged kernel (RW = v - 70 rows x 4 / RW columns),
+// 85 / 86 for its pipelined 8-wave form (RW x CW = 2x4 / 4x2;
+// gemm_lat3_kernel), or 90 + (16-row tiles per wave) for the workgroup-fold
+// kernel;
 // A packed by launch_pack_lat; kstride > 0 selects koff(k) = k * kstride
 // (no K table); with K > 256, ws / counters sized by lat_split_plan.
 bool lat_variant_ok(int variant);

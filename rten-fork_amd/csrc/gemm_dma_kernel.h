@@ -800,7 +800,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     if (d.act == RTENHIP_ACT_RELU) {
       x = fmaxf(x, 0.f);
     } else if (d.act == RTENHIP_ACT_CLIP) {
-      x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+      x = rust_clamp(x, d.act_lo, d.act_hi);
     } else if (d.act == RTENHIP_ACT_GELU) {
       x = vm_gelu(x);
     }
@@ -811,7 +811,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   const float clip_lo = d.act_lo, clip_hi = d.act_hi;
   auto apply_act_sel = [&](float x) __attribute__((always_inline)) {
     const float r = fmaxf(x, 0.f);
-    const float c = x < clip_lo ? clip_lo : (x > clip_hi ? clip_hi : x);
+    const float c = rust_clamp(x, clip_lo, clip_hi);
     return act_relu ? r : (act_clip ? c : x);
   };
   if (VEC_FITS && d.vec4) {

@@ -234,6 +234,199 @@ __global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int
   lat_fold_finish<1>(d, sub0, kb, nkb, wt, col, e, acc, stp);
 }
 
+// Pipelined LDS-staged variant (8x): the workgroup layout of gemm_lat2_kernel
+// (RW x CW tiles of one KC block, one chain per wave, A panels and B tiles
+// staged in LDS once per workgroup), with two changes.
+//  - Phases: the block's 256 k are loaded in four phases of 64 k (4 groups),
+//    every phase's loads issued up front in k order.  Phase q goes to LDS as
+//    soon as its own loads have landed (vmcnt retires in issue order, so the
+//    compiler's wait for phase q leaves the later phases in flight), one raw
+//    s_barrier, and the chains run its 16 MFMA steps while phases q+1.. are
+//    still arriving -- the operand round trip and the chain overlap instead
+//    of adding (the stamps of gemm_lat2_kernel: loads 2.4-3.5 us, then the
+//    chain 1.4-1.8 us).  No __syncthreads: it would drain every load.
+//  - Wider workgroups: RW x CW up to 4 x 4 (64 * RW * CW threads), so a
+//    panel read from L2 / the Infinity Cache serves up to 4 chains -- at
+//    batch 1 the operand bytes per CU, not the MFMA, set the load phase.
+// Thread t of wave w stages, per phase: A float4s e = t + NT*i (panel e >> 8,
+// group (e >> 6) & 3), and B positions e = t + NT*i (tile e >> 8, group
+// w & 3, its 4 k values) -- or, with BVEC, 16-byte row pieces (tile e >> 8,
+// k row (e >> 2) & 63, column quad e & 3).  Same chains, fold and epilogue
+// as gemm_lat2_kernel, so the same bits.
+template <int RW, int CW, bool BVEC>
+__global__ __launch_bounds__(64 * RW * CW) void gemm_lat3_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
+  constexpr int NW = RW * CW, NT = 64 * NW;
+  constexpr int A_PT = 4 / CW;  // A float4 loads per thread and phase (RW * 256 / NT)
+  constexpr int B_PT = 4 / RW;  // B positions (or BVEC pieces) per thread and phase (CW * 256 / NT)
+  static_assert(RW >= 1 && RW <= 4 && CW >= 1 && CW <= 4 && A_PT * CW == 4 && B_PT * RW == 4, "tile shape");
+  __shared__ float4 lds_a[RW][LGROUPS][64];
+  __shared__ float4 lds_b[CW][LGROUPS][64];
+  float* ldsk = reinterpret_cast<float*>(&lds_b[0][0][0]);  // BVEC: [CW][LKC][16]
+  const int t = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lane = t & 63;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
+  const int o = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tn = o % wg_n;
+  const int t2 = o / wg_n;
+  const int tm = t2 % wg_m;
+  const int kb = t2 / wg_m;
+  const int K = d.K;
+  const int k0 = kb * LKC;
+  const int ng = min(LGROUPS, (K - k0 + 15) >> 4);
+  const int wr = wave / CW, wc = wave - (wave / CW) * CW;
+  const int sub0 = tm * RW + wr;
+  const int n0 = (tn * CW + wc) * 16;
+  LatStamps stp = lat_stamps_init(d, kb, sub0, n0);
+
+  typedef unsigned int lat3_u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t ar =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, (int)((int64_t)subs * nkb * LGROUPS * 64 * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
+  const int h = lane >> 4;
+  const bool linear = d.kstride > 0;
+
+  // Per-thread constants of the B copies.
+  uint32_t bcol[B_PT];  // x byte offset of this thread's column (or column quad) per position
+#pragma unroll
+  for (int i = 0; i < B_PT; i++) {
+    const int e = t + NT * i;
+    const int cw = e >> 8;
+    if constexpr (BVEC) {
+      const int n = (tn * CW + cw) * 16 + 4 * (e & 3);
+      uint32_t cb = DMA_OOB;
+      if (n < d.N) {
+        const int img = fdiv(n, d.fdP);
+        cb = (uint32_t)(((int64_t)img * d.x_img + (n - img * d.P)) * 4);
+      }
+      bcol[i] = cb;
+    } else {
+      bcol[i] = lat_col(d, (tn * CW + cw) * 16).vcol;
+    }
+  }
+  // 3x3 windows: this thread's k in phase q, step j is kq + 64 q + 4 j with
+  // kq = k0 + 16 (w & 3) + h; koff(k) for k = 9c + 3ky + kx (see lat_chain).
+  const uint32_t kq = (uint32_t)(k0 + 16 * (wave & 3) + h);
+  const int c0 = linear ? 0 : (int)(__umulhi(kq, 0x38E38E39u) >> 1);  // kq / 9
+  const int r0 = (int)kq - 9 * c0;
+  auto koff = [&](int q, int j) __attribute__((always_inline)) -> uint32_t {
+    const int k = (int)kq + 64 * q + 4 * j;
+    if (k >= K) return DMA_OOB;
+    if (linear) return (uint32_t)k * (uint32_t)d.kstride * 4u;
+    const int kk = r0 + 64 * q + 4 * j;  // < 213: (kk * 57) >> 9 == kk / 9
+    const int q9 = (kk * 57) >> 9;
+    const int rm = kk - 9 * q9;
+    const int ky = (rm * 11) >> 5;
+    const int kx = rm - 3 * ky;
+    return (uint32_t)((c0 + q9) * d.kt_plane + ky * d.kt_row + kx * d.kt_col) * 4u;
+  };
+
+  // Every phase's loads, in k order.
+  lat3_u32x4 av[4][A_PT];
+  float bv[4][BVEC ? 1 : B_PT][4];
+  lat3_u32x4 bq[4][BVEC ? B_PT : 1];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+#pragma unroll
+    for (int i = 0; i < A_PT; i++) {
+      const int e = t + NT * i;
+      const int r = e >> 8, g = 4 * q + ((e >> 6) & 3);
+      const int sub = tm * RW + r;
+      const uint32_t off =
+          (sub < subs && g < ng) ? (uint32_t)(((sub * nkb + kb) * LGROUPS + g) * 64 + lane) * 16u : DMA_OOB;
+      av[q][i] = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
+    }
+    if constexpr (BVEC) {
+#pragma unroll
+      for (int i = 0; i < B_PT; i++) {
+        const int e = t + NT * i;
+        const int k = k0 + 64 * q + ((e >> 2) & 63);
+        const uint32_t off =
+            (k < K && bcol[i] != DMA_OOB) ? bcol[i] + (uint32_t)k * (uint32_t)d.kstride * 4u : DMA_OOB;
+        bq[q][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      }
+    } else {
+      uint32_t ko[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) ko[j] = koff(q, j);
+#pragma unroll
+      for (int i = 0; i < B_PT; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          bv[q][i][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, bcol[i] + ko[j], 0, 0));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the phases' loads in k order
+  }
+
+  // Epilogue operands of this wave's tile, behind the operand loads.
+  const bool live = sub0 < subs && n0 < d.N;
+  const LatCol col = lat_col(d, n0);
+  LatEpi<1> e;
+  if (live) lat_epi_loads<1>(d, sub0, col, e);
+  __builtin_amdgcn_sched_barrier(0);
+
+  lat_f32x4 acc[1];
+  acc[0] = (lat_f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    // Phase q to LDS (the compiler waits for exactly these loads).
+#pragma unroll
+    for (int i = 0; i < A_PT; i++) {
+      const int e2 = t + NT * i;
+      lds_a[e2 >> 8][4 * q + ((e2 >> 6) & 3)][lane] =
+          make_float4(__uint_as_float(av[q][i].x), __uint_as_float(av[q][i].y), __uint_as_float(av[q][i].z),
+                      __uint_as_float(av[q][i].w));
+    }
+    if constexpr (BVEC) {
+#pragma unroll
+      for (int i = 0; i < B_PT; i++) {
+        const int e2 = t + NT * i;
+        *reinterpret_cast<float4*>(ldsk + ((e2 >> 8) * LKC + 64 * q + ((e2 >> 2) & 63)) * 16 + 4 * (e2 & 3)) =
+            make_float4(__uint_as_float(bq[q][i].x), __uint_as_float(bq[q][i].y), __uint_as_float(bq[q][i].z),
+                        __uint_as_float(bq[q][i].w));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_PT; i++) {
+        const int e2 = t + NT * i;
+        lds_b[e2 >> 8][4 * q + (wave & 3)][lane] = make_float4(bv[q][i][0], bv[q][i][1], bv[q][i][2], bv[q][i][3]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (q == 0) stp.at(2);
+    if (live) {
+#pragma unroll
+      for (int gq = 0; gq < 4; gq++) {
+        const int g = 4 * q + gq;
+        if (g < ng) {
+          const float4 a4 = lds_a[wr][g][lane];
+          float4 b4;
+          if constexpr (BVEC) {
+            const float* bp = ldsk + (wc * LKC + 16 * g + h) * 16 + (lane & 15);
+            b4 = make_float4(bp[0], bp[64], bp[128], bp[192]);  // k = 16g + 4j + h, j = 0..3
+          } else {
+            b4 = lds_b[wc][g][lane];
+          }
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b4.x, acc[0], 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b4.y, acc[0], 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b4.z, acc[0], 0, 0, 0);
+          acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b4.w, acc[0], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (!live) return;  // (after the last barrier: every wave helped stage)
+  if (stp.p) {
+    asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][3]));
+    stp.at(3);
+  }
+  const int wt = sub0 * (wg_n * CW) + (n0 >> 4);
+  lat_fold_finish<1>(d, sub0, kb, nkb, wt, col, e, acc, stp);
+}
+
 // All K blocks of one tile in one workgroup: W = min(nkb, 8) waves, wave w
 // computes blocks w, w + W, ...; the chains meet in LDS and wave 0 folds them
 // in K order -- no workspace, no arrival atomics, no round trip through the
@@ -316,7 +509,21 @@ rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float*
   return RTENHIP_OK;
 }
 
+// Pipelined LDS-staged variants (gemm_lat3_kernel): RW x CW tiles per workgroup.
+static bool lat3_shape(int v, int& rw, int& cw) {
+  // (The 4-wave shapes 1x4 / 2x2 / 4x1 and 4x4 were built and measured:
+  // slower than gemm_lat2_kernel on every ResNet-50 batch-1 conv, see
+  // profiles/r5_lat3.txt.)
+  switch (v) {
+    case 85: rw = 2; cw = 4; return true;
+    case 86: rw = 4; cw = 2; return true;
+    default: return false;
+  }
+}
+
 bool lat_variant_ok(int v) {
+  int rw, cw;
+  if (lat3_shape(v, rw, cw)) return true;
   if (v == 91 || v == 92) return true;  // workgroup fold
   if (v == 71 || v == 72 || v == 74) return true;  // LDS-staged, RW = v - 70 rows x CW = 4 / RW columns
   const int wmw = v / 10, mi = v % 10;
@@ -330,7 +537,9 @@ struct LatGrid {
 static LatGrid lat_grid(int M, int N, int K, int v) {
   // (LDS-staged variants: RW row tiles x CW column tiles per workgroup, one each per wave)
   const bool lds = v >= 70 && v < 80;
-  const int wmw = lds ? v - 70 : v / 10, mi = lds ? 1 : v % 10, wnw = 4 / wmw;
+  int rw3 = 0, cw3 = 0;
+  const bool p3 = lat3_shape(v, rw3, cw3);
+  const int wmw = p3 ? rw3 : (lds ? v - 70 : v / 10), mi = (lds || p3) ? 1 : v % 10, wnw = p3 ? cw3 : 4 / wmw;
   LatGrid g;
   g.subs = (M + 15) / 16;
   g.wg_m = (g.subs + wmw * mi - 1) / (wmw * mi);
@@ -348,7 +557,7 @@ DmaSplit lat_split_plan(int M, int N, int K, int v) {
   if (g.nkb < 2) return sp;
   sp.split_tiles = (int)g.tiles;
   sp.nkb = g.nkb;
-  sp.ws_floats = g.tiles * g.nkb * ((v >= 70 && v < 80) ? 1 : v % 10) * 256;
+  sp.ws_floats = g.tiles * g.nkb * ((v >= 70 && v < 90) ? 1 : v % 10) * 256;
   sp.counters = g.tiles;
   return sp;
 }
@@ -363,7 +572,9 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   DmaDesc d = d0;
   d.stamps = nullptr;
   if (g_lat_stamps) {
-    const int64_t waves = v >= 90 ? 0 : lat_grid(d.M, d.N, d.K, v).wgs * 4;
+    int rw3 = 1, cw3 = 4;
+    lat3_shape(v, rw3, cw3);
+    const int64_t waves = v >= 90 ? 0 : lat_grid(d.M, d.N, d.K, v).wgs * rw3 * cw3;
     if (waves > 0 && g_lat_stamps_used + waves <= g_lat_stamps_cap) {
       d.stamps = g_lat_stamps + kLatStampWords * g_lat_stamps_used;
       g_lat_stamps_used += waves;
@@ -391,6 +602,23 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   const LatGrid g = lat_grid(d.M, d.N, d.K, v);
   if (g.wgs > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM grid too large");
   if (g.nkb > 1 && (!d.ws || !d.counters)) return fail(RTENHIP_INVALID_VALUE, "latency GEMM needs its K-block workspace");
+  int rw3 = 0, cw3 = 0;
+  if (lat3_shape(v, rw3, cw3)) {
+    if (d.kstride <= 0 && !d.k3x3) return fail(RTENHIP_UNSUPPORTED_VALUE, "LDS latency GEMM: 1x1 or 3x3 windows only");
+    const dim3 grid((unsigned)g.wgs), blk(64 * rw3 * cw3);
+#define LAT3(R, C)                                                                                        \
+  if (rw3 == R && cw3 == C) {                                                                             \
+    if (d.bvec)                                                                                           \
+      hipLaunchKernelGGL((gemm_lat3_kernel<R, C, true>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);  \
+    else                                                                                                  \
+      hipLaunchKernelGGL((gemm_lat3_kernel<R, C, false>), grid, blk, 0, s, d, g.wg_m, g.wg_n, g.nkb, g.subs); \
+  }
+    LAT3(2, 4)
+    LAT3(4, 2)
+#undef LAT3
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   if (v >= 70 && v < 80) {
     if (d.kstride <= 0 && !d.k3x3) return fail(RTENHIP_UNSUPPORTED_VALUE, "LDS latency GEMM: 1x1 or 3x3 windows only");
     const dim3 grid((unsigned)g.wgs), blk(256);

@@ -21,6 +21,7 @@
 // accumulator per 256-deep block and folds it into a running sum at every
 // block boundary: results are bit-identical to RTen's CPU GEMM.
 #include "common.h"
+#include "vecmath.h"
 
 #include <algorithm>
 
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_mfma_kernel(GemmDesc d, int til
         if (d.act == RTENHIP_ACT_RELU) {
           x = fmaxf(x, 0.f);
         } else if (d.act == RTENHIP_ACT_CLIP) {
-          x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+          x = rust_clamp(x, d.act_lo, d.act_hi);
         }
         if (full_tile || (ncol_ok && ml <= m_lim)) d.out[idx] = x;
       }
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(256) void gemm_kfold_kernel(GemmDesc d, const float
   if (d.act == RTENHIP_ACT_RELU) {
     x = fmaxf(x, 0.f);
   } else if (d.act == RTENHIP_ACT_CLIP) {
-    x = x < d.act_lo ? d.act_lo : (x > d.act_hi ? d.act_hi : x);
+    x = rust_clamp(x, d.act_lo, d.act_hi);
   }
   d.out[(int64_t)m * d.out_m + n] = x;
 }

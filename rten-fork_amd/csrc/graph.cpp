@@ -2222,10 +2222,10 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
                            (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32)) ||
                            (direct_lds_ok && (pw_valu_mode == kPwDirect + 116 || pw_valu_mode == kPwDirect + 132));
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
-    // gemm_lat2_kernel (variants 7x) forms 1x1 and 3x3 window offsets only.
+    // gemm_lat2_kernel / gemm_lat3_kernel (variants 7x / 8x) form 1x1 and 3x3 window offsets only.
     const bool lds_ok = ((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3)) && !getenv("RTENHIP_LAT_KTAB");
     const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode) &&
-                            (lds_ok || lat_mode < 70 || lat_mode >= 80);
+                            (lds_ok || lat_mode < 70 || lat_mode >= 90);
     if (lat_forced) {
       chosen = kLatCfgBase + lat_mode;
       chosen_split = true;
@@ -2303,9 +2303,11 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Latency GEMM variants (small batches: one wave per 16x16 tile and KC
       // block); their K-block fold is part of the kernel (split always on).
       if (lat_mode != 0) {
-        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74}) {
+        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74, 85, 86}) {
           if (lat_mode > 0 && v != lat_mode) continue;
-          if (v >= 70 && v < 80 && !lds_ok) continue;
+          if (v >= 70 && v < 90 && !lds_ok) continue;
+          static const bool lat3_off = getenv("RTENHIP_LAT3") && getenv("RTENHIP_LAT3")[0] == '0';  // A/B runs
+          if (v >= 80 && v < 90 && lat3_off) continue;
           const int cfg = kLatCfgBase + v;
           float* pk = nullptr;
           RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));

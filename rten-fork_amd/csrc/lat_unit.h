@@ -98,14 +98,19 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
 
   // A: packed [subtile][kb][group][lane] float4 (launch_pack_lat: zero past
   // K inside a block); subtiles past M read past the buffer, which returns 0.
-  // Every load below is issued unconditionally, A then B, so a unit pays one
-  // memory round trip (a guarded load would be a branch and a wait each).
+  // B: step s = 4g + j covers k = k0 + 4s + h for this lane.
+  // Every load below is issued unconditionally (a guarded load would be a
+  // branch and a wait each), group by group in k order -- A then B of group
+  // g -- so the chain's first steps wait only for group 0 (vmcnt retires in
+  // issue order) and run while the later groups are still in flight.
   typedef unsigned int lat_u32x4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t ar =
       __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, (int)((int64_t)subs * nkb * LGROUPS * 64 * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
   lat_u32x4 av[LGROUPS][MI];
+  float bv[LKC / 4];
 #pragma unroll
-  for (int g = 0; g < LGROUPS; g++)
+  for (int g = 0; g < LGROUPS; g++) {
 #pragma unroll
     for (int mi = 0; mi < MI; mi++) {
       const uint32_t off = (sub0 + mi < subs && g < ng)
@@ -113,12 +118,6 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
                                : DMA_OOB;
       av[g][mi] = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
     }
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
-
-  // B: step s = 4g + j covers k = k0 + 4s + h for this lane.
-  float bv[LKC / 4];
-#pragma unroll
-  for (int g = 0; g < LGROUPS; g++) {
     uint32_t ko[4];
     if (linear || k3) {
 #pragma unroll
@@ -139,6 +138,7 @@ __device__ __forceinline__ void lat_chain(const DmaDesc& d, const int sub0, cons
 #pragma unroll
     for (int j = 0; j < 4; j++)
       bv[4 * g + j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, col.vcol + ko[j], 0, 0));
+    __builtin_amdgcn_sched_barrier(0);  // keep the groups' loads in k order
   }
 
   if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // timing experiments only
@@ -233,7 +233,7 @@ __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, con
         x = vm_gelu(x);
       } else {
         const float rl = fmaxf(x, 0.f);
-        const float cl = x < lo ? lo : (x > hi ? hi : x);
+        const float cl = rust_clamp(x, lo, hi);
         x = act_relu ? rl : (act_clip ? cl : x);
       }
       if (m < d.M) {

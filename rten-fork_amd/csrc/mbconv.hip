@@ -72,7 +72,9 @@ __host__ __device__ inline int ed_plane(int rows_in, int W) { return kEdZs + row
 // holding copysign(0, -w): its product is exactly -0, and x + (-0) == x for
 // every x (+-0, inf and NaN included), so adding it is the skip -- for finite
 // w.  A channel with a non-finite tap weight takes the select path instead.
-template <int CIN, int S, int CP, int PLANE, int NQ>
+// CLIPS: both activations are Clip (MobileNetV2's ReLU6), compiled in rather
+// than selected per value at run time.
+template <int CIN, int S, int CP, int PLANE, int NQ, bool CLIPS>
 __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   extern __shared__ float4 ed_lds4[];
   float* lds = reinterpret_cast<float*>(ed_lds4);
@@ -139,6 +141,7 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   const bool e_act_relu = d.act_e == RTENHIP_ACT_RELU, e_act_clip = d.act_e == RTENHIP_ACT_CLIP;
   const bool d_act_relu = d.act_d == RTENHIP_ACT_RELU, d_act_clip = d.act_d == RTENHIP_ACT_CLIP;
   auto act = [](float v, bool relu, bool clip, float lo, float hi) __attribute__((always_inline)) {
+    if constexpr (CLIPS) return rust_clamp(v, lo, hi);
     const float r = rust_max(v, 0.f);
     const float c = rust_clamp(v, lo, hi);
     return relu ? r : (clip ? c : v);
@@ -460,11 +463,15 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
   dim3 grid((unsigned)bands, (unsigned)N, (unsigned)chunks);
   // Compile-time planes for MobileNetV2's pairs (features.2 / .3 / .4 / .5-6 / .7).
   const int nq = (int)((d.TR * OW + 255) / 256);  // depthwise outputs per thread and channel
-#define ED_PL(C, SS, PL, Q)                                                                   \
-  if (cin == C && S == SS && plane == PL && nq <= Q) {                                       \
-    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, PL, Q>), grid, dim3(256), lds, s, d);   \
-    RTENHIP_LAUNCH_CHECK();                                                                  \
-    return RTENHIP_OK;                                                                       \
+  const bool clips = act_e == RTENHIP_ACT_CLIP && act_d == RTENHIP_ACT_CLIP;
+#define ED_PL(C, SS, PL, Q)                                                                       \
+  if (cin == C && S == SS && plane == PL && nq <= Q) {                                           \
+    if (clips)                                                                                   \
+      hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, PL, Q, true>), grid, dim3(256), lds, s, d);  \
+    else                                                                                         \
+      hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, PL, Q, false>), grid, dim3(256), lds, s, d); \
+    RTENHIP_LAUNCH_CHECK();                                                                      \
+    return RTENHIP_OK;                                                                           \
   }
   ED_PL(16, 2, 1028, 1)
   ED_PL(24, 1, 1028, 4)
@@ -474,7 +481,7 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
 #undef ED_PL
 #define ED_CASE(C, SS) \
   if (cin == C && S == SS) { \
-    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, 0, kEdMaxQ>), grid, dim3(256), lds, s, d); \
+    hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, 0, kEdMaxQ, false>), grid, dim3(256), lds, s, d); \
     RTENHIP_LAUNCH_CHECK(); \
     return RTENHIP_OK; \
   }

@@ -221,9 +221,14 @@ __device__ __forceinline__ float sqrt_rn(float x) {
 // f32::max (NaN operand -> the other operand), as Relu uses it.
 __device__ __forceinline__ float rust_max(float a, float b) { return fmaxf(a, b); }
 
-// f32::clamp(lo, hi): NaN stays NaN.
-__device__ __forceinline__ float rust_clamp(float x, float lo, float hi) {
-  return x < lo ? lo : (x > hi ? hi : x);
+// Clip: RTen's Clamp::clamp (src/ops/unary_elementwise.rs:263-291), i.e.
+// self.max(lo).min(hi) with the trait's own max (self > val ? self : val) and
+// min (self < val ? self : val) -- not f32::clamp: NaN becomes lo (then
+// min(lo, hi)), and a zero equal to a bound becomes that bound's zero
+// (Clip(0, 6) maps -0 to +0).
+__host__ __device__ __forceinline__ float rust_clamp(float x, float lo, float hi) {
+  const float m = x > lo ? x : lo;
+  return m < hi ? m : hi;
 }
 
 }  // namespace rtenhip

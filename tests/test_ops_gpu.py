@@ -313,7 +313,23 @@ def test_unary_bitexact(rh, oracle, op):
 
 def test_clip_bitexact(rh, oracle):
     x = rnd(oracle, 72, 1001, scale=20.0)
+    x[:8] = np.array([np.nan, -0.0, 0.0, np.inf, -np.inf, 6.0, -1e-30, 7.0], np.float32)
     assert_bits(host(rh.clip(dev(x), 0.0, 6.0)), oracle.clip(x, 0.0, 6.0), "clip")
+    assert_bits(host(rh.clip(dev(x), -1.0, 0.0)), oracle.clip(x, -1.0, 0.0), "clip upper zero")
+
+
+@pytest.mark.parametrize("batch", [1, 2])
+def test_conv_clip_nan(rh, oracle, batch):
+    """NaN conv outputs through the fused Clip epilogue become lo, as RTen's
+    Clamp::clamp makes them (the DMA GEMM at batch 2, the latency GEMM at 1)."""
+    x = rnd(oracle, 73, batch, 32, 10, 10)
+    x[0, 3, 4, 4] = np.nan
+    w = rnd(oracle, 74, 48, 32, 3, 3, scale=0.3)
+    b = rnd(oracle, 75, 48)
+    exp = oracle.clip(oracle.conv(x, w, b, pads=(1, 1, 1, 1)), 0.0, 6.0)
+    assert np.isnan(oracle.conv(x, w, b, pads=(1, 1, 1, 1))).any()
+    got = host(rh.conv(dev(x), dev(w), dev(b), padding=(1, 1, 1, 1), act="clip", act_range=(0.0, 6.0)))
+    assert_bits(got, exp, "conv+clip with NaN")
 
 
 @pytest.mark.parametrize("op", ["Add", "Sub", "Mul", "Div"])

@@ -399,6 +399,25 @@ def test_elementwise_vs_torch(oracle):
     expect_equal(oracle.unary("Sigmoid", x), torch.sigmoid(xt).numpy(), atol=1e-7)
     expect_equal(oracle.unary("Tanh", x), torch.tanh(xt).numpy(), atol=1e-7)
     expect_equal(oracle.clip(x, 0.0, 6.0), np.clip(x, 0, 6))
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def test_clip_clamp_trait_semantics(oracle):
+    """Clip is RTen's Clamp::clamp = self.max(lo).min(hi) with the trait's own
+    max (self > val ? self : val) and min (self < val ? self : val)
+    (src/ops/unary_elementwise.rs:263-323): NaN -> lo, and a zero that equals a
+    bound takes that bound's zero -- unlike f32::clamp / np.clip."""
+    nan, inf = np.float32(np.nan), np.float32(np.inf)
+    x = np.array([nan, -0.0, 0.0, 7.0, -3.0, 6.0, inf, -inf, 2.5], np.float32)
+    assert (_bits(oracle.clip(x, 0.0, 6.0)) == _bits([0.0, 0.0, 0.0, 6.0, 0.0, 6.0, 6.0, 0.0, 2.5])).all()
+    # Upper bound +0: -0 (not below -1) compares equal to +0, so min returns hi = +0.
+    y = np.array([nan, -0.0, 0.5, -2.0, -0.5], np.float32)
+    assert (_bits(oracle.clip(y, -1.0, 0.0)) == _bits([-1.0, 0.0, 0.0, -1.0, -0.5])).all()
+    # Lower bound -0: +0 is not greater than -0, so max returns lo = -0.
+    assert (_bits(oracle.clip(np.array([0.0], np.float32), -0.0, 1.0)) == _bits([-0.0])).all()
     a = oracle.xorshift(1, 2 * 3 * 4).reshape(2, 3, 4)
     b = oracle.xorshift(2, 4)
     assert np.array_equal(oracle.add(a, b), a + b)
