@@ -121,6 +121,8 @@ bool dma_cfg_dual(int cfg);
 // order, one wave per 16x16 output tile and KC block (small-batch convs).
 // variant = 10 * (waves along M: 1, 2, 4) + (16-row tiles per wave: 1, 2),
 // 71 / 72 / 74 for the LDS-staged kernel (RW = v - 70 rows x 4 / RW columns),
+// 61 / 62 / 63 / 66 for the slab kernel (RW x CW = 1x4, 2x4, 1x8, 2x8;
+// gemm_lat4_kernel: one image, a KC block's input planes staged in LDS),
 // 85 / 86 for its pipelined 8-wave form (RW x CW = 2x4 / 4x2;
 // gemm_lat3_kernel), or 90 + (16-row tiles per wave) for the workgroup-fold
 // kernel;

@@ -427,6 +427,195 @@ __global__ __launch_bounds__(64 * RW * CW) void gemm_lat3_kernel(DmaDesc d, int 
   lat_fold_finish<1>(d, sub0, kb, nkb, wt, col, e, acc, stp);
 }
 
+// Slab variant (6x), for one-image convs whose KC block reads few input
+// values -- the 3x3 convs at 14x14 / 7x7 and the 1x1 convs at 7x7 of
+// ResNet-50 at batch 1.  The B operand of such a block is im2col of at most
+// 30 (3x3) or 256 (1x1) input planes of 81..256 floats, and every column tile
+// of the block reads the same planes.  So a workgroup copies those planes --
+// one contiguous run [c_lo * plane, c_hi * plane) of the (zero-bordered)
+// input, 16-byte loads -- into LDS with its RW packed A panels, and forms
+// every B operand from LDS: lane (c, h) at step s reads slab[colF(n) +
+// koffF(k) - base], the same element the gather kernels load from memory
+// (k past K and columns past N read a zero slot).  B then costs one linear
+// copy per workgroup instead of a 4-byte gather per element and column tile,
+// and the workgroup covers CW column tiles (4 or 8) x RW row tiles, one chain
+// per wave.  Chains, fold and epilogue as gemm_lat2_kernel: the same bits.
+template <int RW, int CW>
+__global__ __launch_bounds__(64 * RW * CW) void gemm_lat4_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
+  constexpr int NW = RW * CW, NT = 64 * NW;
+  constexpr int A_PT = RW * LGROUPS * 64 / NT;  // A float4 loads per thread (16 / CW)
+  static_assert(A_PT * NT == RW * LGROUPS * 64, "A split");
+  extern __shared__ float4 l4_lds[];
+  float4* lds_a = l4_lds;                                             // [RW][16 groups][64 lanes]
+  float* slab = reinterpret_cast<float*>(l4_lds + RW * LGROUPS * 64);  // the block's input planes, then a zero slot
+  const int t = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lane = t & 63;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
+  const int o = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int tn = o % wg_n;
+  const int t2 = o / wg_n;
+  const int tm = t2 % wg_m;
+  const int kb = t2 / wg_m;
+  const int K = d.K;
+  const int k0 = kb * LKC;
+  const int ng = min(LGROUPS, (K - k0 + 15) >> 4);
+  const int wr = wave / CW, wc = wave - (wave / CW) * CW;
+  const int sub0 = tm * RW + wr;
+  const int n0 = (tn * CW + wc) * 16;
+  const int h = lane >> 4;
+  LatStamps stp = lat_stamps_init(d, kb, sub0, n0);
+
+  // The block's planes: channels [c_lo, c_hi), copied from the 16-byte
+  // aligned element base4 <= c_lo * plane (base4 in the slab is index 0).
+  const bool linear = d.kstride > 0;
+  const int plane = linear ? d.kstride : d.kt_plane;
+  const int k_last = min(K, k0 + LKC) - 1;
+  const int c_lo = linear ? k0 : k0 / 9;
+  const int c_hi = (linear ? k_last : k_last / 9) + 1;
+  const int base4 = (c_lo * plane) & ~3;
+  const int n4 = ((c_hi * plane + 3) & ~3) - base4 >> 2;  // float4s
+  const int zslot = n4 * 4;
+
+  typedef unsigned int lat4_u32x4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t ar =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.apk, 0, (int)((int64_t)subs * nkb * LGROUPS * 64 * 16), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)d.x, 0, (int)d.x_bytes, 0x00020000);
+  lat4_u32x4 av[A_PT];
+#pragma unroll
+  for (int i = 0; i < A_PT; i++) {
+    const int e = t + NT * i;
+    const int r = e >> 10, gl = e & 1023;
+    const int sub = tm * RW + r;
+    const uint32_t off =
+        (sub < subs && ((gl >> 6) < ng)) ? (uint32_t)(((sub * nkb + kb) * LGROUPS * 64 + gl) * 16) : DMA_OOB;
+    av[i] = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
+  }
+  // The slab: 8 loads in flight per thread per round (one round for the
+  // 7x7 planes, two or three at 14x14 with 256 threads).
+  constexpr int SU = 8;
+  for (int i0 = t; i0 < n4; i0 += SU * NT) {
+    lat4_u32x4 v[SU];
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+      const int i = i0 + u * NT;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(xr, i < n4 ? (uint32_t)(base4 + 4 * i) * 4u : DMA_OOB, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < SU; u++) {
+      const int i = i0 + u * NT;
+      if (i < n4)
+        reinterpret_cast<float4*>(slab)[i] = make_float4(__uint_as_float(v[u].x), __uint_as_float(v[u].y),
+                                                         __uint_as_float(v[u].z), __uint_as_float(v[u].w));
+    }
+  }
+  if (t == 0) slab[zslot] = 0.f;
+#pragma unroll
+  for (int i = 0; i < A_PT; i++) {
+    const int e = t + NT * i;
+    lds_a[e] = make_float4(__uint_as_float(av[i].x), __uint_as_float(av[i].y), __uint_as_float(av[i].z),
+                           __uint_as_float(av[i].w));
+  }
+
+  // This lane's B address at step s (k = k0 + 4s + h): colF(n) - base4 +
+  // koffF(k).  A column past N reads any slab element (its outputs are never
+  // stored); a k past K (only in the last, partial group) the zero slot, as
+  // A is zero there and the slab may not cover it.
+  const bool live = sub0 < subs && n0 < d.N;
+  const LatCol col = lat_col(d, n0);
+  const int colF = (col.vcol != DMA_OOB ? (int)(col.vcol >> 2) : 0) - base4;
+  LatEpi<1> e;
+  if (live) lat_epi_loads<1>(d, sub0, col, e);
+  __syncthreads();
+  if (!live) return;  // (after the barrier: every wave helped stage)
+  stp.at(2);
+
+  lat_f32x4 acc[1];
+  acc[0] = (lat_f32x4){0.f, 0.f, 0.f, 0.f};
+  const bool kpart = ((K - k0) & 15) != 0;  // the last group is partial
+  // Group g + 1's LDS reads are issued before group g's MFMAs.
+  auto chain = [&](auto addr_of) __attribute__((always_inline)) {
+    auto ld = [&](int g, float4& a4, float (&b)[4]) __attribute__((always_inline)) {
+      a4 = lds_a[(wr * LGROUPS + g) * 64 + lane];
+      int ad[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) ad[j] = addr_of(4 * g + j);
+      if (kpart && g == ng - 1) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) ad[j] = k0 + 16 * g + 4 * j + h < K ? ad[j] : zslot;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) b[j] = slab[ad[j]];
+    };
+    float4 an;
+    float bn[4];
+    ld(0, an, bn);
+#pragma unroll
+    for (int g = 0; g < LGROUPS; g++) {
+      if (g < ng) {
+        const float4 a4 = an;
+        const float b0 = bn[0], b1 = bn[1], b2 = bn[2], b3 = bn[3];
+        if (g + 1 < LGROUPS && g + 1 < ng) ld(g + 1, an, bn);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, b0, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, b1, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, b2, acc[0], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, b3, acc[0], 0, 0, 0);
+      }
+    }
+  };
+  if (linear) {
+    const int lb = colF + (k0 + h) * d.kstride;
+    const int s4 = 4 * d.kstride;
+    chain([&](int st) { return lb + st * s4; });
+  } else {
+    // 3x3 windows: koffF(k) for k = 9c + 3ky + kx at k0 + h + 4s, s = 0..8;
+    // koffF(k + 36) = koffF(k) + 4 plane.
+    int lb[9];
+    const uint32_t kh0 = (uint32_t)(k0 + h);
+    const int c0 = (int)(__umulhi(kh0, 0x38E38E39u) >> 1);
+    const int r0 = (int)kh0 - 9 * c0;
+#pragma unroll
+    for (int s9 = 0; s9 < 9; s9++) {
+      const int kk = r0 + 4 * s9;
+      const int q = (kk * 57) >> 9;
+      const int rm = kk - 9 * q;
+      const int ky = (rm * 11) >> 5;
+      const int kx = rm - 3 * ky;
+      lb[s9] = colF + (c0 + q) * d.kt_plane + ky * d.kt_row + kx * d.kt_col;
+    }
+    const int p4 = 4 * d.kt_plane;
+    chain([&](int st) { return lb[st % 9] + (st / 9) * p4; });
+  }
+  if (stp.p) {
+    asm volatile("" ::"v"(acc[0][0]), "v"(acc[0][3]));
+    stp.at(3);
+  }
+  const int wt = sub0 * (wg_n * CW) + (n0 >> 4);
+  lat_fold_finish<1>(d, sub0, kb, nkb, wt, col, e, acc, stp);
+}
+
+// Slab variants: LDS floats of the largest KC block's input planes (with the
+// alignment slack and the zero slot), 0 when the conv does not qualify (more
+// than one image, or no 1x1 / 3x3 window).
+constexpr int64_t kLatSlabCap = 13312;  // 52 KB of planes
+
+int64_t lat_slab_floats(const DmaDesc& d) {
+  if (d.N != d.P) return 0;
+  const bool linear = d.kstride > 0;
+  if (!linear && !d.k3x3) return 0;
+  const int64_t plane = linear ? d.kstride : d.kt_plane;
+  int64_t best = 0;
+  for (int k0 = 0; k0 < d.K; k0 += LKC) {
+    const int k_last = (d.K < k0 + LKC ? d.K : k0 + LKC) - 1;
+    const int64_t c_lo = linear ? k0 : k0 / 9, c_hi = (linear ? k_last : k_last / 9) + 1;
+    const int64_t b4 = (c_lo * plane) & ~int64_t(3);
+    const int64_t n = ((c_hi * plane + 3) & ~int64_t(3)) - b4;
+    if (n + 4 > best) best = n + 4;
+  }
+  return best;
+}
+
 // All K blocks of one tile in one workgroup: W = min(nkb, 8) waves, wave w
 // computes blocks w, w + W, ...; the chains meet in LDS and wave 0 folds them
 // in K order -- no workspace, no arrival atomics, no round trip through the
@@ -521,9 +710,20 @@ static bool lat3_shape(int v, int& rw, int& cw) {
   }
 }
 
+// Slab variants (gemm_lat4_kernel): RW x CW tiles per workgroup.
+static bool lat4_shape(int v, int& rw, int& cw) {
+  switch (v) {
+    case 61: rw = 1; cw = 4; return true;
+    case 62: rw = 2; cw = 4; return true;
+    case 63: rw = 1; cw = 8; return true;
+    case 66: rw = 2; cw = 8; return true;
+    default: return false;
+  }
+}
+
 bool lat_variant_ok(int v) {
   int rw, cw;
-  if (lat3_shape(v, rw, cw)) return true;
+  if (lat3_shape(v, rw, cw) || lat4_shape(v, rw, cw)) return true;
   if (v == 91 || v == 92) return true;  // workgroup fold
   if (v == 71 || v == 72 || v == 74) return true;  // LDS-staged, RW = v - 70 rows x CW = 4 / RW columns
   const int wmw = v / 10, mi = v % 10;
@@ -538,7 +738,7 @@ static LatGrid lat_grid(int M, int N, int K, int v) {
   // (LDS-staged variants: RW row tiles x CW column tiles per workgroup, one each per wave)
   const bool lds = v >= 70 && v < 80;
   int rw3 = 0, cw3 = 0;
-  const bool p3 = lat3_shape(v, rw3, cw3);
+  const bool p3 = lat3_shape(v, rw3, cw3) || lat4_shape(v, rw3, cw3);
   const int wmw = p3 ? rw3 : (lds ? v - 70 : v / 10), mi = (lds || p3) ? 1 : v % 10, wnw = p3 ? cw3 : 4 / wmw;
   LatGrid g;
   g.subs = (M + 15) / 16;
@@ -557,7 +757,7 @@ DmaSplit lat_split_plan(int M, int N, int K, int v) {
   if (g.nkb < 2) return sp;
   sp.split_tiles = (int)g.tiles;
   sp.nkb = g.nkb;
-  sp.ws_floats = g.tiles * g.nkb * ((v >= 70 && v < 90) ? 1 : v % 10) * 256;
+  sp.ws_floats = g.tiles * g.nkb * ((v >= 60 && v < 90) ? 1 : v % 10) * 256;
   sp.counters = g.tiles;
   return sp;
 }
@@ -573,7 +773,7 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   d.stamps = nullptr;
   if (g_lat_stamps) {
     int rw3 = 1, cw3 = 4;
-    lat3_shape(v, rw3, cw3);
+    if (!lat3_shape(v, rw3, cw3)) lat4_shape(v, rw3, cw3);
     const int64_t waves = v >= 90 ? 0 : lat_grid(d.M, d.N, d.K, v).wgs * rw3 * cw3;
     if (waves > 0 && g_lat_stamps_used + waves <= g_lat_stamps_cap) {
       d.stamps = g_lat_stamps + kLatStampWords * g_lat_stamps_used;
@@ -603,6 +803,28 @@ rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {
   if (g.wgs > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM grid too large");
   if (g.nkb > 1 && (!d.ws || !d.counters)) return fail(RTENHIP_INVALID_VALUE, "latency GEMM needs its K-block workspace");
   int rw3 = 0, cw3 = 0;
+  if (lat4_shape(v, rw3, cw3)) {
+    const int64_t slab = lat_slab_floats(d);
+    if (slab <= 0 || slab > kLatSlabCap)
+      return fail(RTENHIP_UNSUPPORTED_VALUE, "slab latency GEMM: one image and a 1x1 / 3x3 window whose planes fit LDS");
+    const size_t lds = (size_t)rw3 * LGROUPS * 64 * 16 + (size_t)slab * 4;
+    const dim3 grid((unsigned)g.wgs), blk(64 * rw3 * cw3);
+#define LAT4(R, C)                                                                                          \
+  if (rw3 == R && cw3 == C) {                                                                               \
+    static const bool attr = hipFuncSetAttribute((const void*)gemm_lat4_kernel<R, C>,                        \
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) ==   \
+                             hipSuccess;                                                                    \
+    (void)attr;                                                                                             \
+    hipLaunchKernelGGL((gemm_lat4_kernel<R, C>), grid, blk, lds, s, d, g.wg_m, g.wg_n, g.nkb, g.subs);       \
+  }
+    LAT4(1, 4)
+    LAT4(2, 4)
+    LAT4(1, 8)
+    LAT4(2, 8)
+#undef LAT4
+    RTENHIP_LAUNCH_CHECK();
+    return RTENHIP_OK;
+  }
   if (lat3_shape(v, rw3, cw3)) {
     if (d.kstride <= 0 && !d.k3x3) return fail(RTENHIP_UNSUPPORTED_VALUE, "LDS latency GEMM: 1x1 or 3x3 windows only");
     const dim3 grid((unsigned)g.wgs), blk(64 * rw3 * cw3);

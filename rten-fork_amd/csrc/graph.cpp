@@ -2224,8 +2224,16 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
     // gemm_lat2_kernel / gemm_lat3_kernel (variants 7x / 8x) form 1x1 and 3x3 window offsets only.
     const bool lds_ok = ((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3)) && !getenv("RTENHIP_LAT_KTAB");
+    // gemm_lat4_kernel (variants 6x): one image, and the planes of a KC block
+    // (at most 30 channels of a 3x3 conv, 256 of a 1x1) fit the LDS slab
+    // (a bound on lat_slab_floats: padded planes, alignment slack).
+    const int64_t slab_plane = (int64_t)(g.H + g.pads[0] + g.pads[2]) * (g.W + g.pads[1] + g.pads[3]);
+    const int64_t slab_span = std::min<int64_t>(g.C / g.groups, (g.kh == 3 && g.kw == 3) ? 30 : 256);
+    const bool slab_ok = lds_ok && g.N == 1 && g.groups == 1 && slab_span * slab_plane + 8 <= 13312 &&
+                         ((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3));
     const bool lat_forced = !pw_forced && lat_mode > 0 && lat_variant_ok(lat_mode) &&
-                            (lds_ok || lat_mode < 70 || lat_mode >= 90);
+                            (lds_ok || lat_mode < 70 || lat_mode >= 90) &&
+                            (slab_ok || lat_mode < 60 || lat_mode >= 70);
     if (lat_forced) {
       chosen = kLatCfgBase + lat_mode;
       chosen_split = true;
@@ -2303,11 +2311,13 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       // Latency GEMM variants (small batches: one wave per 16x16 tile and KC
       // block); their K-block fold is part of the kernel (split always on).
       if (lat_mode != 0) {
-        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74, 85, 86}) {
+        for (int v : {41, 21, 11, 42, 22, 12, 91, 92, 71, 72, 74, 85, 86, 61, 62, 63, 66}) {
           if (lat_mode > 0 && v != lat_mode) continue;
           if (v >= 70 && v < 90 && !lds_ok) continue;
           static const bool lat3_off = getenv("RTENHIP_LAT3") && getenv("RTENHIP_LAT3")[0] == '0';  // A/B runs
           if (v >= 80 && v < 90 && lat3_off) continue;
+          static const bool slab_off = getenv("RTENHIP_LAT_SLAB") && getenv("RTENHIP_LAT_SLAB")[0] == '0';  // A/B runs
+          if (v >= 60 && v < 70 && (!slab_ok || slab_off)) continue;
           const int cfg = kLatCfgBase + v;
           float* pk = nullptr;
           RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
