@@ -171,7 +171,7 @@ def traffic_bytes(model, batch):
     rocprofv3 PMC summary of this workload (scripts/gpu_prof.sh ->
     tools/pmc_traffic.py --marker): FETCH_SIZE x2 (gfx950) + WRITE_SIZE,
     eager forwards.  (None, None) when no summary exists for this workload."""
-    for rnd in ("r4", "r3"):
+    for rnd in ("r5", "r4", "r3"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic_{model}_b{batch}.json")
         if not os.path.exists(path):
             continue
