@@ -34,8 +34,13 @@ def main():
     rows = list(csv.DictReader(open(path)))
     # (bench.py's per-op timing runs hold the stream with rtenhip::hold_kernel
     # until their plan is queued: a timing artefact, not part of a forward.)
-    rows = [r for r in rows if "hold_kernel" not in r["Kernel_Name"]]
+    # They follow the timed replays and run eagerly with an event around every
+    # op (each event a cache flush, so their kernels run slower): the steady
+    # state is the stretch before the first of them.
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    first_hold = next((i for i, r in enumerate(rows) if "hold_kernel" in r["Kernel_Name"]), None)
+    if first_hold is not None:
+        rows = rows[:first_hold]
     names = [r["Kernel_Name"] for r in rows]
     # smallest period p of the trailing sequence that repeats at least twice
     period = None
