@@ -63,6 +63,16 @@ constexpr int kEdZs = 16;    // floats before a plane's interior: the 9 zero slo
 // Expand plane size in floats (zero slots, rows_in rows of W, a tail margin).
 __host__ __device__ inline int ed_plane(int rows_in, int W) { return kEdZs + rows_in * W + 4; }
 
+// Position of input column ix within an expand plane row.  At stride 2 a row
+// is stored de-interleaved -- the even columns, then the odd ones -- so the
+// taps of consecutive outputs (columns 2 ox - 1, 2 ox, 2 ox + 1) are
+// consecutive LDS words instead of every other one (2-way bank conflicts).
+template <int S>
+__device__ __forceinline__ int ed_col(int ix, int W) {
+  if constexpr (S == 2) return (ix & 1) * (W >> 1) + (ix >> 1);
+  return ix;
+}
+
 // CP channels per pass (one barrier per pass); PLANE = ed_plane(...) when
 // compile-time (every LDS offset an immediate), 0 = runtime.  The block's
 // expand and depthwise weights and biases are staged in LDS once; each
@@ -123,7 +133,7 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
     const int o = t + 256 * q;
     const int ol = o / d.OW, ox = o - ol * d.OW;
     const int oy = oy0 + ol;
-    const int base = kEdZs + ol * S * d.W + ox * S - d.pl;  // tap (0, 0), LDS row ol * S
+    const int rbase = kEdZs + ol * S * d.W;  // LDS row ol * S
     uint32_t m = o < n_out ? 1u << 9 : 0u;  // bit 9: an output of this band
 #pragma unroll
     for (int ky = 0; ky < 3; ky++) {
@@ -133,7 +143,7 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
       for (int kx = 0; kx < 3; kx++) {
         const bool on = o < n_out && row_ok && ox >= d.omin[kx] && ox < d.omax[kx];
         m |= on ? 1u << (ky * 3 + kx) : 0u;
-        taddr[q][ky * 3 + kx] = on ? base + ky * d.W + kx : ky * 3 + kx;
+        taddr[q][ky * 3 + kx] = on ? rbase + ky * d.W + ed_col<S>(ox * S + kx - d.pl, d.W) : ky * 3 + kx;
       }
     }
     tmask[q] = m;
@@ -177,7 +187,13 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
         v.y = act(v.y, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
         v.z = act(v.z, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
         v.w = act(v.w, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
-        *(float4*)(ebuf + j * plane + kEdZs + er * d.W + ec) = v;
+        float* erow = ebuf + j * plane + kEdZs + er * d.W;
+        if constexpr (S == 2) {  // de-interleaved row: even columns, then odd ones (see ed_col)
+          *(float2*)(erow + (ec >> 1)) = make_float2(v.x, v.z);
+          *(float2*)(erow + (d.W >> 1) + (ec >> 1)) = make_float2(v.y, v.w);
+        } else {
+          *(float4*)(erow + ec) = v;
+        }
       }
     }
     if (t < 9 * CP) {  // zero slots: copysign(0, -w) per tap
