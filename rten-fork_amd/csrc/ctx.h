@@ -120,6 +120,14 @@ bool conv_direct_valu_eligible(const ConvPlan& g, bool padded_out);
 bool conv_direct_lds_eligible(const ConvPlan& g, bool padded_out);
 rtenhip_status conv_direct_valu(const ConvDmaArgs& a, int mc, hipStream_t s);
 constexpr int kPwDirect = 300;
+// Network stems on MFMA with the im2col in LDS (conv_stem.hip): C = 3, 7x7 or
+// 3x3, stride 2, ungrouped, M <= 64, no residual / BN, unpadded input and
+// output; variant kPwStem.  Weights packed [K pair][2][M rounded to 32].
+constexpr int kPwStem = 800;
+bool conv_stem_eligible(const ConvPlan& g, bool padded_out);
+int64_t stem_weight_floats(int64_t M, int64_t K);
+rtenhip_status pack_stem_weights(const float* w, int64_t M, int64_t K, float* out, hipStream_t s);
+rtenhip_status conv_stem(const ConvDmaArgs& a, hipStream_t s);
 rtenhip_status conv_pw_valu(const ConvDmaArgs& a, int variant, hipStream_t s);
 // DMA-config numbers at and above this select the pointwise VALU kernel,
 // variant cfg - kPwCfgBase (graph tuner).

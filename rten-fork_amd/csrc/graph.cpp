@@ -2170,14 +2170,20 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   const bool direct_ok = n.fused_bn < 0 && pin == p.padded.end() && conv_direct_valu_eligible(g, pout != p.padded.end()) &&
                          (uintptr_t)a.y % 16 == 0 && (!a.residual || (uintptr_t)a.residual % 16 == 0);
   const bool direct_lds_ok = direct_ok && conv_direct_lds_eligible(g, pout != p.padded.end());
+  static const bool stem_off = getenv("RTENHIP_STEM") && getenv("RTENHIP_STEM")[0] == '0';  // A/B runs
+  const bool stem_ok = !stem_off && n.fused_bn < 0 && pin == p.padded.end() && !a.residual &&
+                       conv_stem_eligible(g, pout != p.padded.end());
   auto launch = [&]() -> rtenhip_status {
+    if (a.cfg == kPwCfgBase + kPwStem) return conv_stem(a, s);
     if (a.cfg >= kPwCfgBase + kPwDirect) return conv_direct_valu(a, a.cfg - kPwCfgBase - kPwDirect, s);
     return a.cfg >= kPwCfgBase ? conv_pw_valu(a, a.cfg - kPwCfgBase, s) : conv_dma(ctx, a);
   };
   auto weight_floats = [&](int cfg) {
+    if (cfg == kPwCfgBase + kPwStem) return stem_weight_floats(g.O, K);
     return cfg >= kPwCfgBase ? pw_weight_floats(g.O, K) : packed_conv_weight_floats(g, cfg);
   };
   auto pack_for = [&](int cfg, float* out) -> rtenhip_status {
+    if (cfg == kPwCfgBase + kPwStem) return pack_stem_weights(w, g.O, K, out, s);
     return cfg >= kPwCfgBase ? pack_pw_weights(w, g.O, K, out, s) : pack_conv_weights(ctx, w, g, cfg, out);
   };
   auto bind = [&](const ConvExec& e) {
@@ -2220,7 +2226,8 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     (void)hipStreamIsCapturing(s, &cs);
     const bool pw_forced = (pw_ok && pw_valu_mode > 0 && pw_valu_mode < kPwDirect && pw_variant_ok(pw_valu_mode, K)) ||
                            (direct_ok && (pw_valu_mode == kPwDirect + 16 || pw_valu_mode == kPwDirect + 32)) ||
-                           (direct_lds_ok && (pw_valu_mode == kPwDirect + 116 || pw_valu_mode == kPwDirect + 132));
+                           (direct_lds_ok && (pw_valu_mode == kPwDirect + 116 || pw_valu_mode == kPwDirect + 132)) ||
+                           (stem_ok && pw_valu_mode == kPwStem);
     if (pw_forced) chosen = kPwCfgBase + pw_valu_mode;
     // gemm_lat2_kernel / gemm_lat3_kernel (variants 7x / 8x) form 1x1 and 3x3 window offsets only.
     const bool lds_ok = ((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3)) && !getenv("RTENHIP_LAT_KTAB");
@@ -2357,9 +2364,9 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           cands.push_back({ms, cfg, 0, 0, pk});
         }
       }
-      if (direct_ok && pw_valu_mode != 0) {
+      if ((direct_ok || stem_ok) && pw_valu_mode != 0) {
         // The DMA candidates' times exclude the padded copy of the input
-        // they need (made once above); the direct kernel pads in place.
+        // they need (made once above); the direct and stem kernels pad in place.
         float pad_ms = 0;
         if (has_pad && a.xin != a.x_unpadded) {
           std::vector<float> ts;
@@ -2380,8 +2387,10 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           for (Cand& c : cands)
             if (c.cfg < kPwCfgBase) c.ms += pad_ms;
         }
-        for (int mc : {16, 32, 116, 132}) {
-          if (mc >= 100 && !direct_lds_ok) continue;
+        for (int mc : {16, 32, 116, 132, kPwStem - kPwDirect}) {
+          if (mc < kPwStem - kPwDirect && !direct_ok) continue;
+          if (mc >= 100 && mc < 200 && !direct_lds_ok) continue;
+          if (mc == kPwStem - kPwDirect && !stem_ok) continue;
           const int cfg = kPwCfgBase + kPwDirect + mc;
           float* pk = nullptr;
           RTENHIP_HIP_CHECK(hipMalloc(&pk, (size_t)weight_floats(cfg) * 4));
@@ -2930,7 +2939,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           const long long gm = cg.O, gn = cg.N * cg.oh * cg.ow, gk = cg.KC * cg.kh * cg.kw;
           const double fl = 2.0 * gm * (double)gn * gk;
           const int cc = ce->second.cfg;
-          const std::string cname = cc >= kPwCfgBase   ? "valu" + std::to_string(cc - kPwCfgBase)
+          const std::string cname = cc == kPwCfgBase + kPwStem ? std::string("stem")
+                                    : cc >= kPwCfgBase       ? "valu" + std::to_string(cc - kPwCfgBase)
                                     : is_lat_cfg(cc) ? "lat" + std::to_string(cc - kLatCfgBase)
                                                      : std::to_string(cc);
           snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%s%s%s %.1f TF/s", gm, gn, gk,

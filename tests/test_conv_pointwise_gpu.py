@@ -309,3 +309,79 @@ def test_expand_depthwise_fused_bitexact(rh, monkeypatch, case, policy):
         assert fused == ((C in (16, 24) or (C == 32 and s == 2)) and W % 4 == 0), g.timing_report()
 
 
+
+# Network stems on MFMA (csrc/conv_stem.hip), forced with RTENHIP_PW_VALU=800:
+# (N, C, H, W, O, k, pads, tail, bias)
+STEM_CASES = [
+    (2, 3, 32, 32, 64, 7, [3, 3, 3, 3], "relu", True),      # ResNet-50 stem, small
+    (1, 3, 224, 224, 64, 7, [3, 3, 3, 3], "relu", True),    # ResNet-50 stem, full size
+    (2, 3, 224, 224, 32, 3, [1, 1, 1, 1], "clip", True),    # MobileNetV2 stem, full size
+    (3, 3, 19, 23, 24, 3, [1, 1, 1, 1], "none", False),     # odd sizes, M < 32, no bias
+    (2, 3, 30, 17, 48, 7, [2, 3, 3, 1], "clip", True),      # asymmetric pads, partial 32-row tile
+    (2, 3, 4, 4, 64, 7, [3, 3, 3, 3], "relu", True),        # 2x2 output
+    (1, 3, 150, 250, 16, 3, [0, 0, 1, 1], "relu", True),    # OW = 125: partial column tile
+]
+
+
+@pytest.mark.parametrize("case", STEM_CASES, ids=lambda c: "x".join(map(str, c[:6])) + f"-{c[7]}")
+def test_stem_mfma_bitexact(rh, monkeypatch, case):
+    """The stem kernel gives the oracle's bits (one KC block, k in im2col
+    order from +0, then bias and the fused Relu / Clip), eager and replayed."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, C, H, W, O, k, pads, tail, bias = case
+    monkeypatch.setenv("RTENHIP_PW_VALU", "800")
+    rng = np.random.default_rng(H * 7 + O + k)
+    m = ModelSpec("stem")
+    x = m.value("x")
+    m.inputs = ["x"]
+    ins = {"x": rng.uniform(-1, 1, (N, C, H, W)).astype(np.float32)}
+    args = [x, m.const("w", rng.uniform(-0.5, 0.5, (O, C, k, k)).astype(np.float32))]
+    if bias:
+        args.append(m.const("b", rng.uniform(-0.2, 0.2, (O,)).astype(np.float32)))
+    y = m.op("Conv", args, {"pads": pads, "strides": [2, 2]})
+    if tail == "relu":
+        y = m.op("Relu", [y])
+    elif tail == "clip":
+        y = m.op("Clip", [y, m.const("lo", np.array(0, np.float32)), m.const("hi", np.array(6, np.float32))])
+    m.outputs = [y]
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    dev = {g.input_ids[0]: torch.from_numpy(ins["x"]).cuda()}
+    out = None
+    for _ in range(3):  # eager, capture, replay
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        o = out[0].cpu().numpy()
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+    g.set_timing(True)
+    g.run(dev, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    assert "cfg=stem" in g.timing_report(), g.timing_report()
+
+
+@pytest.mark.parametrize("model", ["resnet50", "mobilenet_v2"])
+def test_model_stem_mfma(rh, monkeypatch, model):
+    """ResNet-50 / MobileNetV2 (batch 2) with the stem forced onto the MFMA
+    stem kernel (every other conv tuned as usual): oracle bits."""
+    import torch
+    import graph_runner
+    from rten_hip import models
+
+    monkeypatch.setenv("RTENHIP_PW_VALU", "800")
+    spec = getattr(models, model)()
+    x = np.random.default_rng(21).random((2, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {spec.inputs[0]: x})[spec.outputs[0]]
+    g = spec.to_graph()
+    xd = torch.from_numpy(x).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
+    g.set_timing(True)
+    g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    assert g.timing_report().count("cfg=stem") == 1, g.timing_report()
