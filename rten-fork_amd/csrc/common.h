@@ -171,6 +171,13 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
                                 float* y, int N, int cin, int hidden, int H, int W, int OH, int OW, int S, int pt,
                                 int pl, int act_e, float lo_e, float hi_e, int act_d, float lo_d, float hi_d,
                                 hipStream_t s);
+// Fused 3x3 depthwise (+bias, act) -> 1x1 projection (+bias, residual, act)
+// (dw_project.hip): stride 1, pads 1, C = 32, W = 112, M <= 32.
+bool dw_project_eligible(int C, int H, int W, int M, int S, int pt, int pl, int pb, int pr);
+rtenhip_status launch_dw_project(const float* x, const float* wd, const float* bd, int act_d, float lo_d,
+                                 float hi_d, const float* wp, const float* bp, const float* res, int act_p,
+                                 float lo_p, float hi_p, float* y, int N, int C, int H, int W, int M,
+                                 hipStream_t s);
 // ReduceMean (norm.hip): rows of `len` contiguous elements in slice_sum order,
 // or per output element an iter_sum over a strided sub-block (up to 8 kept
 // and 8 reduced dims).

@@ -780,6 +780,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (nodes[op].fused_residual >= 0) uses[nodes[op].fused_residual]++;
     auto ef = p.expand_fused.find(op);
     if (ef != p.expand_fused.end()) uses[ef->second]++;
+    auto df = p.dwpw_fused.find(op);
+    if (df != p.dwpw_fused.end()) uses[df->second]++;
   }
   std::set<int> outset(out_ids.begin(), out_ids.end());
 
@@ -823,6 +825,33 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.expand_fused[op] = e.inputs[0];
       drop.push_back(n.fe_op);
     }
+    // Depthwise -> projection pairs (Node::fd_op): the depthwise op leaves
+    // the plan, the projection op runs both.
+    const bool dwpw_off = getenv("RTENHIP_DW_PROJECT") && getenv("RTENHIP_DW_PROJECT")[0] == '0';  // A/B runs (read per plan)
+    for (int op : p.ops) {
+      const Node& n = nodes[op];
+      if (dwpw_off || n.op_type != "Conv" || n.fd_op < 0 || !in_plan.count(n.fd_op) ||
+          std::find(drop.begin(), drop.end(), n.fd_op) != drop.end() || p.expand_fused.count(n.fd_op))
+        continue;
+      const Node& dn = nodes[n.fd_op];
+      if (dn.outputs.size() != 1 || n.inputs[0] != dn.outputs[0] || outset0.count(dn.outputs[0]) ||
+          uses_of_value(p.ops, dn.outputs[0]) != 1)
+        continue;
+      const Shape* xs = shape_of(dn.inputs[0]);
+      const Shape& ys = shapes[n.outputs[0]];
+      if (!xs || xs->size() != 4 || ys.size() != 4 || p.dtypes[dn.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
+      ConvAttrs da = conv_attrs(dn, false);
+      int64_t ohw[2], fp[4];
+      const bool ok = da.mode == 0 && da.dil == std::vector<int64_t>{1, 1} && da.strides == std::vector<int64_t>{1, 1} &&
+                      output_size_and_padding((*xs)[2], (*xs)[3], 3, 3, 1, 1, 0, da.pads.data(), 1, 1, ohw, fp) ==
+                          RTENHIP_OK &&
+                      ys[2] == ohw[0] && ys[3] == ohw[1] && ys[0] == (*xs)[0] &&
+                      dw_project_eligible((int)(*xs)[1], (int)(*xs)[2], (int)(*xs)[3], (int)ys[1], 1, (int)fp[0],
+                                          (int)fp[1], (int)fp[2], (int)fp[3]);
+      if (!ok) continue;
+      p.dwpw_fused[op] = dn.inputs[0];
+      drop.push_back(n.fd_op);
+    }
     if (!drop.empty()) {
       std::vector<int> kept;
       for (int op : p.ops)
@@ -832,7 +861,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   }
   for (int op : p.ops) {
     const Node& n = nodes[op];
-    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op)) continue;
+    if (n.op_type != "Conv" || n.inputs.size() < 2 || p.expand_fused.count(op) || p.dwpw_fused.count(op)) continue;
     const Shape* xs = shape_of(n.inputs[0]);
     const Shape* ws = shape_of(n.inputs[1]);
     if (!xs || !ws || nodes[n.inputs[1]].kind != NodeKind::Constant) continue;
@@ -1061,6 +1090,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       // (fused expand ops read their input through these maps, not inputs)
       auto ef = p.expand_fused.find(op);
       if (ef != p.expand_fused.end()) readers[ef->second].push_back(op);
+      auto df = p.dwpw_fused.find(op);
+      if (df != p.dwpw_fused.end()) readers[df->second].push_back(op);
     }
     for (auto& kv : p.convs) {
       if (kv.second.fc) continue;
@@ -1118,7 +1149,7 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       auto cd = p.convs.find(ds);
       if (dn.op_type != "Conv" || cd == p.convs.end() || cd->second.fc || cd->second.g.groups != 1 ||
           dn.fused_residual >= 0 || dn.fused_act || dn.fused_bn >= 0 || outset.count(v) || uses[v] != 1 ||
-          p.conv_unfused.count(ds) || p.expand_fused.count(ds) || p.padded.count(v))
+          p.conv_unfused.count(ds) || p.expand_fused.count(ds) || p.dwpw_fused.count(ds) || p.padded.count(v))
         continue;
       const ConvPlan& gd = cd->second.g;
       const bool ds_pad = gd.pads[0] || gd.pads[1] || gd.pads[2] || gd.pads[3];
@@ -1255,6 +1286,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (n.fused_residual >= 0) drop_use(n.fused_residual);
     auto ef = p.expand_fused.find(op);
     if (ef != p.expand_fused.end()) drop_use(ef->second);
+    auto df = p.dwpw_fused.find(op);
+    if (df != p.dwpw_fused.end()) drop_use(df->second);
     auto cdu = p.conv_dual.find(op);
     if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
     // An output nobody reads is released right after its producer.
@@ -1357,6 +1390,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     return c.ops[0] == op_id ? exec_chain(p, c) : RTENHIP_OK;  // members run inside the chain's launch
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
+  if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_project(p, op_id);
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
   if (t == "MatMul" && p.mm_group_skip.count(op_id)) return RTENHIP_OK;  // computed by its group's leader
   if (t == "Conv" && p.conv_dual.count(op_id)) {
@@ -1615,6 +1649,25 @@ rtenhip_status Graph::exec_expand_dw(Plan& p, int op_id) {
                           ptr_of(p, n.outputs[0]), (int)xs[0], (int)xs[1], (int)ys[1], (int)xs[2], (int)xs[3],
                           (int)ys[2], (int)ys[3], (int)ca.strides[0], (int)fp[0], (int)fp[1], e.fused_act, e.act_lo,
                           e.act_hi, n.fused_act, n.act_lo, n.act_hi, ctx->stream);
+}
+
+// Depthwise (3x3) -> projection (1x1) pair (Node::fd_op) the plan runs as one
+// dw_project.hip launch, reading the depthwise conv's input.
+rtenhip_status Graph::exec_dw_project(Plan& p, int op_id) {
+  const Node& n = nodes[op_id];
+  const Node& dn = nodes[n.fd_op];
+  const int xv = p.dwpw_fused[op_id];
+  const Shape* xsp = plan_shape(*this, p, xv);
+  const Shape* ysp = plan_shape(*this, p, n.outputs[0]);
+  if (!xsp || !ysp) return fail(RTENHIP_HIP_ERROR, "depthwise+projection: missing shapes");
+  const Shape& xs = *xsp;
+  const Shape& ys = *ysp;
+  const float* bd = dn.inputs.size() > 2 && dn.inputs[2] >= 0 ? ptr_of(p, dn.inputs[2]) : nullptr;
+  const float* bp = n.inputs.size() > 2 && n.inputs[2] >= 0 ? ptr_of(p, n.inputs[2]) : nullptr;
+  const float* res = n.fused_residual >= 0 ? ptr_of(p, n.fused_residual) : nullptr;
+  return launch_dw_project(ptr_of(p, xv), ptr_of(p, dn.inputs[1]), bd, dn.fused_act, dn.act_lo, dn.act_hi,
+                           ptr_of(p, n.inputs[1]), bp, res, n.fused_act, n.act_lo, n.act_hi, ptr_of(p, n.outputs[0]),
+                           (int)xs[0], (int)xs[1], (int)xs[2], (int)xs[3], (int)ys[1], ctx->stream);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -2871,6 +2924,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
             (n.fused_residual >= 0 || n.fused_act || n.fused_colbias >= 0 || n.fused_bn >= 0))
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
+        if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+project)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
@@ -3215,6 +3269,38 @@ rtenhip_status Graph::optimize() {
                                                          nodes[dn.inputs[2]].kind != NodeKind::Constant))
       continue;
     dn.fe_op = i;
+    fused++;
+  }
+  // Depthwise 3x3 Conv (+ its fused activation) whose only consumer is a 1x1
+  // projection Conv (+ bias, residual, activation) -> one node running both
+  // (dw_project.hip) where the plan's shapes allow.
+  for (int i = 0; i < (int)nodes.size(); i++) {
+    Node& dn = nodes[i];
+    if (dn.kind != NodeKind::Operator || dn.removed || dn.op_type != "Conv" || dn.fused_residual >= 0 ||
+        dn.fused_bn >= 0 || dn.fe_op >= 0 || dn.outputs.size() != 1 || dn.inputs.size() < 2 || !dn.input_perm.empty())
+      continue;
+    const int dwv = dn.inputs[1];
+    if (dwv < 0 || nodes[dwv].kind != NodeKind::Constant || nodes[dwv].shape.size() != 4 ||
+        nodes[dwv].shape[1] != 1 || nodes[dwv].shape[2] != 3 || nodes[dwv].shape[3] != 3 ||
+        (int64_t)dn.attrs.num("groups", 1) != nodes[dwv].shape[0] ||
+        (dn.inputs.size() > 2 && dn.inputs[2] >= 0 && nodes[dn.inputs[2]].kind != NodeKind::Constant))
+      continue;
+    const int p_op = sole(dn.outputs[0]);
+    if (p_op < 0) continue;
+    Node& pn = nodes[p_op];
+    if (pn.removed || pn.op_type != "Conv" || pn.fused_bn >= 0 || pn.fe_op >= 0 || pn.fd_op >= 0 ||
+        pn.inputs.size() < 2 || pn.inputs[0] != dn.outputs[0] || !pn.input_perm.empty())
+      continue;
+    const int pwv = pn.inputs[1];
+    if (pwv < 0 || nodes[pwv].kind != NodeKind::Constant || nodes[pwv].shape.size() != 4 ||
+        nodes[pwv].shape[1] != nodes[dwv].shape[0] || nodes[pwv].shape[2] != 1 || nodes[pwv].shape[3] != 1 ||
+        (pn.inputs.size() > 2 && pn.inputs[2] >= 0 && nodes[pn.inputs[2]].kind != NodeKind::Constant))
+      continue;
+    ConvAttrs pa = conv_attrs(pn, false);
+    if (pa.mode != 0 || pa.groups != 1 || pa.pads != std::vector<int64_t>{0, 0, 0, 0} ||
+        pa.strides != std::vector<int64_t>{1, 1} || pa.dil != std::vector<int64_t>{1, 1})
+      continue;
+    pn.fd_op = i;
     fused++;
   }
   // FusedTranspose (optimize.rs:329-378): a MatMul reads a Transpose's input

@@ -110,6 +110,11 @@ struct Node {
   // fused kernel takes (mbconv.hip) drops that op and runs both here, reading
   // the expand's input; otherwise both run as they are.
   int fe_op = -1;
+  // The mirror pair: a 1x1 projection Conv whose input is a depthwise 3x3
+  // Conv's output read by nothing else (MobileNetV2's features.1).  A plan
+  // whose shapes dw_project.hip takes drops the depthwise op and runs both
+  // here, reading the depthwise conv's input.
+  int fd_op = -1;
   // MatMul epilogue: constant [N] added per column after the K fold
   // (MatMul -> Add(bias)), before the residual and the activation.
   int fused_colbias = -1;
@@ -196,6 +201,9 @@ struct Plan {
   // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
   // the expand's input value, which the depthwise op then reads.
   std::map<int, int> expand_fused;
+  // Projection convs running their depthwise conv too (see Node::fd_op): op id
+  // -> the depthwise conv's input value, which the projection op then reads.
+  std::map<int, int> dwpw_fused;
   // Grouped MatMuls (MatMulExec::nseg): leader op -> members (leader first),
   // members run by their leader; the members' outputs are segments of one
   // arena block of [nseg][M][N].
@@ -394,6 +402,7 @@ struct Graph {
   rtenhip_status exec_conv_dual(Plan& p, int op_id, bool& handled);
   void conv_io_args(Plan& p, int op_id, ConvDmaArgs& a);
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
+  rtenhip_status exec_dw_project(Plan& p, int op_id);
   // Conv chains (graph_chain.cpp).
   rtenhip_status build_chains(Plan& p);
   rtenhip_status exec_chain(Plan& p, Plan::ConvChain& c);

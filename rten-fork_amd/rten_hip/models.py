@@ -189,6 +189,13 @@ def _expand_dw_fused(cin: int, h: int, w: int, stride: int = 1) -> bool:
     return banded and (cin in (16, 24) or (cin == 32 and stride == 2))
 
 
+def _dw_project_fused(c: int, h: int, w: int, m: int, stride: int) -> bool:
+    """Whether csrc/dw_project.hip runs a depthwise 3x3 -> 1x1 projection pair
+    of these shapes as one kernel (dw_project_eligible; pads 1 checked by the
+    caller through the output size)."""
+    return c == 32 and w == 112 and m <= 32 and stride == 1
+
+
 def expand_dw_pairs(spec: ModelSpec, batch: int = 1, hw: int = 224) -> int:
     """Expand -> depthwise pairs of ``spec`` the executor fuses by default."""
     return int(conv_io_bytes(spec, batch, hw, count_pairs=True))
@@ -209,21 +216,24 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224, count_pairs: bool 
     conv reads its input and weights (+ bias) once and writes its output once;
     a residual Add fused into the conv's epilogue reads its other operand once;
     Relu / Clip ride in the epilogue (no traffic); an expand -> depthwise pair
-    run as one kernel (mbconv.hip) neither writes nor reads the expand output.
+    run as one kernel (mbconv.hip) neither writes nor reads the expand output,
+    nor a depthwise -> projection pair (dw_project.hip) the depthwise output.
     The HBM-roofline figure for bandwidth-bound models (MobileNetV2,
     SURVEY.md §8d)."""
     shapes = {spec.inputs[0]: (batch, 3, hw, hw)}
     consts = {n.name: n.data.shape for n in spec.nodes if n.kind == "const"}
     producer = {o: n for n in spec.nodes if n.kind == "op" for o in n.outputs}
 
-    def source_conv(v):
-        """The 1x1 Conv behind value v (through a Clip / Relu), or None."""
+    def source_conv(v, k=(1, 1)):
+        """The k[0] x k[1] Conv behind value v (through a Clip / Relu), or None."""
         n = producer.get(v)
         if n is not None and n.op_type in ("Clip", "Relu"):
             n = producer.get(n.inputs[0])
-        if n is None or n.op_type != "Conv" or consts[n.inputs[1]][2:] != (1, 1):
+        if n is None or n.op_type != "Conv" or consts[n.inputs[1]][2:] != k:
             return None
         return n
+
+    expand_fused_dw = set()  # depthwise convs run with their expand conv
 
     fused_e, fused_d = set(), set()
     total = 0.0
@@ -244,8 +254,15 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224, count_pairs: bool 
                 ex = shapes[e.inputs[0]]
                 if _expand_dw_fused(ex[1], ex[2], ex[3], s[0]):
                     pairs += 1
+                    expand_fused_dw.add(n.name)
                     rd = 0  # the expand output never reaches HBM
                     total -= 4.0 * N * C * H * W  # nor is written by the expand
+            d = source_conv(n.inputs[0], (3, 3)) if (kh, kw) == (1, 1) and n.attrs.get("groups", 1) == 1 else None
+            if d is not None and d.name not in expand_fused_dw and d.attrs.get("groups", 1) == C:
+                dx = shapes[d.inputs[0]]
+                if dx[2:] == (H, W) and _dw_project_fused(C, H, W, o, d.attrs["strides"][0]):
+                    rd = 0  # the depthwise output never reaches HBM
+                    total -= 4.0 * N * C * H * W  # nor is written by the depthwise conv
             total += 4.0 * (rd + wr + o * ci * kh * kw + o)
             shapes[n.outputs[0]] = (N, o, oh, ow)
         elif n.op_type == "Add":

@@ -120,9 +120,13 @@ def test_mobilenet_v2_pointwise_valu(rh, monkeypatch, mode):
         rep = g.timing_report()
         m = re.search(r"Conv\(expand\+dw\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
         fused = int(m.group(1)) if m else 0
+        # and the depthwise -> projection pair (dw_project.hip), features.1
+        m2 = re.search(r"Conv\(dw\+project\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
+        assert m2 and int(m2.group(1)) == 1, rep
+        fused += 1
         # bench.py's HBM bytes (models.conv_io_bytes) assume the executor's pairs
         from rten_hip import models as _m
-        assert fused == _m.expand_dw_pairs(spec), (fused, _m.expand_dw_pairs(spec))
+        assert fused - 1 == _m.expand_dw_pairs(spec), (fused, _m.expand_dw_pairs(spec))
         assert rep.count("cfg=valu16") + fused >= 20, rep
 
 
@@ -385,3 +389,72 @@ def test_model_stem_mfma(rh, monkeypatch, model):
     g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
     torch.cuda.synchronize()
     assert g.timing_report().count("cfg=stem") == 1, g.timing_report()
+
+
+# Depthwise 3x3 -> 1x1 projection pairs run as one kernel (csrc/dw_project.hip):
+# (N, C, H, W, M, dw act, projection tail, biases)
+DW_PROJECT = [
+    (2, 32, 112, 112, 16, "clip", "none", True),       # MobileNetV2 features.1
+    (1, 32, 9, 112, 24, "relu", "relu", False),        # partial band, M not a multiple of 16
+    (3, 32, 6, 112, 32, "none", "add_clip", True),     # residual, two channel tiles
+    (1, 32, 1, 112, 16, "clip", "add", True),          # one row: both window rows skipped
+    (2, 48, 8, 112, 16, "clip", "none", True),         # C = 48: runs unfused
+]
+
+
+@pytest.mark.parametrize("case", DW_PROJECT, ids=lambda c: "x".join(map(str, c[:5])) + f"-{c[5]}-{c[6]}")
+@pytest.mark.parametrize("policy", ["on", "off"])
+def test_dw_project_fused_bitexact(rh, monkeypatch, case, policy):
+    """The fused depthwise -> projection kernel gives the two operators'
+    bits (conv_2d_depthwise_block then conv_2d_pointwise, with the graph's
+    Clip / Relu / Add after each), eager and replayed; RTENHIP_DW_PROJECT=0
+    and shapes it does not take run the two convs apart."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, C, H, W, M, act_d, tail, biases = case
+    if policy == "off":
+        monkeypatch.setenv("RTENHIP_DW_PROJECT", "0")
+    else:
+        monkeypatch.delenv("RTENHIP_DW_PROJECT", raising=False)
+    rng = np.random.default_rng(C * 5 + M + H)
+    m = ModelSpec("dwpw")
+    x = m.value("x")
+    m.inputs = ["x"]
+    lo, hi = m.const("lo", np.array(0.0, np.float32)), m.const("hi", np.array(6.0, np.float32))
+    ins = {"x": rng.uniform(-1, 2, (N, C, H, W)).astype(np.float32)}
+    wd = m.const("wd", rng.uniform(-0.5, 0.5, (C, 1, 3, 3)).astype(np.float32))
+    args = [x, wd] + ([m.const("bd", rng.uniform(-0.2, 0.2, (C,)).astype(np.float32))] if biases else [])
+    dv = m.op("Conv", args, {"pads": [1, 1, 1, 1], "strides": [1, 1], "groups": C}, name="dw")
+    if act_d == "clip":
+        dv = m.op("Clip", [dv, lo, hi])
+    elif act_d == "relu":
+        dv = m.op("Relu", [dv])
+    wp = m.const("wp", rng.uniform(-0.5, 0.5, (M, C, 1, 1)).astype(np.float32))
+    args = [dv, wp] + ([m.const("bp", rng.uniform(-0.2, 0.2, (M,)).astype(np.float32))] if biases else [])
+    y = m.op("Conv", args, {"pads": [0, 0, 0, 0], "strides": [1, 1]}, name="project")
+    if tail.startswith("add"):
+        r = m.value("r")
+        m.inputs.append("r")
+        ins["r"] = rng.uniform(-1, 1, (N, M, H, W)).astype(np.float32)
+        y = m.op("Add", [y, r])
+    if tail.endswith("clip"):
+        y = m.op("Clip", [y, lo, hi])
+    elif tail.endswith("relu"):
+        y = m.op("Relu", [y])
+    m.outputs = [y]
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
+    out = None
+    for _ in range(3):  # eager, capture, replay
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        o = out[0].cpu().numpy()
+        assert _bits_equal(o, exp), np.abs(o - exp).max()
+    g.set_timing(True)
+    g.run(dev, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    fused = "Conv(dw+project)" in g.timing_report()
+    assert fused == (policy == "on" and C == 32), g.timing_report()
