@@ -4,15 +4,16 @@
 // trip through HBM (written by the depthwise kernel, read back by the
 // projection: 2 x 205 MB at batch 128).
 //
-// A workgroup (4 waves) owns one image and 4 output rows, one per wave.  The
+// A workgroup (8 waves) owns one image and 8 output rows, one per wave.  The
 // projection is a v_mfma_f32_16x16x4_f32 chain over the channels, k-steps of 4
 // channels; lane l = 16 kq + j supplies channel 4 g + kq of pixel group j in
 // k-step g.  Its B operands are the depthwise outputs themselves: the lane
 // computes channel 4 g + kq of pixels PX j .. PX j + PX - 1 (PX = W / 16) from
 // a 3 x (PX + 2) window in LDS, and feeds them to PX MFMAs (tile p holds
 // pixels PX j + p, so each tile is 16 pixels x 16 channels).  The input rows
-// of k-step g + 1's four channels are loaded while k-step g computes (two LDS
-// buffers of 4 channels x 6 rows).
+// of k-step g + 2's four channels are loaded while k-step g computes, and
+// g + 1's stored to LDS after it (two LDS buffers of 4 channels x ROWS + 2
+// rows).
 //
 // Arithmetic (bit-identical to the two operators apart):
 // - depthwise (conv_2d_depthwise_block, src/ops/conv/depthwise.rs:49-203, as
@@ -45,21 +46,23 @@ struct DwProjDesc {
   const float* res;   // [N, M, H, W] or null
   float* y;           // [N, M, H, W]
   int C, M, H, W;
-  int bands;          // ceil(H / 4)
+  int bands;          // ceil(H / rows per workgroup)
   int act_d, act_p;
   float lo_d, hi_d, lo_p, hi_p;
 };
 
-constexpr int kDpRows = 4;  // output rows per workgroup (one per wave)
-constexpr int kDpIn = kDpRows + 2;
+// Output rows per workgroup (one per wave): 8 measured 1-2% faster than 4
+// (profiles/r5_dw_project.txt).
+constexpr int kDpRowsHost = 8;
 
-template <int G, int MT, int PX>
-__global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
+template <int G, int MT, int PX, int ROWS>  // ROWS output rows per workgroup, one per wave
+__global__ __launch_bounds__(64 * ROWS) void dw_project_kernel(DwProjDesc d) {
+  constexpr int kDpRows = ROWS, kDpIn = ROWS + 2, NTH = 64 * ROWS;
   constexpr int W = 16 * PX;
   constexpr int RS = W + 8;           // staged row: 4 floats of margin either side
   constexpr int NQ = W / 4;           // float4s per row
   constexpr int NV = 4 * kDpIn * NQ;  // float4s per k-step's staged rows
-  constexpr int NIT = (NV + 255) / 256;
+  constexpr int NIT = (NV + NTH - 1) / NTH;
   constexpr int BUF = 4 * kDpIn * RS;
   constexpr int C = 4 * G;
   extern __shared__ float4 dp_lds4[];
@@ -82,7 +85,7 @@ __global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
   auto load_step = [&](int g, dp_f32x4 (&pre)[NIT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NIT; u++) {
-      const int e = min(t + 256 * u, NV - 1);
+      const int e = min(t + NTH * u, NV - 1);
       const int cc = e / (kDpIn * NQ), rem = e - cc * (kDpIn * NQ);
       const int r = rem / NQ, q = rem - r * NQ;
       const int iy = min(max(oy0 - 1 + r, 0), H - 1);
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
   auto store_step = [&](int buf, const dp_f32x4 (&pre)[NIT]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < NIT; u++) {
-      const int e = t + 256 * u;
+      const int e = t + NTH * u;
       const int cc = e / (kDpIn * NQ), rem = e - cc * (kDpIn * NQ);
       const int r = rem / NQ, q = rem - r * NQ;
       float* dst = e < NV ? xb + buf * BUF + (cc * kDpIn + r) * RS + 4 + 4 * q : dummy;
@@ -101,10 +104,13 @@ __global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
     }
   };
 
-  dp_f32x4 pre[NIT];
-  load_step(0, pre);
-  for (int i = t; i < C * 9; i += 256) wdl[i] = d.wd[i];
-  for (int i = t; i < C; i += 256) bdl[i] = d.bd ? d.bd[i] : 0.f;
+  // Two k-steps in flight: step g + 2's rows are loaded while step g
+  // computes, step g + 1's (loaded a step earlier) stored after it.
+  dp_f32x4 pre[2][NIT];
+  load_step(0, pre[0]);
+  if (G > 1) load_step(1, pre[1]);
+  for (int i = t; i < C * 9; i += NTH) wdl[i] = d.wd[i];
+  for (int i = t; i < C; i += NTH) bdl[i] = d.bd ? d.bd[i] : 0.f;
   // The projection's A operands: W[16 mt + j][4 g + kq] (0 past M).
   float wa[G][MT];
 #pragma unroll
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
       const int m = 16 * mt + j;
       wa[g][mt] = m < d.M ? d.wp[(int64_t)m * C + 4 * g + kq] : 0.f;
     }
-  store_step(0, pre);
+  store_step(0, pre[0]);
   __syncthreads();
 
   const int oy = oy0 + wave;
@@ -128,7 +134,7 @@ __global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
 
 #pragma unroll
   for (int g = 0; g < G; g++) {
-    if (g + 1 < G) load_step(g + 1, pre);
+    if (g + 2 < G) load_step(g + 2, pre[g & 1]);
     const int c = 4 * g + kq;
     const float* wk = wdl + c * 9;
     float wv[9];
@@ -166,7 +172,7 @@ __global__ __launch_bounds__(256) void dw_project_kernel(DwProjDesc d) {
 #pragma unroll
       for (int mt = 0; mt < MT; mt++)
         acc[p][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][mt], v[p], acc[p][mt], 0, 0, 0);
-    if (g + 1 < G) store_step((g + 1) & 1, pre);
+    if (g + 1 < G) store_step((g + 1) & 1, pre[(g + 1) & 1]);
     __syncthreads();
   }
 
@@ -228,7 +234,8 @@ rtenhip_status launch_dw_project(const float* x, const float* wd, const float* b
   d.M = M;
   d.H = H;
   d.W = W;
-  d.bands = (H + kDpRows - 1) / kDpRows;
+  constexpr int R = kDpRowsHost;
+  d.bands = (H + R - 1) / R;
   d.act_d = act_d;
   d.act_p = act_p;
   d.lo_d = lo_d;
@@ -236,13 +243,12 @@ rtenhip_status launch_dw_project(const float* x, const float* wd, const float* b
   d.lo_p = lo_p;
   d.hi_p = hi_p;
   constexpr int PX = 7, G = 8;
-  const size_t lds = (size_t)(2 * 4 * kDpIn * (16 * PX + 8) + C * 9 + C + 4) * sizeof(float);
+  const size_t lds = (size_t)(2 * 4 * (R + 2) * (16 * PX + 8) + C * 9 + C + 4) * sizeof(float);
   const int64_t blocks = (int64_t)N * d.bands;
   if (blocks > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "depthwise+projection: grid too large");
-  if (M <= 16)
-    hipLaunchKernelGGL((dw_project_kernel<G, 1, PX>), dim3((unsigned)blocks), dim3(256), lds, s, d);
-  else
-    hipLaunchKernelGGL((dw_project_kernel<G, 2, PX>), dim3((unsigned)blocks), dim3(256), lds, s, d);
+  const dim3 grid((unsigned)blocks), blk(64 * R);
+  if (M <= 16) hipLaunchKernelGGL((dw_project_kernel<G, 1, PX, R>), grid, blk, lds, s, d);
+  else hipLaunchKernelGGL((dw_project_kernel<G, 2, PX, R>), grid, blk, lds, s, d);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }
