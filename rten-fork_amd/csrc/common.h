@@ -178,6 +178,14 @@ rtenhip_status launch_dw_project(const float* x, const float* wd, const float* b
                                  float hi_d, const float* wp, const float* bp, const float* res, int act_p,
                                  float lo_p, float hi_p, float* y, int N, int C, int H, int W, int M,
                                  hipStream_t s);
+// A bottleneck's conv3 (1x1, K 64 -> 256, + bias, residual, Relu) and the next
+// block's conv1 (1x1, K 256 -> 64, + bias, act) as one launch
+// (conv_pair.hip); weights packed [K / 2][2][M] by pack_pair_weights.
+bool conv_pair_eligible(int64_t P, int64_t OW, int64_t K3, int64_t M3, int64_t K1, int64_t M1);
+rtenhip_status pack_pair_weights(const float* w, int64_t M, int64_t K, float* out, hipStream_t s);
+rtenhip_status launch_conv_pair(const float* x, const float* w3p, const float* b3, const float* res, float* y3,
+                                const float* w1p, const float* b1, int act1, float* y1, int64_t y1_img,
+                                int64_t y1_c, int y1_row, int y1_off, int N, int P, int OW, int M1, hipStream_t s);
 // ReduceMean (norm.hip): rows of `len` contiguous elements in slice_sum order,
 // or per output element an iter_sum over a strided sub-block (up to 8 kept
 // and 8 reduced dims).

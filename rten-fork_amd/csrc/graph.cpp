@@ -87,6 +87,10 @@ Plan::~Plan() {
   }
   for (auto& kv : padded)
     if (kv.second.base) (void)hipFree(kv.second.base);
+  for (auto& kv : pair_exec) {
+    if (kv.second.w3p) (void)hipFree(kv.second.w3p);
+    if (kv.second.w1p) (void)hipFree(kv.second.w1p);
+  }
   for (auto& kv : matmuls) {
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
@@ -1163,6 +1167,50 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     }
   }
 
+  // conv3 -> next conv1 pairs (Plan::conv_pair, conv_pair.hip): adjacent in
+  // the plan, conv3 a 1x1 K = 64 -> 256 conv with a fused residual and Relu,
+  // conv1 a 1x1 K = 256 -> 64 conv reading conv3's output; batches of
+  // 8+ images (smaller ones run the latency GEMMs).  conv3's x and residual
+  // stay allocated until conv1's position (the pair runs at conv3's, writing
+  // conv1's output early: its block is only reused after conv1's position).
+  {
+    const char* e = getenv("RTENHIP_CONV_PAIR");  // A/B runs: 0 disables
+    const bool pair_off = e && e[0] == '0';
+    std::set<int> ds_ops;
+    for (auto& kv : p.conv_dual) ds_ops.insert(kv.second);
+    for (size_t i = 0; !pair_off && i + 1 < p.ops.size(); i++) {
+      const int o3 = p.ops[i], o1 = p.ops[i + 1];
+      auto c3 = p.convs.find(o3);
+      auto c1 = p.convs.find(o1);
+      if (c3 == p.convs.end() || c1 == p.convs.end() || c3->second.fc || c1->second.fc) continue;
+      const Node& n3 = nodes[o3];
+      const Node& n1 = nodes[o1];
+      const ConvPlan& g3 = c3->second.g;
+      const ConvPlan& g1 = c1->second.g;
+      auto plain_1x1 = [](const ConvPlan& g) {
+        return !g.one_d && g.groups == 1 && g.kh == 1 && g.kw == 1 && g.sh == 1 && g.sw == 1 && g.dh == 1 &&
+               g.dw == 1 && !g.pads[0] && !g.pads[1] && !g.pads[2] && !g.pads[3];
+      };
+      if (!plain_1x1(g3) || !plain_1x1(g1) || g3.N < 8 || g1.N != g3.N || g1.oh != g3.oh || g1.ow != g3.ow) continue;
+      if (!conv_pair_eligible(g3.oh * g3.ow, g3.ow, g3.C, g3.O, g1.C, g1.O)) continue;
+      if (n3.fused_residual < 0 || n3.fused_act != RTENHIP_ACT_RELU || n3.fused_bn >= 0 || n1.fused_residual >= 0 ||
+          n1.fused_bn >= 0 || (n1.fused_act != RTENHIP_ACT_RELU && n1.fused_act != 0) || n1.inputs[0] != n3.outputs[0])
+        continue;
+      if (p.conv_dual.count(o3) || p.conv_dual.count(o1) || ds_ops.count(o3) || ds_ops.count(o1) ||
+          p.conv_unfused.count(o3) || p.conv_unfused.count(o1) || p.conv_pair.count(p.ops[i ? i - 1 : 0]))
+        continue;
+      const int x3 = n3.inputs[0], r3 = n3.fused_residual, y3 = n3.outputs[0];
+      if (p.padded.count(x3) || p.padded.count(r3) || p.padded.count(y3) || outset.count(y3) ||
+          p.dtypes[x3] == RTENHIP_DTYPE_INT32)
+        continue;
+      p.conv_pair[o3] = o1;
+      p.pair_hold[o1] = {x3, r3};
+      uses[x3]++;
+      uses[r3]++;
+      i++;  // o1 cannot start another pair
+    }
+  }
+
   // Storage blocks with best-fit reuse; aliases share their base's block.
   struct Block {
     size_t off, size;
@@ -1290,6 +1338,11 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (df != p.dwpw_fused.end()) drop_use(df->second);
     auto cdu = p.conv_dual.find(op);
     if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
+    auto ph = p.pair_hold.find(op);
+    if (ph != p.pair_hold.end()) {
+      drop_use(ph->second.first);
+      drop_use(ph->second.second);
+    }
     // An output nobody reads is released right after its producer.
     if (block_of.count(out) && blocks[block_of[out]].refs == 0) {
       Block& b = blocks[block_of[out]];
@@ -1391,6 +1444,8 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_project(p, op_id);
+  if (t == "Conv" && p.conv_pair.count(op_id)) return exec_conv_pair(p, op_id);
+  if (t == "Conv" && p.pair_hold.count(op_id)) return RTENHIP_OK;  // run by its conv3's op
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
   if (t == "MatMul" && p.mm_group_skip.count(op_id)) return RTENHIP_OK;  // computed by its group's leader
   if (t == "Conv" && p.conv_dual.count(op_id)) {
@@ -1668,6 +1723,48 @@ rtenhip_status Graph::exec_dw_project(Plan& p, int op_id) {
   return launch_dw_project(ptr_of(p, xv), ptr_of(p, dn.inputs[1]), bd, dn.fused_act, dn.act_lo, dn.act_hi,
                            ptr_of(p, n.inputs[1]), bp, res, n.fused_act, n.act_lo, n.act_hi, ptr_of(p, n.outputs[0]),
                            (int)xs[0], (int)xs[1], (int)xs[2], (int)xs[3], (int)ys[1], ctx->stream);
+}
+
+// conv3 -> next conv1 pair (Plan::conv_pair) as one conv_pair.hip launch.
+rtenhip_status Graph::exec_conv_pair(Plan& p, int op_id) {
+  const Node& n3 = nodes[op_id];
+  const int o1 = p.conv_pair.at(op_id);
+  const Node& n1 = nodes[o1];
+  const ConvPlan& g3 = p.convs.at(op_id).g;
+  const ConvPlan& g1 = p.convs.at(o1).g;
+  hipStream_t s = ctx->stream;
+  Plan::PairExec& pe = p.pair_exec[op_id];
+  if (!pe.w3p) {
+    RTENHIP_HIP_CHECK(hipMalloc(&pe.w3p, (size_t)g3.O * g3.C * sizeof(float)));
+    RTENHIP_HIP_CHECK(hipMalloc(&pe.w1p, (size_t)g1.O * g1.C * sizeof(float)));
+    rtenhip_status st = pack_pair_weights(ptr_of(p, n3.inputs[1]), g3.O, g3.C, pe.w3p, s);
+    if (st) return st;
+    if ((st = pack_pair_weights(ptr_of(p, n1.inputs[1]), g1.O, g1.C, pe.w1p, s))) return st;
+  }
+  const float* b3 = n3.inputs.size() > 2 && n3.inputs[2] >= 0 ? ptr_of(p, n3.inputs[2]) : nullptr;
+  const float* b1 = n1.inputs.size() > 2 && n1.inputs[2] >= 0 ? ptr_of(p, n1.inputs[2]) : nullptr;
+  const int64_t P = g1.oh * g1.ow;
+  float* y1;
+  int64_t y1_img, y1_c;
+  int y1_row, y1_off;
+  auto pout = p.padded.find(n1.outputs[0]);
+  if (pout != p.padded.end()) {
+    const PaddedValue& pv = pout->second;
+    y1 = pv.base;
+    y1_c = pv.phys[2] * pv.phys[3];
+    y1_img = pv.phys[1] * y1_c;
+    y1_row = (int)pv.phys[3];
+    y1_off = (int)(pv.pads[0] * pv.phys[3] + pv.pads[1]);
+  } else {
+    y1 = ptr_of(p, n1.outputs[0]);
+    y1_c = P;
+    y1_img = g1.O * P;
+    y1_row = (int)g1.ow;
+    y1_off = 0;
+  }
+  return launch_conv_pair(ptr_of(p, n3.inputs[0]), pe.w3p, b3, ptr_of(p, n3.fused_residual), ptr_of(p, n3.outputs[0]),
+                          pe.w1p, b1, n1.fused_act, y1, y1_img, y1_c, y1_row, y1_off, (int)g3.N, (int)P, (int)g3.ow,
+                          (int)g1.O, s);
 }
 
 // FusedAttention (see Graph::optimize): attention.hip when the shapes fit
@@ -2925,6 +3022,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
         if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+project)";
+        if (plan->conv_pair.count(plan->ops[i])) key = "Conv(conv3+conv1)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";

@@ -201,6 +201,17 @@ struct Plan {
   // Depthwise convs running their expand conv too (see Node::fe_op): op id ->
   // the expand's input value, which the depthwise op then reads.
   std::map<int, int> expand_fused;
+  // A bottleneck's conv3 and the next block's conv1 as one conv_pair.hip
+  // launch at conv3's position (conv1's op then skips): conv3 op -> conv1 op;
+  // conv1 op -> the conv3 inputs it keeps allocated until then (x, residual);
+  // conv3 op -> its packed weights.
+  std::map<int, int> conv_pair;
+  std::map<int, std::pair<int, int>> pair_hold;
+  struct PairExec {
+    float* w3p = nullptr;
+    float* w1p = nullptr;
+  };
+  std::map<int, PairExec> pair_exec;
   // Projection convs running their depthwise conv too (see Node::fd_op): op id
   // -> the depthwise conv's input value, which the projection op then reads.
   std::map<int, int> dwpw_fused;
@@ -403,6 +414,7 @@ struct Graph {
   void conv_io_args(Plan& p, int op_id, ConvDmaArgs& a);
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_dw_project(Plan& p, int op_id);
+  rtenhip_status exec_conv_pair(Plan& p, int op_id);
   // Conv chains (graph_chain.cpp).
   rtenhip_status build_chains(Plan& p);
   rtenhip_status exec_chain(Plan& p, Plan::ConvChain& c);

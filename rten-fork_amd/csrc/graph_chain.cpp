@@ -61,7 +61,9 @@ rtenhip_status Graph::build_chains(Plan& p) {
     const ConvPlan& g = ce.g;
     if (ce.fc || g.groups != 1 || g.one_d) return false;
     if (!((g.kh == 1 && g.kw == 1) || (g.kh == 3 && g.kw == 3))) return false;
-    if (p.expand_fused.count(op) || p.dwpw_fused.count(op) || p.conv_unfused.count(op)) return false;
+    if (p.expand_fused.count(op) || p.dwpw_fused.count(op) || p.conv_unfused.count(op) || p.conv_pair.count(op) ||
+        p.pair_hold.count(op))
+      return false;
     const Node& n = nodes[op];
     const bool has_pad = g.pads[0] || g.pads[1] || g.pads[2] || g.pads[3];
     if (has_pad && !p.padded.count(n.inputs[0])) return false;

@@ -9,7 +9,7 @@ SUB=$2; shift 2
 R=$PWD
 cd /tmp
 timeout -s KILL 90 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $R/"$@" > $O/kt.log 2>&1 || { tail -5 $O/kt.log; exit 1; }
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $O/pmc -o run -- python3 $R/"$@" > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; exit 1; }
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $O/pmc -o run -- python3 $R/"$@" > $O/pmc.log 2>&1 || { tail -5 $O/pmc.log; exit 1; }
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc2 -o run -- python3 $R/"$@" > $O/pmc2.log 2>&1 || { tail -5 $O/pmc2.log; exit 1; }
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc3 -o run -- python3 $R/"$@" > $O/pmc3.log 2>&1 || { tail -5 $O/pmc3.log; exit 1; }
 cd $R
