@@ -159,10 +159,10 @@ def cpu_baseline(spec, seconds: float, batch: int, feed_fn):
 # Kernel families the roofline's dominant-kernel time covers, per model (the
 # ops bench.py sums: Conv / Gemm / MatMul / FusedAttention).
 _ROOF_KERNELS = {
-    "resnet50": ("gemm_dma_kernel", "gemm_lat", "gemv"),
+    "resnet50": ("gemm_dma_kernel", "gemm_lat", "gemv", "conv_stem_kernel", "conv_pair_kernel"),
     "bert": ("gemm_dma_kernel", "pack_a_kernel", "attention_kernel"),
     "mobilenet_v2": ("gemm_dma_kernel", "gemm_lat", "gemv", "conv_pw_valu_kernel", "conv_direct",
-                     "depthwise", "expand_dw_kernel"),
+                     "depthwise", "expand_dw_kernel", "dw_project_kernel", "conv_stem_kernel"),
 }
 
 
