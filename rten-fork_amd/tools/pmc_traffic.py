@@ -72,7 +72,8 @@ def marker_mode(root, runs):
         tail = [d for d in ids if d > last_marker]
         fam = defaultdict(float)
         for d in tail:
-            k = names[d].split("(")[0].split("<")[0].replace("void ", "").strip()
+            k = names[d].replace("(anonymous namespace)::", "")
+            k = k.split("(")[0].split("<")[0].replace("void ", "").strip()
             fam[k] += per[d] * 1024 * mult / runs
             fam_all[k] += per[d] * 1024 * mult / runs
         res[ctr] = {"bytes_per_forward": sum(fam.values()), "dispatches_per_forward": len(tail) / runs,

@@ -19,6 +19,7 @@ from collections import defaultdict
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"^void ", "", name)
     return re.sub(r"[<(].*$", "", name)
 
@@ -85,7 +86,7 @@ def main():
                 if f * period + i > 0:
                     prev = tail[f * period + i - 1]
                     gaps.append(int(r["Start_Timestamp"]) - int(prev["End_Timestamp"]))
-            name = re.sub(r"^void (rtenhip::)?", "", tail[i]["Kernel_Name"])
+            name = re.sub(r"^void (rtenhip::)?", "", tail[i]["Kernel_Name"].replace("(anonymous namespace)::", ""))
             name = re.sub(r"\(.*$", "", name)
             g = sum(gaps) / len(gaps) / 1e3 if gaps else 0.0
             print(f"  {i:3d} {sum(durs) / len(durs) / 1e3:8.2f} gap {g:6.2f}  {name[:90]}")
