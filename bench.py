@@ -75,7 +75,27 @@ def _git_head():
     except (OSError, subprocess.SubprocessError):
         pass
     try:
-        return open(os.path.join(ROOT, "BUILD_COMMIT")).read().strip() + " (BUILD_COMMIT)"
+        return open(os.path.join(ROOT, "BUILD_COMMIT")).read().split()[0] + " (BUILD_COMMIT)"
+    except (OSError, IndexError):
+        return None
+
+
+def _source_commit():
+    """The last commit that changed the product sources (__graft_entry__.
+    SOURCE_PATHS), or the one build() recorded in BUILD_COMMIT: a committed
+    rocprof summary taken at it describes this build's kernels."""
+    try:
+        from __graft_entry__ import SOURCE_PATHS
+
+        src = subprocess.run(["git", "-C", ROOT, "log", "-1", "--format=%h", "--abbrev=12", "--"] + SOURCE_PATHS,
+                             capture_output=True, text=True, timeout=5).stdout.strip()
+        if src:
+            return src
+    except (OSError, ImportError, subprocess.SubprocessError):
+        pass
+    try:
+        parts = open(os.path.join(ROOT, "BUILD_COMMIT")).read().split()
+        return parts[1] if len(parts) > 1 else None
     except OSError:
         return None
 
@@ -406,7 +426,8 @@ class Workload:
                             "plan is queued), capped at ms_per_step when larger (capped: true)"}
         rp = rocprof_kernel_ms(self.model, self.B)
         if rp:
-            head = (_git_head() or "").split()[0]
+            # (the summary's commit vs the last commit that changed the sources)
+            head = _source_commit() or ""
             rp["matches_head"] = bool(head and rp["commit"] and (head.startswith(rp["commit"]) or
                                                                  rp["commit"].startswith(head)))
             if self.model == "mobilenet_v2":
