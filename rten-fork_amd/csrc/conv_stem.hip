@@ -65,7 +65,10 @@ struct StemDesc {
 };
 
 constexpr int kStemThreads = 256;
-constexpr int kStemNT = 7;        // items (32 x 32 output tiles) per wave and band
+// Items (32 x 32 output tiles) per wave and band: 7 for large batches; 2 when
+// the batch has too few TR-row bands to fill the chip (batch 1: one output
+// row per band, 112 workgroups instead of 28).
+constexpr int kStemNT = 7, kStemNTSmall = 2;
 // Staged rows per wave (a bound on C R / 4, in registers while the next band
 // is loaded): ResNet-50's band (TR = 4, 3 x 13 rows of 232) needs 10;
 // MobileNetV2's gets TR = 7 (3 x 15 rows) within 12.
@@ -77,13 +80,12 @@ __device__ __forceinline__ void stem_static_for(std::integer_sequence<int, Is...
   (f(std::integral_constant<int, Is>{}), ...);
 }
 
-template <int C, int KH, int KW, int S, int MT>
+template <int C, int KH, int KW, int S, int MT, int NT>
 __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) {
   constexpr int K = C * KH * KW;
   constexpr int KP = (K + 1) & ~1;  // k pairs of the 32x32x2 MFMA
   constexpr int NS = KP / 2;
   constexpr int MW = MT * 32;       // packed channel rows
-  constexpr int NT = kStemNT;
   constexpr int SR = stem_rows_cap(KH);
   extern __shared__ float4 stem_lds4[];
   float* lds = reinterpret_cast<float*>(stem_lds4);
@@ -267,26 +269,39 @@ __global__ void pack_stem_kernel(const float* __restrict__ w, float* __restrict_
 }
 
 struct StemShape {
-  int TR, R, LW, tiles_y, stage_n;
+  int TR, R, LW, tiles_y, stage_n, NT;
 };
 int stem_mt(int64_t M) { return M <= 32 ? 1 : (M <= 64 ? 2 : 0); }
 
 // Output rows per band: the most whose tiles fit 4 waves x NT items, with the
-// staged rows within the per-thread register stage and the LDS budget.
-StemShape stem_shape(int C, int kh, int kw, int S, int OH, int OW, int64_t M) {
+// staged rows within the per-thread register stage and the LDS budget; the
+// small-item variant when the large one leaves fewer bands than 2 per CU.
+StemShape stem_shape(int C, int kh, int kw, int S, int OH, int OW, int64_t M, int64_t N, int cus) {
   StemShape e{};
   const int mt = stem_mt(M);
   if (mt == 0 || OW < 1 || OH < 1) return e;
   const int wfloats = ((C * kh * kw + 1) & ~1) * mt * 32;
   const int lw = ((OW - 1) * S + kw + 3) & ~3;
-  auto fits = [&](int tr) {
+  auto fits = [&](int tr, int nt) {
     const int tiles = (tr * OW + 31) / 32;
     const int staged = C * ((tr - 1) * S + kh) * lw;
-    return tiles * mt <= 4 * kStemNT && C * ((tr - 1) * S + kh) <= 4 * stem_rows_cap(kh) && lw <= 256 &&
+    return tiles * mt <= 4 * nt && C * ((tr - 1) * S + kh) <= 4 * stem_rows_cap(kh) && lw <= 256 &&
            wfloats + staged + 1 + mt * 32 <= kStemLdsFloats;
   };
-  int tr = 0;
-  while (tr < OH && fits(tr + 1)) tr++;
+  auto rows_for = [&](int nt) {
+    int r = 0;
+    while (r < OH && fits(r + 1, nt)) r++;
+    return r;
+  };
+  int nt = kStemNT, tr = rows_for(nt);
+  if (tr >= 1 && N * ((OH + tr - 1) / tr) < 2 * (int64_t)cus) {
+    const int trs = rows_for(kStemNTSmall);
+    if (trs >= 1) {
+      nt = kStemNTSmall;
+      tr = trs;
+    }
+  }
+  e.NT = nt;
   if (tr < 1) return e;
   e.TR = tr;
   e.R = (tr - 1) * S + kh;
@@ -313,7 +328,8 @@ bool conv_stem_eligible(const ConvPlan& g, bool padded_out) {
   const bool resnet = g.C == 3 && g.kh == 7 && g.kw == 7 && g.sh == 2 && g.sw == 2;
   const bool mnv2 = g.C == 3 && g.kh == 3 && g.kw == 3 && g.sh == 2 && g.sw == 2;
   if (!(resnet || mnv2) || g.groups != 1 || g.dh != 1 || g.dw != 1 || padded_out) return false;
-  const StemShape e = stem_shape((int)g.C, (int)g.kh, (int)g.kw, (int)g.sh, (int)g.oh, (int)g.ow, g.O);
+  const StemShape e = stem_shape((int)g.C, (int)g.kh, (int)g.kw, (int)g.sh, (int)g.oh, (int)g.ow, g.O, g.N,
+                                 stem_grid_cap() / 2);
   return e.TR > 0 && g.C * g.H * g.W < (int64_t(1) << 29) && g.N * e.tiles_y < (int64_t(1) << 31) &&
          g.N * g.O * g.oh * g.ow < (int64_t(1) << 40);
 }
@@ -336,7 +352,8 @@ rtenhip_status conv_stem(const ConvDmaArgs& a, hipStream_t s) {
   if (!(resnet || mnv2) || a.groups != 1 || a.dh != 1 || a.dw != 1 || mt == 0 || !a.x_unpadded || a.residual ||
       a.bn || a.y_off != 0 || (a.y_row != 0 && a.y_row != a.ow) || a.y_img != a.O * a.oh * a.ow)
     return fail(RTENHIP_INVALID_VALUE, "stem conv: unsupported layout");
-  const StemShape e = stem_shape((int)a.C, (int)a.kh, (int)a.kw, (int)a.sh, (int)a.oh, (int)a.ow, a.O);
+  const StemShape e = stem_shape((int)a.C, (int)a.kh, (int)a.kw, (int)a.sh, (int)a.oh, (int)a.ow, a.O, a.N,
+                                 stem_grid_cap() / 2);
   if (e.TR == 0 || a.C * a.H * a.W >= (int64_t(1) << 29) || a.N * e.tiles_y >= (int64_t(1) << 31))
     return fail(RTENHIP_UNSUPPORTED_VALUE, "stem conv: shape outside the kernel's bounds");
   StemDesc d{};
@@ -364,18 +381,24 @@ rtenhip_status conv_stem(const ConvDmaArgs& a, hipStream_t s) {
   const size_t lds = (size_t)(KP * mt * 32 + e.stage_n + 1 + mt * 32) * 4;
   const dim3 grid((unsigned)std::min(d.nbands, stem_grid_cap())), blk(kStemThreads);
   // (over 64 KiB of dynamic LDS: opted in once per instantiation)
-#define STEM_LAUNCH(KH, MT)                                                                                \
+#define STEM_LAUNCH(KH, MT, NT)                                                                            \
   {                                                                                                        \
-    static const hipError_t attr = hipFuncSetAttribute((const void*)conv_stem_kernel<3, KH, KH, 2, MT>,    \
+    static const hipError_t attr = hipFuncSetAttribute((const void*)conv_stem_kernel<3, KH, KH, 2, MT, NT>, \
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,         \
                                                        kStemLdsFloats * 4);                                \
     RTENHIP_HIP_CHECK(attr);                                                                               \
-    hipLaunchKernelGGL((conv_stem_kernel<3, KH, KH, 2, MT>), grid, blk, lds, s, d);                        \
+    hipLaunchKernelGGL((conv_stem_kernel<3, KH, KH, 2, MT, NT>), grid, blk, lds, s, d);                    \
   }
-  if (resnet && mt == 2) STEM_LAUNCH(7, 2)
-  else if (resnet) STEM_LAUNCH(7, 1)
-  else if (mt == 1) STEM_LAUNCH(3, 1)
-  else STEM_LAUNCH(3, 2)
+  const bool small = e.NT == kStemNTSmall;
+  if (resnet && mt == 2) {
+    if (small) STEM_LAUNCH(7, 2, kStemNTSmall) else STEM_LAUNCH(7, 2, kStemNT)
+  } else if (resnet) {
+    if (small) STEM_LAUNCH(7, 1, kStemNTSmall) else STEM_LAUNCH(7, 1, kStemNT)
+  } else if (mt == 1) {
+    if (small) STEM_LAUNCH(3, 1, kStemNTSmall) else STEM_LAUNCH(3, 1, kStemNT)
+  } else {
+    if (small) STEM_LAUNCH(3, 2, kStemNTSmall) else STEM_LAUNCH(3, 2, kStemNT)
+  }
 #undef STEM_LAUNCH
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
