@@ -19,13 +19,16 @@
 //   2. a band is TR * OW pixels = tiles of 32 pixels x MT tiles of 32
 //      channels; item (tile, m) = tile * MT + m, wave w takes items w, w + 4,
 //      ... (NT of them, one channel tile m per wave), each a
-//      v_mfma_f32_32x32x2_f32 chain over k = (c, ky, kx): the B operand of
+//      v_mfma_f32_32x32x2_f32 chain over k = (c, ky, kx): the A operand of
 //      lane (pixel j, half h) at step s is the LDS word
 //      pix(j) + off(2 s + h), off(k) = c R LW + ky LW + kx, with (c, ky, kx)
 //      compile-time constants (the step loop is unrolled; k = K reads a zero
-//      slot), the A operand one LDS word of the weights packed
+//      slot), the B operand one LDS word of the weights packed
 //      [k pair][half][channel]; operands are loaded PD steps ahead;
-//   3. bias, activation, and 16 stores per lane of 32 contiguous pixels.
+//   3. bias, activation, and (MT = 2) 4 stores per lane and item of 4
+//      adjacent pixels: pixels are the MFMA's rows (A and B above swap), so
+//      an accumulator register group holds 4 of them; with MT = 1, 16 stores
+//      per lane of 32 contiguous pixels.
 // The host picks TR so that a band is at most 4 NT items (ResNet-50: TR = 4,
 // 14 tiles x 2 -- seven items per wave; MobileNetV2: TR = 7, 25 tiles x 1).
 // Measured (ResNet-50 b64 stem, profiles/r5_stem_mfma.txt): 0.194 ms per
@@ -62,6 +65,7 @@ struct StemDesc {
   int stage_n;      // C * R * LW staged floats
   int act;
   float lo, hi;
+  int vec;          // OW % 4 == 0 and y 16-byte aligned: 4-pixel vector stores
 };
 
 constexpr int kStemThreads = 256;
@@ -87,6 +91,9 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
   constexpr int NS = KP / 2;
   constexpr int MW = MT * 32;       // packed channel rows
   constexpr int SR = stem_rows_cap(KH);
+  // Pixels as the MFMA's rows (vector stores in the epilogue) with two
+  // channel tiles; with one, the 4-pixel groups' addresses and guards spill.
+  constexpr bool PXR = MT == 2;
   extern __shared__ float4 stem_lds4[];
   float* lds = reinterpret_cast<float*>(stem_lds4);
   float* wl = lds;                  // [NS][2][MW]
@@ -221,7 +228,10 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
       load(std::integral_constant<int, s + PD>{});
 #pragma unroll
       for (int i = 0; i < NT; i++)
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s % (PD + 1)], bq[s % (PD + 1)][i], acc[i], 0, 0, 0);
+        if constexpr (PXR)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(bq[s % (PD + 1)][i], aq[s % (PD + 1)], acc[i], 0, 0, 0);
+        else
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(aq[s % (PD + 1)], bq[s % (PD + 1)][i], acc[i], 0, 0, 0);
       // (keeps the scheduler from sinking the loads ahead to their MFMAs)
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -232,24 +242,56 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
     const int nb = b + (int)gridDim.x;
     if (nb < d.nbands) band_loads(nb, xv);
 
-    // Epilogue: element 4 q + r of lane (j, half) is channel
-    // m 32 + 8 q + 4 half + r, pixel j of the tile; band pixels are
-    // contiguous in the output plane.
+    // Epilogue: pixels are the MFMA's rows (A = the im2col tile), so element
+    // 4 q + r of lane (j, half) is pixel 8 q + 4 half + r of the tile,
+    // channel m 32 + j: four adjacent pixels of one channel per q, one
+    // 16-byte store when d.vec (band pixels are contiguous in the plane).
     const int64_t oplane = (int64_t)d.OH * d.OW;
     float* yb = d.y + (int64_t)img * d.M * oplane + (int64_t)oy0 * d.OW;
+    if constexpr (!PXR) {
+      // (channels as rows: element 4 q + r is channel m 32 + 8 q + 4 half + r,
+      // pixel j of the tile)
 #pragma unroll
-    for (int i = 0; i < NT; i++) {
-      if (!pok[i]) continue;
-      float* yp = yb + ((wave / MT) + (4 / MT) * i) * 32 + j;
+      for (int i = 0; i < NT; i++) {
+        if (!pok[i]) continue;
+        float* yp = yb + ((wave / MT) + (4 / MT) * i) * 32 + j;
 #pragma unroll
-      for (int e = 0; e < 16; e++) {
-        const int ch = m * 32 + 8 * (e >> 2) + 4 * half + (e & 3);
-        if (ch < d.M) {
-          float v = acc[i][e];
-          if (d.bias) v = __fadd_rn(v, bl[ch]);
-          if (d.act == RTENHIP_ACT_RELU) v = rust_max(v, 0.f);
-          else if (d.act == RTENHIP_ACT_CLIP) v = rust_clamp(v, d.lo, d.hi);
-          yp[(int64_t)ch * oplane] = v;
+        for (int e = 0; e < 16; e++) {
+          const int c = m * 32 + 8 * (e >> 2) + 4 * half + (e & 3);
+          if (c < d.M) {
+            float v = acc[i][e];
+            if (d.bias) v = __fadd_rn(v, bl[c]);
+            if (d.act == RTENHIP_ACT_RELU) v = rust_max(v, 0.f);
+            else if (d.act == RTENHIP_ACT_CLIP) v = rust_clamp(v, d.lo, d.hi);
+            yp[(int64_t)c * oplane] = v;
+          }
+        }
+      }
+    } else if (m * 32 + j < d.M) {
+      const int ch = m * 32 + j;
+      const float bv = bl[ch];
+      float* yc = yb + (int64_t)ch * oplane;
+#pragma unroll
+      for (int i = 0; i < NT; i++) {
+        const int tp = ((wave / MT) + (4 / MT) * i) * 32;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int p0 = tp + 8 * q + 4 * half;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            v[r] = acc[i][4 * q + r];
+            if (d.bias) v[r] = __fadd_rn(v[r], bv);
+            if (d.act == RTENHIP_ACT_RELU) v[r] = rust_max(v[r], 0.f);
+            else if (d.act == RTENHIP_ACT_CLIP) v[r] = rust_clamp(v[r], d.lo, d.hi);
+          }
+          if (d.vec) {
+            if (p0 < opb) *reinterpret_cast<float4*>(yc + p0) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+              if (p0 + r < opb) yc[p0 + r] = v[r];
+          }
         }
       }
     }
@@ -377,6 +419,7 @@ rtenhip_status conv_stem(const ConvDmaArgs& a, hipStream_t s) {
   d.act = a.act;
   d.lo = a.lo;
   d.hi = a.hi;
+  d.vec = a.ow % 4 == 0 && ((uintptr_t)a.y & 15) == 0;
   const int64_t K = a.C * a.kh * a.kw, KP = (K + 1) & ~int64_t(1);
   const size_t lds = (size_t)(KP * mt * 32 + e.stage_n + 1 + mt * 32) * 4;
   const dim3 grid((unsigned)std::min(d.nbands, stem_grid_cap())), blk(kStemThreads);
