@@ -320,6 +320,8 @@ STEM_CASES = [
     (2, 3, 32, 32, 64, 7, [3, 3, 3, 3], "relu", True),      # ResNet-50 stem, small
     (1, 3, 224, 224, 64, 7, [3, 3, 3, 3], "relu", True),    # ResNet-50 stem, batch 1 (one row per band)
     (20, 3, 224, 224, 64, 7, [3, 3, 3, 3], "relu", True),   # enough bands for the 4-row, 7-item variant
+    (20, 3, 202, 200, 64, 7, [3, 3, 3, 3], "relu", True),   # 7-item variant, last band of 1 row, partial tile
+    (3, 3, 200, 200, 64, 7, [3, 3, 3, 3], "relu", True),    # 2-item variant, 100-pixel bands (partial tile)
     (2, 3, 224, 224, 32, 3, [1, 1, 1, 1], "clip", True),    # MobileNetV2 stem, full size
     (3, 3, 19, 23, 24, 3, [1, 1, 1, 1], "none", False),     # odd sizes, M < 32, no bias
     (2, 3, 30, 17, 48, 7, [2, 3, 3, 1], "clip", True),      # asymmetric pads, partial 32-row tile
