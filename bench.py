@@ -370,10 +370,14 @@ class Workload:
         g = self.g
         g.set_timing(True)
         ms, report = 0.0, ""
+        self.hold_timeouts = 0
         for _ in range(runs):
             g.run({g.input_ids[0]: self.x, **self.extra}, g.output_ids, out=[self.out])
             torch.cuda.synchronize()
             report = g.timing_report()
+            # (the stream hold gave up before the plan was queued: that run's
+            # event pairs include host launch time, graph.cpp launch_hold)
+            self.hold_timeouts += "hold timed out" in report.splitlines()[0]
             for line in report.splitlines()[1:]:
                 name = line.split()[0]
                 if name.startswith(("Conv", "MatMul", "FusedAttention")) or name == "Gemm":
@@ -421,7 +425,7 @@ class Workload:
         traffic, traffic_src = traffic_bytes(self.model, self.B)
         common = {"traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_desc,
                   "kernel_ms_per_step": round(kms, 4), "kernel_ms_eager_events": round(kernel_ms_eager, 4),
-                  "capped": capped,
+                  "capped": capped, "hold_timeouts": getattr(self, "hold_timeouts", 0),
                   "timing": "per-op hipEvents on the executor stream over eager runs (stream held until the "
                             "plan is queued), capped at ms_per_step when larger (capped: true)"}
         rp = rocprof_kernel_ms(self.model, self.B)

@@ -378,6 +378,59 @@ rtenhip_status rtenhip_cast_f32_to_i32(rtenhip_ctx* ctx, const rtenhip_tensor* x
 rtenhip_status rtenhip_cast_i32_to_f32(rtenhip_ctx* ctx, const rtenhip_tensor_i32* x,
                                        rtenhip_tensor* y);
 
+/* ---- host-resident runs (Model::run with host tensors) -------------------
+ * RTen's Model::run takes and returns host tensors (src/model.rs:580-592) and
+ * rten-cli times that call in a loop (rten-cli/src/main.rs:296-317).  These
+ * entry points give a host caller the same surface without paying the PCIe
+ * copies on top of every forward. */
+/* Page-locked (pinned) host memory, the form the upload DMA reads directly
+ * (hipHostMalloc).  Pageable memory works with rtenhip_graph_run_host too,
+ * but its copies are staged and do not overlap the forward. */
+void* rtenhip_host_alloc(rtenhip_ctx* ctx, size_t bytes);
+void rtenhip_host_free(rtenhip_ctx* ctx, void* ptr);
+/* Queue one Model::run over HOST tensors and return without waiting:
+ * inputs[i].data / outputs[j].data are host pointers (contiguous; shapes and
+ * element types as for rtenhip_graph_run_typed, input_dtypes NULL = all
+ * float32).  Inside the library: the inputs are uploaded on a high-priority
+ * copy stream into one of two device slots while the previous run computes;
+ * the forward (hipGraph replay after the plan's first run) waits only for its
+ * slot's upload; its outputs are downloaded behind the next run's upload.
+ * The host buffers must stay untouched until the run is waited for.  *run_id
+ * (may be NULL) receives the run's id for rtenhip_graph_wait.  Gather index
+ * errors (gather.rs:52-60) of host runs are reported by rtenhip_graph_wait. */
+rtenhip_status rtenhip_graph_run_host(rtenhip_graph* g, const int32_t* input_ids, const rtenhip_tensor* inputs,
+                                      const int32_t* input_dtypes, int32_t n_inputs, const int32_t* output_ids,
+                                      rtenhip_tensor* outputs, int32_t n_outputs, uint64_t* run_id);
+/* Block until host run `run_id` has its outputs on the host (and every
+ * earlier run too); run_id 0 waits for every queued run of the graph.  The
+ * point where RTen's synchronous Model::run returns (src/model.rs:580-592). */
+rtenhip_status rtenhip_graph_wait(rtenhip_graph* g, uint64_t run_id);
+
+/* ---- batch-sharded runs over several GPUs ----------------
+ * One replica of a .rten model (rtenhip_model_load_with_options) per device,
+ * the batch split into contiguous slices (earlier shards take the remainder),
+ * and one exchange: an RCCL all-gather of the per-shard outputs over xGMI
+ * when the devices are distinct (RTENHIP_SHARDED_RCCL=0 disables it), else
+ * device-to-host copies of each shard.  Batch items are independent
+ * (src/ops/conv.rs:243-270), so each image's output is the reference's bits
+ * for the shard its device ran (a one-image shard's FC takes RTen's gemv
+ * order, gemm.rs:651-704).  Models with one input and one output. */
+typedef struct rtenhip_sharded rtenhip_sharded;
+rtenhip_sharded* rtenhip_sharded_create(const uint8_t* model_bytes, size_t len, const int32_t* devices,
+                                        int32_t n_devices, int optimize);
+void rtenhip_sharded_destroy(rtenhip_sharded* s);
+/* 1 when the outputs are all-gathered with RCCL, 0 for host copies. */
+int32_t rtenhip_sharded_gather_mode(rtenhip_sharded* s);
+/* The replica of shard i (for its timing report / tuning knobs), or NULL. */
+rtenhip_graph* rtenhip_sharded_graph(rtenhip_sharded* s, int32_t shard);
+/* Model::run over a HOST batch: input [B, ...] -> output [B, ...], both host
+ * buffers; returns when the output is on the host. */
+rtenhip_status rtenhip_sharded_run_host(rtenhip_sharded* s, const rtenhip_tensor* input, rtenhip_tensor* output);
+/* RCCL mode: the gathered outputs of the last run on shard i's device
+ * ([n_shards][rows][...] with rows = ceil(B / n_shards), short shards
+ * zero-padded), for a device-resident consumer; NULL otherwise. */
+const float* rtenhip_sharded_gathered(rtenhip_sharded* s, int32_t shard);
+
 #ifdef __cplusplus
 }
 #endif

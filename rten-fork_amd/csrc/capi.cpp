@@ -196,16 +196,6 @@ static void fill_conv_desc(const ConvDmaArgs& a, int64_t g, bool lat, const DmaT
   }
 }
 
-// The latency-GEMM descriptor of an ungrouped 1x1 or 3x3 conv (the forms
-// gemm_lat2 / the conv chain address without a K table).
-rtenhip_status lat_conv_desc(const ConvDmaArgs& a, DmaDesc& d) {
-  if (a.groups != 1) return fail(RTENHIP_UNSUPPORTED_VALUE, "conv chain: grouped conv");
-  fill_conv_desc(a, 0, true, DmaTile{16, 256, 1}, nullptr, d);
-  d.dbg = 0;
-  if (!(d.kstride > 0 || d.k3x3)) return fail(RTENHIP_UNSUPPORTED_VALUE, "conv chain: 1x1 or 3x3 windows only");
-  return RTENHIP_OK;
-}
-
 // 16-byte B copies: pointwise stride-1 convs (B[k][n] = x[img][k][p],
 // linear in k) whose 4-pixel groups stay inside one image.
 static void set_conv_bvec(const ConvDmaArgs& a, int cfg, const DmaTile& tile, DmaDesc& d) {

@@ -120,7 +120,7 @@ rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b,
 
 // Holds stream s until *release (pinned host word) is non-zero or max_ms
 // passes (timing runs only, elementwise.hip).
-rtenhip_status launch_hold(const int* release, double max_ms, hipStream_t s);
+rtenhip_status launch_hold(int* word, double max_ms, hipStream_t s);
 
 // Elementwise / pooling / normalisation (elementwise.hip, pool.hip, norm.hip).
 rtenhip_status launch_unary(int op, const float* x, float* y, int64_t n, float p0, float p1,

@@ -95,9 +95,6 @@ struct ConvDmaArgs {
   int64_t H, W, pad_t, pad_l;
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
-struct DmaDesc;
-// Latency-GEMM descriptor of an ungrouped 1x1 / 3x3 conv (conv chain).
-rtenhip_status lat_conv_desc(const ConvDmaArgs& a, DmaDesc& d);
 // conv3 + downsample as one dual DMA GEMM (see capi.cpp); cfg = a3.cfg, both
 // packed for it.
 bool conv_dual_ok(const ConvDmaArgs& a3, const ConvDmaArgs& ad, int cfg);

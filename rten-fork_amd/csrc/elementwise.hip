@@ -325,20 +325,27 @@ rtenhip_status launch_fill(void* y, int64_t n, uint32_t bits, hipStream_t s) {
 // Timing runs only (Graph::run with timing on): one wave that holds the
 // stream until the host has queued the whole eager plan, so the per-op event
 // pairs time the kernels back to back instead of the host's launch pace.  It
-// polls a word of pinned, uncached host memory the host sets after queueing
+// polls word[0] of pinned, uncached host memory the host sets after queueing
 // (a load over PCIe each time, so never stale) and gives up after max_ticks
-// of s_memrealtime (100 MHz) whatever happens: it cannot hang the queue.
-__global__ void hold_kernel(const volatile int* release, uint64_t max_ticks) {
+// of s_memrealtime (100 MHz) whatever happens: it cannot hang the queue.  On
+// giving up it sets word[1] (a vector store from lane 0), so the host can tell
+// that the events of that run include host time (Graph::run's report).
+__global__ void hold_kernel(int* word, uint64_t max_ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  bool released = false;
   while (__builtin_amdgcn_s_memrealtime() - t0 < max_ticks) {
-    if (__hip_atomic_load(const_cast<const int*>(release), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) break;
+    if (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+      released = true;
+      break;
+    }
     __builtin_amdgcn_s_sleep(64);
   }
+  if (!released && threadIdx.x == 0) __hip_atomic_store(word + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-rtenhip_status launch_hold(const int* release, double max_ms, hipStream_t s) {
+rtenhip_status launch_hold(int* word, double max_ms, hipStream_t s) {
   const uint64_t ticks = (uint64_t)(max_ms * 1e5);  // s_memrealtime runs at 100 MHz
-  hipLaunchKernelGGL(hold_kernel, dim3(1), dim3(64), 0, s, release, ticks);
+  hipLaunchKernelGGL(hold_kernel, dim3(1), dim3(64), 0, s, word, ticks);
   RTENHIP_LAUNCH_CHECK();
   return RTENHIP_OK;
 }

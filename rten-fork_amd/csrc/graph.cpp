@@ -68,7 +68,6 @@ static rtenhip_tensor desc(float* p, const Shape& s) {
 
 Plan::~Plan() {
   drop_captures();
-  for (auto& c : chains) c.release();
   if (gather_flag) (void)hipFree(gather_flag);
   for (auto& c : gchk) {
     if (c.ev) {
@@ -154,6 +153,7 @@ static ConvAttrs conv_attrs(const Node& n, bool one_d) {
 }
 
 Graph::~Graph() {
+  destroy_host_pipe(host_pipe);  // (waits for its queued copies)
   for (auto& pl : plans) pl->drop_captures();
   if (hold_word) {
     if (exec_stream) (void)hipStreamSynchronize(exec_stream);
@@ -1437,10 +1437,6 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     if (to == RTENHIP_DTYPE_INT32)
       return rtenhip_cast_f32_to_i32(c, &x, reinterpret_cast<rtenhip_tensor_i32*>(&y));
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
-  }
-  if (t == "Conv" && p.chain_of.count(op_id)) {
-    Plan::ConvChain& c = p.chains[p.chain_of[op_id]];
-    return c.ops[0] == op_id ? exec_chain(p, c) : RTENHIP_OK;  // members run inside the chain's launch
   }
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_project(p, op_id);
@@ -2860,24 +2856,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     RTENHIP_HIP_CHECK(hipMalloc(&arena, plan->arena_bytes));
     arena_cap = plan->arena_bytes;
   }
-  // Conv chains are built once the plan's convs are tuned (after its first,
-  // eager run), outside any capture; rebuilt when the arena moved.
-  if (plan->eager_runs >= 1 && chain_mode != 0 && (!plan->chains_built || plan->chains_arena != arena)) {
-    RTENHIP_HIP_CHECK(hipStreamSynchronize(exec_stream));
-    for (auto& c : plan->chains) c.release();
-    plan->chains.clear();
-    plan->chain_of.clear();
-    plan->drop_captures();
-    hipStream_t saved = ctx->stream;
-    ctx->stream = exec_stream;
-    plan->bound_in.assign(ins ? n_in : 0, nullptr);
-    for (int i = 0; i < n_in; i++) plan->bound_in[i] = ins[i].data;
-    plan->bound_out.assign(n_out, nullptr);
-    for (int i = 0; i < n_out; i++) plan->bound_out[i] = outs[i].data;
-    rtenhip_status cst = build_chains(*plan);
-    ctx->stream = saved;
-    if (cst) return cst;
-  }
   const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
   if (replay) {
     // The ctx scratch buffers a capture bakes in must not move afterwards:
@@ -2904,8 +2882,14 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
   plan->bound_in = bin;
   plan->bound_out = bout;
 
-  RTENHIP_HIP_CHECK(hipEventRecord(ev_in, caller));
-  RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, ev_in, 0));
+  if (ext_order) {
+    // Host-resident runs (graph_io.cpp): the executor stream is ordered after
+    // the run's upload and the previous download of its slot, not the caller.
+    for (hipEvent_t e : ext_waits) RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, e, 0));
+  } else {
+    RTENHIP_HIP_CHECK(hipEventRecord(ev_in, caller));
+    RTENHIP_HIP_CHECK(hipStreamWaitEvent(exec_stream, ev_in, 0));
+  }
   ctx->stream = exec_stream;
   rtenhip_status st = RTENHIP_OK;
   auto run_op = [&](int op) -> rtenhip_status { return exec_op(*plan, op); };
@@ -2976,15 +2960,17 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     // (Not on the plan's first run: its tuner synchronizes inside the ops.)
     const bool hold = timing && plan->eager_runs >= 1;
     if (hold) {
-      if (!hold_word) RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hold_word), sizeof(int), hipHostMallocCoherent));
+      if (!hold_word) RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hold_word), 2 * sizeof(int), hipHostMallocCoherent));
       __atomic_store_n(hold_word, 0, __ATOMIC_SEQ_CST);
+      __atomic_store_n(hold_word + 1, 0, __ATOMIC_SEQ_CST);
       st = launch_hold(hold_word, 100.0, exec_stream);
     }
     for (int op : plan->ops) {
       if (st) break;
       hipEvent_t a = nullptr, b = nullptr;
       // (a downsample computed by its conv3's dual GEMM launches nothing: no events)
-      const bool timed = timing && !plan->dual_skip.count(op);
+      // (nor does a conv1 computed by its conv3's pair kernel)
+      const bool timed = timing && !plan->dual_skip.count(op) && !plan->pair_hold.count(op);
       if (timed) {
         (void)hipEventCreate(&a);
         (void)hipEventCreate(&b);
@@ -3023,11 +3009,10 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
         if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+project)";
         if (plan->conv_pair.count(plan->ops[i])) key = "Conv(conv3+conv1)";
+        if (plan->pair_hold.count(plan->ops[i])) key = "Conv(in_pair)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
-        if (plan->chain_of.count(plan->ops[i]))
-          key = plan->chains[plan->chain_of[plan->ops[i]]].ops[0] == plan->ops[i] ? "Conv(chain)" : "Conv(in_chain)";
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -3041,8 +3026,11 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       std::sort(rows.rbegin(), rows.rend());
       std::ostringstream os;
       char buf[512];
-      snprintf(buf, sizeof buf, "Graph run of %zu ops finished in %.3f ms (device time)\n",
-               plan->ops.size(), total);
+      // A hold that gave up before the plan was queued (word 1) leaves host
+      // launch time inside the event pairs: the report says so.
+      const bool hold_timeout = hold && __atomic_load_n(hold_word + 1, __ATOMIC_SEQ_CST) != 0;
+      snprintf(buf, sizeof buf, "Graph run of %zu ops finished in %.3f ms (device time)%s\n",
+               plan->ops.size(), total, hold_timeout ? " (hold timed out: times include host launch pace)" : "");
       os << buf;
       for (auto& r : rows) {
         snprintf(buf, sizeof buf, "%-22s %10.3f ms (%5.2f%%)  x%d\n", r.second.c_str(), r.first,
@@ -3065,17 +3053,22 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         // GEMM shape and the tuned DMA configuration of GEMM-backed ops.
         auto ce = plan->convs.find(plan->ops[i]);
         auto du = plan->dual_on.find(plan->ops[i]);
-        if (plan->chain_of.count(plan->ops[i])) {
-          const Plan::ConvChain& ch = plan->chains[plan->chain_of[plan->ops[i]]];
-          if (ch.ops[0] == plan->ops[i]) {
-            snprintf(buf, sizeof buf, "  chain of %zu convs, %d phases, grid %d (built: chain %.4f ms vs %.4f ms one by one)",
-                     ch.ops.size(), ch.n_phases, ch.grid, ch.chain_ms, ch.ops_ms);
-            os << buf;
-          } else {
-            os << "  (in its chain's launch)";
-          }
-        } else if (plan->dual_skip.count(plan->ops[i])) {
+        auto pr = plan->conv_pair.find(plan->ops[i]);
+        if (plan->dual_skip.count(plan->ops[i])) {
           os << "  (in its conv3's dual GEMM)";
+        } else if (plan->pair_hold.count(plan->ops[i])) {
+          os << "  (in its conv3's pair kernel)";
+        } else if (pr != plan->conv_pair.end() && ce != plan->convs.end()) {
+          // One launch computes both convs of the pair: its time and FLOPs are
+          // booked here together (the conv1's row has none).
+          const ConvPlan& c3 = ce->second.g;
+          const ConvPlan& c1 = plan->convs.at(pr->second).g;
+          const double fl = 2.0 * ((double)c3.N * c3.oh * c3.ow * c3.O * (double)c3.KC * c3.kh * c3.kw +
+                                   (double)c1.N * c1.oh * c1.ow * c1.O * (double)c1.KC * c1.kh * c1.kw);
+          snprintf(buf, sizeof buf, "  pair conv3 M=%lld K=%lld + conv1 M=%lld K=%lld N=%lld cfg=pair %.1f TF/s",
+                   (long long)c3.O, (long long)(c3.KC * c3.kh * c3.kw), (long long)c1.O,
+                   (long long)(c1.KC * c1.kh * c1.kw), (long long)(c3.N * c3.oh * c3.ow), ms > 0 ? fl / (ms * 1e9) : 0.0);
+          os << buf;
         } else if (du != plan->dual_on.end()) {
           // FLOPs of both convs of the pair.
           const ConvPlan& c3 = ce->second.g;
@@ -3149,6 +3142,10 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       c.run = this_run;
       plan->gchk_next = (plan->gchk_next + 1) % Plan::kGatherChecks;
     }
+  }
+  if (ext_order) {
+    for (hipEvent_t e : ext_records) RTENHIP_HIP_CHECK(hipEventRecord(e, exec_stream));
+    return st;
   }
   RTENHIP_HIP_CHECK(hipEventRecord(ev_out, exec_stream));
   RTENHIP_HIP_CHECK(hipStreamWaitEvent(caller, ev_out, 0));
@@ -3574,7 +3571,6 @@ rtenhip_graph* rtenhip_graph_create(rtenhip_ctx* ctx) {
   if (const char* s = getenv("RTENHIP_PERSIST")) g->persist_mode = std::max(0, std::min(16, atoi(s)));
   if (const char* s = getenv("RTENHIP_PW_VALU")) g->pw_valu_mode = atoi(s);
   if (const char* s = getenv("RTENHIP_LAT")) g->lat_mode = atoi(s);
-  if (const char* s = getenv("RTENHIP_CHAIN")) g->chain_mode = atoi(s);
   return reinterpret_cast<rtenhip_graph*>(g);
 }
 

@@ -238,31 +238,6 @@ struct Plan {
   };
   std::map<int, DualExec> dual_on;   // conv3 op -> its dual launch
   std::set<int> dual_skip;           // downsample ops computed by their conv3
-  // Conv chains (graph_chain.cpp, conv_chain.hip): runs of small-batch convs
-  // executed as one persistent launch; built after the plan's first (tuning)
-  // run, kept only when one launch times faster than the convs one by one.
-  struct ConvChain {
-    std::vector<int> ops;            // member convs in plan order (the first launches the chain)
-    void* layers_dev = nullptr;      // ChainLayer[nl]
-    void* phases_dev = nullptr;      // ChainPhase[nph]
-    int n_layers = 0, n_phases = 0, grid = 0;
-    int* ctrl = nullptr;             // kChainCtrlInts control words
-    std::vector<void*> owned;        // private activations, lat-packed weights, workspaces, counters
-    float chain_ms = 0, ops_ms = 0;  // build-time timing (best of 3)
-    void release() {
-      for (void* b : owned) (void)hipFree(b);
-      owned.clear();
-      if (layers_dev) (void)hipFree(layers_dev);
-      if (phases_dev) (void)hipFree(phases_dev);
-      if (ctrl) (void)hipFree(ctrl);
-      layers_dev = phases_dev = nullptr;
-      ctrl = nullptr;
-    }
-  };
-  std::vector<ConvChain> chains;
-  std::map<int, int> chain_of;        // member op -> chain index
-  bool chains_built = false;
-  void* chains_arena = nullptr;       // the arena the chains' pointers were taken from
   float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
   int64_t mm_pack_floats = 0;
   // What mm_pack holds during a run: the A value it was packed from (value
@@ -333,6 +308,9 @@ struct Plan {
   int eager_runs = 0;
 };
 
+struct HostPipe;
+void destroy_host_pipe(HostPipe* p);
+
 struct Graph {
   Ctx* ctx = nullptr;
   rtenhip_ctx* cptr = nullptr;
@@ -349,7 +327,7 @@ struct Graph {
   hipStream_t exec_stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
-  int* hold_word = nullptr;  // pinned coherent host word releasing launch_hold (timing runs)
+  int* hold_word = nullptr;  // pinned coherent host words: [0] releases launch_hold, [1] set when it timed out
   bool use_hip_graph = true;
   // Gather index checks (Plan::gchk): false = each run waits for its own
   // check and returns its error; true = checks are queued and reported by
@@ -361,9 +339,15 @@ struct Graph {
   int persist_mode = -1; // DMA GEMM launches: -1 tuned, 0 never persistent, k: always, k blocks/CU
   int lat_mode = -1;     // latency GEMM convs (gemm_lat.hip): -1 tuned, 0 never, v > 0 forced variant
   int pw_valu_mode = -1; // pointwise convs on the VALU kernel: -1 tuned, 0 never, v > 0 forced variant (pw_variant_ok)
-  int chain_mode = -1;   // conv chains: -1 when timed faster, 0 never, 1 always (RTENHIP_CHAIN)
   std::string timing_report;
   std::map<std::string, std::pair<double, int>> timing_totals;  // op type -> (ms, count)
+  // Host-resident runs (graph_io.cpp, rtenhip_graph_run_host): the staging
+  // pipeline, and while ext_order is set run() orders the executor stream
+  // after ext_waits and records ext_records at its end instead of syncing with
+  // the caller's stream.
+  HostPipe* host_pipe = nullptr;
+  bool ext_order = false;
+  std::vector<hipEvent_t> ext_waits, ext_records;
 
   ~Graph();
   int add_node(Node n);
@@ -415,9 +399,6 @@ struct Graph {
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_dw_project(Plan& p, int op_id);
   rtenhip_status exec_conv_pair(Plan& p, int op_id);
-  // Conv chains (graph_chain.cpp).
-  rtenhip_status build_chains(Plan& p);
-  rtenhip_status exec_chain(Plan& p, Plan::ConvChain& c);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   // The packed-A store a producer of value v makes this run, or false.

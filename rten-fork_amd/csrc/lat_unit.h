@@ -164,10 +164,7 @@ struct LatEpi {
   float bias[MI][4], res[MI][4];
   float cbv;
 };
-// SC1 (the persistent chain, conv_chain.hip): the residual was stored by
-// another workgroup of the same launch, so it is read with sc1 loads (L1
-// bypassed; the hand-off's consumer side, MI355X guide "Valid forms").
-template <int MI, bool SC1 = false>
+template <int MI>
 __device__ __forceinline__ void lat_epi_loads(const DmaDesc& d, const int sub0, const LatCol& col,
                                               LatEpi<MI>& e) {
   const int h = (threadIdx.x & 63) >> 4;
@@ -182,7 +179,7 @@ __device__ __forceinline__ void lat_epi_loads(const DmaDesc& d, const int sub0, 
       e.res[mi][r] = 0.f;
       if (d.residual && col.n < d.N) {
         const float* rp = d.residual + rbase + (int64_t)mc * d.res_c;
-        e.res[mi][r] = SC1 ? __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *rp;
+        e.res[mi][r] = *rp;
       }
     }
   e.cbv = (d.colbias && col.n < d.N) ? d.colbias[col.p] : 0.f;
@@ -195,9 +192,8 @@ __device__ __forceinline__ float lat_first_block(const DmaDesc& d, float a, floa
   return x;
 }
 
-// Column bias, residual, activation and the store of the folded tile (SC1:
-// write-through sc1 stores, read by other workgroups of the same launch).
-template <int MI, bool SC1 = false>
+// Column bias, residual, activation and the store of the folded tile.
+template <int MI>
 __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, const LatCol& col, const LatEpi<MI>& e,
                                            const lat_f32x4 (&sum)[MI]) {
   const int h = (threadIdx.x & 63) >> 4;
@@ -238,8 +234,7 @@ __device__ __forceinline__ void lat_finish(const DmaDesc& d, const int sub0, con
       }
       if (m < d.M) {
         float* op = d.out + obase + (int64_t)m * d.out_c;
-        if (SC1) __hip_atomic_store(op, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else *op = x;
+        *op = x;
       }
     }
 }
@@ -280,7 +275,7 @@ __device__ __forceinline__ LatStamps lat_stamps_init(const DmaDesc& d, int kb, i
 // x 16 bytes, 8-byte agent-scope stores), drained before the arrival count,
 // and the last block of the tile to arrive folds all chains in K order.
 // Returns false for a unit that did not store the tile.
-template <int MI, bool SC1 = false>
+template <int MI>
 __device__ __forceinline__ bool lat_fold_finish(const DmaDesc& d, const int sub0, const int kb, const int nkb,
                                                 const int wt, const LatCol& col, const LatEpi<MI>& e,
                                                 const lat_f32x4 (&acc)[MI], LatStamps& stp) {
@@ -349,7 +344,7 @@ __device__ __forceinline__ bool lat_fold_finish(const DmaDesc& d, const int sub0
     }
   }
 
-  lat_finish<MI, SC1>(d, sub0, col, e, sum);
+  lat_finish<MI>(d, sub0, col, e, sum);
   if (stp.p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stp.at(6);

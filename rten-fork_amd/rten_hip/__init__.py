@@ -123,6 +123,9 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts", "rtenhip_reduce_mean_f32",
     "rtenhip_graph_describe", "rtenhip_log_softmax_f32", "rtenhip_instance_norm_f32",
     "rtenhip_graph_synchronize", "rtenhip_graph_set_deferred_checks",
+    "rtenhip_host_alloc", "rtenhip_host_free", "rtenhip_graph_run_host", "rtenhip_graph_wait",
+    "rtenhip_sharded_create", "rtenhip_sharded_destroy", "rtenhip_sharded_gather_mode",
+    "rtenhip_sharded_graph", "rtenhip_sharded_run_host", "rtenhip_sharded_gathered",
 ]
 
 # rtenhip_dtype (sg::DataType order, include/rten_hip.h)

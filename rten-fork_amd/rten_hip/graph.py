@@ -203,6 +203,35 @@ class Graph:
                                             oa, odescs, C.c_int32(len(outputs))))
         return out
 
+    def run_host(self, inputs: Dict[int, np.ndarray], outputs: Sequence[int], out: Sequence[np.ndarray]) -> int:
+        """Model::run over HOST arrays (rtenhip_graph_run_host): inputs {value
+        id: float32 / int32 numpy array}, outputs written into ``out`` (host
+        arrays of the planned shapes; pinned ones from host.pinned overlap the
+        forward).  Returns without waiting; the run id goes to wait().  No
+        torch tensor is involved: the staging pipeline is librten_hip.so's."""
+        from .host import _bind, host_desc
+
+        L = _bind()
+        in_ids = list(inputs.keys())
+        arrs = list(inputs.values())
+        descs = (Tensor * max(1, len(arrs)))(*[host_desc(a) for a in arrs])
+        idt = (C.c_int32 * max(1, len(arrs)))(*[DTYPE_INT32 if a.dtype == np.int32 else DTYPE_FLOAT32
+                                                  for a in arrs])
+        odescs = (Tensor * max(1, len(out)))(*[host_desc(a) for a in out])
+        ia = (C.c_int32 * max(1, len(in_ids)))(*in_ids)
+        oa = (C.c_int32 * max(1, len(outputs)))(*outputs)
+        rid = C.c_uint64(0)
+        check(L.rtenhip_graph_run_host(C.c_void_p(self.ptr), ia, descs, idt, C.c_int32(len(in_ids)), oa, odescs,
+                                       C.c_int32(len(outputs)), C.byref(rid)))
+        return int(rid.value)
+
+    def wait(self, run_id: int = 0):
+        """rtenhip_graph_wait: block until host run ``run_id`` (0: every queued
+        run) has its outputs on the host; raises its Gather index error."""
+        from .host import _bind
+
+        check(_bind().rtenhip_graph_wait(C.c_void_p(self.ptr), C.c_uint64(run_id)))
+
 
 @dataclass
 class Node:

@@ -418,6 +418,11 @@ def test_clip_clamp_trait_semantics(oracle):
     assert (_bits(oracle.clip(y, -1.0, 0.0)) == _bits([-1.0, 0.0, 0.0, -1.0, -0.5])).all()
     # Lower bound -0: +0 is not greater than -0, so max returns lo = -0.
     assert (_bits(oracle.clip(np.array([0.0], np.float32), -0.0, 1.0)) == _bits([-0.0])).all()
+
+
+def test_binary_broadcast(oracle):
+    """Add / Mul broadcasting and the incompatible-shape error
+    (src/ops/binary_elementwise.rs:23-45, 158-439)."""
     a = oracle.xorshift(1, 2 * 3 * 4).reshape(2, 3, 4)
     b = oracle.xorshift(2, 4)
     assert np.array_equal(oracle.add(a, b), a + b)
