@@ -289,8 +289,22 @@ class Workload:
         if self.extra:
             raise ValueError("host-input mode covers single-input image models")
         g = self.g
-        outs = [self.out, torch.empty_like(self.out)]
         total = self.world * self.B
+        if self.world == 1:
+            # Through the C ABI (rtenhip_graph_run_host / rtenhip_graph_wait,
+            # csrc/graph_io.cpp): pinned host arrays in and out, the staging
+            # pipeline inside librten_hip.so -- what a Rust Model::run caller
+            # binds.  No torch tensor is involved in the step.
+            from rten_hip.host import pinned
+
+            self.host_in = pinned(self.feed_np["input"].shape)
+            self.host_in[...] = self.feed_np["input"]
+            out_shape = tuple(self.out.shape)
+            self.host_out = [pinned(out_shape), pinned(out_shape)]
+            self.k_host = 0
+            self.capi_host = True
+            return
+        outs = [self.out, torch.empty_like(self.out)]
 
         def fwd(xb, slot):
             g.run({g.input_ids[0]: xb}, g.output_ids, out=[outs[slot]])
@@ -303,12 +317,18 @@ class Workload:
         self.k_host = 0
 
     def host_step(self):
-        self.staging.submit(self.host_in, self.host_out[self.k_host % 2])
+        if getattr(self, "capi_host", False):
+            g = self.g
+            g.run_host({g.input_ids[0]: self.host_in}, g.output_ids, [self.host_out[self.k_host % 2]])
+        else:
+            self.staging.submit(self.host_in, self.host_out[self.k_host % 2])
         self.k_host += 1
 
     def sync(self):
         import torch
 
+        if getattr(self, "capi_host", False):
+            self.g.wait()
         if self.staging is not None:
             self.staging.synchronize()
         torch.cuda.synchronize()
@@ -452,7 +472,7 @@ class Workload:
                 **common}
 
 
-def secondary_entry(ctx, model, B, seq, steps, warmup):
+def secondary_entry(ctx, model, B, seq, steps, warmup, cpu_seconds=0.0):
     """One extra single-GPU configuration, timed like the headline: W warmup
     steps, then K steps between synchronisations (K raised so the timed
     region is >= ~0.15 s for short steps)."""
@@ -470,6 +490,12 @@ def secondary_entry(ctx, model, B, seq, steps, warmup):
            "config": {"workload": workload, "model": w.spec.name, "global_batch": B,
                       "seq_len": seq if model == "bert" else None},
            "roofline": w.roofline(kms, ms, value)}
+    if cpu_seconds > 0:
+        # BASELINE.json configs[0]: the same batch-1 model on RTen's CPU path
+        # (the restated algorithm, timed like the headline's cpu_baseline),
+        # next to the GPU figure (rten-cli/src/main.rs:296-317 times one
+        # Model::run per iteration).
+        ent["cpu_baseline"] = cpu_baseline(w.spec, cpu_seconds, B, lambda: w.feed_np)
     del w
     return ent
 
@@ -484,14 +510,17 @@ def host_input_entry(ctx, steps, warmup, headline_ms):
     w.enable_host_input()
     elapsed, _ = w.timed(steps, warmup, None, host=True)
     ms = elapsed / steps * 1e3
-    pcie = pcie_rates(w.host_in.numel() * 4, w.host_out[0].numel() * 4, w.x.device)
+    pcie = pcie_rates(w.host_in.size * 4, w.host_out[0].size * 4, w.x.device)
     ent = {"metric": "images/sec ResNet-50 f32 batch=64, host-resident input and logits",
            "value": round(64 * steps / elapsed, 2), "unit": "images/s", "ms_per_step": round(ms, 4),
            "steps": steps, "warmup": warmup, "dtype": "f32",
-           "config": {"workload": "resnet50 f32 batch=64, images in pinned host memory uploaded every step "
-                                  "(38.5 MB H2D on a copy stream, overlapped with the previous step's forward), "
-                                  "logits downloaded every step (256 KB D2H); the drop-in Model::run case "
-                                  "(src/model.rs:580-592)", "model": w.spec.name, "global_batch": 64},
+           "config": {"workload": "resnet50 f32 batch=64, images in pinned host memory (rtenhip_host_alloc) "
+                                  "uploaded every step (38.5 MB H2D on the library's copy stream, overlapped with "
+                                  "the previous step's forward), logits downloaded every step (256 KB D2H); the "
+                                  "drop-in Model::run case (src/model.rs:580-592) through the C ABI "
+                                  "(rtenhip_graph_run_host / rtenhip_graph_wait)", "model": w.spec.name,
+                      "global_batch": 64},
+           "entry": "rtenhip_graph_run_host",
            "pcie": pcie,
            "vs_device_resident": round(headline_ms / ms, 4) if headline_ms else None}
     del w
@@ -624,7 +653,8 @@ def main():
             sec = []
             for model, B in (("resnet50", 1), ("mobilenet_v2", 128), ("bert", 32)):
                 try:
-                    sec.append(secondary_entry(ctx, model, B, args.seq, args.steps, args.warmup))
+                    cpu_s = 6.0 if (model, B) == ("resnet50", 1) and not args.no_cpu_baseline else 0.0
+                    sec.append(secondary_entry(ctx, model, B, args.seq, args.steps, args.warmup, cpu_s))
                 except Exception as e:  # noqa: BLE001 -- reported in the line, never hides the headline
                     sec.append({"model": model, "batch": B, "error": f"{type(e).__name__}: {e}"})
             try:
