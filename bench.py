@@ -611,6 +611,12 @@ def main():
     import rten_hip
 
     ctx = rten_hip.Context(torch.cuda.current_device())
+    # One stream for the whole step: the graph executor runs on the stream the
+    # steps are issued from (rtenhip_set_exec_stream), so consecutive runs are
+    # not separated by cross-stream event round trips.
+    step_stream = torch.cuda.Stream()
+    torch.cuda.set_stream(step_stream)
+    ctx.use_stream(step_stream)
     w = Workload(ctx, args.model, args.batch, args.seq, rank, world, backend)
     if args.host_input:
         w.enable_host_input()

@@ -78,6 +78,14 @@ void rtenhip_destroy(rtenhip_ctx* ctx);
 /* Stream used by all subsequent calls on ctx (a hipStream_t; NULL = default). */
 rtenhip_status rtenhip_set_stream(rtenhip_ctx* ctx, void* stream);
 void* rtenhip_get_stream(rtenhip_ctx* ctx);
+/* The stream the context's graphs execute and capture on (Graph::run's
+ * executor; by default a non-blocking stream the library creates on the first
+ * graph run).  A caller that submits runs from one stream can make it the
+ * executor (a non-blocking stream, never the legacy NULL stream: NULL reverts
+ * to a library-owned one); runs issued from the executor stream itself skip
+ * the two cross-stream events each run otherwise puts between the caller's
+ * stream and the executor.  Synchronizes the previous executor first. */
+rtenhip_status rtenhip_set_exec_stream(rtenhip_ctx* ctx, void* stream);
 const char* rtenhip_last_error_message(void);
 /* Status code of the last error on this thread (for entry points that return
  * a handle rather than a status, e.g. rtenhip_model_load). */

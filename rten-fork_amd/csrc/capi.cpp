@@ -42,7 +42,7 @@ Ctx::Ctx(int dev) : device(dev), ref_threads(rten_num_threads()) {}
 Ctx::~Ctx() {
   if (exec_stream) {
     (void)hipStreamSynchronize(exec_stream);
-    (void)hipStreamDestroy(exec_stream);
+    if (owns_exec) (void)hipStreamDestroy(exec_stream);
   }
   for (auto& kv : ktabs) (void)hipFree(kv.second);
   for (auto& kv : dtabs) (void)hipFree(kv.second);
@@ -828,6 +828,17 @@ rtenhip_status rtenhip_set_stream(rtenhip_ctx* ctx, void* stream) {
   return RTENHIP_OK;
 }
 void* rtenhip_get_stream(rtenhip_ctx* ctx) { return C_(ctx)->stream; }
+
+rtenhip_status rtenhip_set_exec_stream(rtenhip_ctx* ctx, void* stream) {
+  Ctx* c = C_(ctx);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (s == c->exec_stream) return RTENHIP_OK;
+  if (c->exec_stream) RTENHIP_HIP_CHECK(hipStreamSynchronize(c->exec_stream));
+  if (c->exec_stream && c->owns_exec) (void)hipStreamDestroy(c->exec_stream);
+  c->exec_stream = s;  // NULL: the next graph run creates a library-owned one
+  c->owns_exec = false;
+  return RTENHIP_OK;
+}
 
 const char* rtenhip_last_error_message(void) { return g_err.c_str(); }
 int32_t rtenhip_last_error_code(void) { return g_err_code; }

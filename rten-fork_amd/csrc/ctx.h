@@ -20,6 +20,9 @@ struct Ctx {
   // default), and streams beyond that share them, serialising copies or
   // kernels queued behind another graph's work.
   hipStream_t exec_stream = nullptr;
+  // exec_stream was created by the library (else the caller's, set through
+  // rtenhip_set_exec_stream, and not destroyed here).
+  bool owns_exec = false;
   // Thread count RTen would run with (RTEN_NUM_THREADS semantics,
   // src/threading.rs:41-62).  It only changes numerics in the gemv path,
   // where the reference's column blocking depends on it (gemm.rs:673).

@@ -123,7 +123,7 @@ EXPORTED_SYMBOLS = [
     "rtenhip_graph_plan_typed", "rtenhip_num_threads", "rtenhip_cpu_counts", "rtenhip_reduce_mean_f32",
     "rtenhip_graph_describe", "rtenhip_log_softmax_f32", "rtenhip_instance_norm_f32",
     "rtenhip_graph_synchronize", "rtenhip_graph_set_deferred_checks",
-    "rtenhip_host_alloc", "rtenhip_host_free", "rtenhip_graph_run_host", "rtenhip_graph_wait",
+    "rtenhip_set_exec_stream", "rtenhip_host_alloc", "rtenhip_host_free", "rtenhip_graph_run_host", "rtenhip_graph_wait",
     "rtenhip_sharded_create", "rtenhip_sharded_destroy", "rtenhip_sharded_gather_mode",
     "rtenhip_sharded_graph", "rtenhip_sharded_run_host", "rtenhip_sharded_gathered",
 ]
@@ -189,6 +189,15 @@ class Context:
         torch = _torch()
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         check(lib().rtenhip_set_stream(C.c_void_p(self.ptr), C.c_void_p(s.cuda_stream)))
+
+    def use_stream(self, stream):
+        """Run this context's graphs on ``stream`` (a torch.cuda.Stream) and
+        make it the caller's stream too (rtenhip_set_exec_stream): graph runs
+        issued under ``with torch.cuda.stream(stream)`` then need no
+        cross-stream events between runs."""
+        self.exec_stream = stream  # keep the torch stream alive as long as the context uses it
+        check(lib().rtenhip_set_exec_stream(C.c_void_p(self.ptr), C.c_void_p(stream.cuda_stream)))
+        self.sync_stream(stream)
 
     def close(self):
         if self.ptr:

@@ -163,3 +163,37 @@ def test_sharded_errors(rh):
     out = np.zeros((0, 10), np.float32)
     sm.run(np.zeros((0, 8, 12, 12), np.float32), out)  # empty batch: nothing to do
     sm.close()
+
+
+def test_runs_on_the_executor_stream(rh):
+    """rtenhip_set_exec_stream: a caller issuing runs from the executor stream
+    itself (no cross-stream events between runs) gets the oracle's bits through
+    eager, capture and replay runs, and can go back to a library-owned
+    executor."""
+    import torch
+    import graph_runner
+    from rten_hip import Context, models
+
+    spec = models.resnet50()
+    x = np.random.default_rng(3).random((1, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {"input": x})[spec.outputs[0]]
+    ctx = Context(0)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        ctx.use_stream(s)
+        g = spec.to_graph(ctx)
+        xd = torch.from_numpy(x).cuda()
+        out = None
+        for r in range(4):
+            out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+            s.synchronize()
+            assert _bits_equal(out[0].cpu().numpy(), exp), f"run {r}"
+    from rten_hip import check, lib
+    import ctypes as C
+
+    check(lib().rtenhip_set_exec_stream(C.c_void_p(ctx.ptr), None))  # back to a library-owned executor
+    out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    assert _bits_equal(out[0].cpu().numpy(), exp)
+    g.close()
+    ctx.close()
