@@ -186,12 +186,12 @@ _ROOF_KERNELS = {
 }
 
 
-def traffic_bytes(model, batch):
+def traffic_bytes(model, batch, all_kernels=False):
     """HBM bytes per step of the roofline's kernels, from the newest committed
     rocprofv3 PMC summary of this workload (scripts/gpu_prof.sh ->
     tools/pmc_traffic.py --marker): FETCH_SIZE x2 (gfx950) + WRITE_SIZE,
     eager forwards.  (None, None) when no summary exists for this workload."""
-    for rnd in ("r5", "r4", "r3"):
+    for rnd in ("r6", "r5", "r4", "r3"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic_{model}_b{batch}.json")
         if not os.path.exists(path):
             continue
@@ -201,6 +201,8 @@ def traffic_bytes(model, batch):
         except (OSError, ValueError, KeyError):
             continue
         fams = _ROOF_KERNELS[model]
+        if all_kernels:
+            return round(js.get("all_kernels_bytes_per_forward") or sum(by.values())), path
         return round(sum(v for k, v in by.items() if any(f in k for f in fams))), \
             f"profiles/{os.path.basename(path)} (commit {js.get('commit', 'unrecorded')})"
     return None, None
@@ -214,7 +216,7 @@ def rocprof_kernel_ms(model, batch):
     no summary exists."""
     import re
 
-    for rnd in ("r5", "r4"):
+    for rnd in ("r6", "r5", "r4"):
         path = os.path.join(ROOT, "profiles", f"{rnd}_rocprof_{model}_b{batch}_per_forward.txt")
         if not os.path.exists(path):
             continue
@@ -403,6 +405,7 @@ class Workload:
                 if name.startswith(("Conv", "MatMul", "FusedAttention")) or name == "Gemm":
                     ms += float(line.split()[1])
         g.set_timing(False)
+        self.report = report
         return ms / runs, report
 
     def describe(self):
@@ -430,6 +433,29 @@ class Workload:
             metric = ({"resnet50": f"images/sec ResNet-50 f32 batch={B} per GPU",
                        "mobilenet_v2": "images/sec MobileNetV2 f32"})[model]
         return metric, workload, kernel_desc, data
+
+    def fused_io_bytes(self, report):
+        """Algorithmic HBM bytes of one ResNet step as the executor fused it:
+        models.conv_io_bytes (each conv / pool reads its input and weights and
+        writes its output once, fused residual reads once) minus what the
+        fused kernels the plan took never move -- a dual conv3 + downsample
+        GEMM neither writes nor re-reads the downsample output (2 x M x N
+        floats), a conv3 -> conv1 pair kernel reads conv1's input from LDS (K1
+        x N floats).  Parsed from the plan's per-op report lines."""
+        import re
+
+        from rten_hip import models
+
+        total = models.conv_io_bytes(self.spec, self.B)
+        for line in report.splitlines():
+            m = re.search(r"  dual M=(\d+) N=(\d+) K=(\d+)\+(\d+)", line)
+            if m:
+                # the downsample's M equals conv3's (both produce the residual sum's operands)
+                total -= 2 * 4.0 * int(m.group(1)) * int(m.group(2))
+            m = re.search(r"  pair conv3 M=(\d+) K=(\d+) \+ conv1 M=(\d+) K=(\d+) N=(\d+)", line)
+            if m:
+                total -= 4.0 * int(m.group(4)) * int(m.group(5))
+        return total
 
     def roofline(self, kernel_ms_eager, ms_per_step, value):
         # The eager per-op event pairs bracket each op's launches (the stream
@@ -466,6 +492,14 @@ class Workload:
             return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(gbs / HBM_PEAK_GBPS, 4), "bytes_per_step": self.io_bytes,
                     "mfma_tflops": round(achieved, 2), **common}
+        if self.model == "resnet50" and getattr(self, "report", ""):
+            # All kernels' PMC bytes (pooling included, as in the algorithmic
+            # figure) over the fused path's algorithmic bytes.
+            io = self.fused_io_bytes(self.report)
+            all_bytes = traffic_bytes(self.model, self.B, all_kernels=True)[0]
+            common["bytes_per_step"] = round(io)
+            common["traffic_all_kernels"] = all_bytes
+            common["traffic_ratio"] = round(all_bytes / io, 3) if all_bytes else None
         return {"bound": "mfma", "achieved": round(achieved, 2), "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4), "flops_per_step": gemm_flops,
                 "model_frac": round(value / self.world * self.flops_per_img / 1e12 / F32_MFMA_PEAK_TFLOPS, 4),

@@ -166,6 +166,7 @@ def conv_flops(spec: ModelSpec, batch: int, hw: int = 224) -> float:
             k, s, p = n.attrs["kernel_size"], n.attrs["strides"], n.attrs["pads"]
             shapes[n.outputs[0]] = (N, C, (H + p[0] + p[2] - k[0]) // s[0] + 1,
                                     (W + p[1] + p[3] - k[1]) // s[1] + 1)
+            total += 4.0 * (N * C * H * W + float(np.prod(shapes[n.outputs[0]])))  # read + write
         elif n.op_type == "GlobalAveragePool":
             shapes[n.outputs[0]] = (xs[0], xs[1], 1, 1)
         elif n.op_type == "Flatten":
@@ -273,6 +274,7 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224, count_pairs: bool 
             k, s, p = n.attrs["kernel_size"], n.attrs["strides"], n.attrs["pads"]
             shapes[n.outputs[0]] = (N, C, (H + p[0] + p[2] - k[0]) // s[0] + 1,
                                     (W + p[1] + p[3] - k[1]) // s[1] + 1)
+            total += 4.0 * (N * C * H * W + float(np.prod(shapes[n.outputs[0]])))  # read + write
         elif n.op_type == "GlobalAveragePool":
             shapes[n.outputs[0]] = (xs[0], xs[1], 1, 1)
         elif n.op_type == "Flatten":
