@@ -441,7 +441,8 @@ class Workload:
         fused kernels the plan took never move -- a dual conv3 + downsample
         GEMM neither writes nor re-reads the downsample output (2 x M x N
         floats), a conv3 -> conv1 pair kernel reads conv1's input from LDS (K1
-        x N floats).  Parsed from the plan's per-op report lines."""
+        x N floats), the stem + MaxPool kernel never writes the stem's output
+        (2 x its floats: the write and the pool's read).  Parsed from the plan's per-op report lines."""
         import re
 
         from rten_hip import models
@@ -455,6 +456,10 @@ class Workload:
             m = re.search(r"  pair conv3 M=(\d+) K=(\d+) \+ conv1 M=(\d+) K=(\d+) N=(\d+)", line)
             if m:
                 total -= 4.0 * int(m.group(4)) * int(m.group(5))
+            m = re.search(r"  stem\+pool M=\d+ N=\d+ K=\d+ stem_out=(\d+)", line)
+            if m:
+                # the stem's output is neither written nor read back by the pool
+                total -= 2 * 4.0 * int(m.group(1))
         return total
 
     def roofline(self, kernel_ms_eager, ms_per_step, value):

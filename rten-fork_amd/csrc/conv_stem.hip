@@ -66,6 +66,7 @@ struct StemDesc {
   int act;
   float lo, hi;
   int vec;          // OW % 4 == 0 and y 16-byte aligned: 4-pixel vector stores
+  float* halo;      // POOL: [N, M, tiles_y, OW / 2] row-pooled last conv row of each band
 };
 
 constexpr int kStemThreads = 256;
@@ -84,7 +85,7 @@ __device__ __forceinline__ void stem_static_for(std::integer_sequence<int, Is...
   (f(std::integral_constant<int, Is>{}), ...);
 }
 
-template <int C, int KH, int KW, int S, int MT, int NT>
+template <int C, int KH, int KW, int S, int MT, int NT, bool POOL = false>
 __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) {
   constexpr int K = C * KH * KW;
   constexpr int KP = (K + 1) & ~1;  // k pairs of the 32x32x2 MFMA
@@ -99,6 +100,7 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
   float* wl = lds;                  // [NS][2][MW]
   float* xs = lds + KP * MW;        // [C][R][LW], then one zero slot
   float* bl = xs + d.stage_n + 1;   // [MW] bias (0 past M, or without bias)
+  float* ex = bl + MW;              // POOL: [MT][4 rows][32 channels] column exchange
   const int zs = d.stage_n;         // the zero slot (index into xs)
   const int t = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -184,11 +186,20 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
     bool pok[NT];
 #pragma unroll
     for (int i = 0; i < NT; i++) {
-      const int p = ((wave / MT) + (4 / MT) * i) * 32 + j;
-      pok[i] = p < opb;
-      const int pc = pok[i] ? p : 0;
-      const int oyl = pc / d.OW, ox = pc - oyl * d.OW;
-      pb[i] = oyl * S * d.LW + ox * S;
+      if constexpr (POOL) {
+        // Tile t = 4 rows x 8 columns (the band's rows; waves 0 / 1 take
+        // tiles 0..6, waves 2 / 3 tiles 7..13), pixel j = (row j / 8,
+        // column 8 t + j % 8): an accumulator lane then holds a 4 x 4 patch.
+        const int t = (wave >> 1) * NT + i;
+        pok[i] = true;
+        pb[i] = (j >> 3) * S * d.LW + (8 * t + (j & 7)) * S;
+      } else {
+        const int p = ((wave / MT) + (4 / MT) * i) * 32 + j;
+        pok[i] = p < opb;
+        const int pc = pok[i] ? p : 0;
+        const int oyl = pc / d.OW, ox = pc - oyl * d.OW;
+        pb[i] = oyl * S * d.LW + ox * S;
+      }
     }
     stem_f32x16 acc[NT];
 #pragma unroll
@@ -248,7 +259,64 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
     // 16-byte store when d.vec (band pixels are contiguous in the plane).
     const int64_t oplane = (int64_t)d.OH * d.OW;
     float* yb = d.y + (int64_t)img * d.M * oplane + (int64_t)oy0 * d.OW;
-    if constexpr (!PXR) {
+    if constexpr (POOL) {
+      // MaxPool 3x3 / 2, pads 1 (pooling.rs:104-238) on the band's Relu'd
+      // conv outputs, in registers.  Lane (channel j, half h) of item i holds
+      // rows 0..3 x columns 8 t + 4 h .. + 3; pooled column 4 t + 2 h + u
+      // takes columns 8 t + 4 h + 2 u - 1 .. + 1, the left one from the
+      // other half (h = 1) or the previous tile (h = 0: the previous item, or
+      // for tile 7 wave 0 / 1's tile 6 through LDS; tile 0 has only padding
+      // there).  Pooled row 2 b + 1 (conv rows 4 b + 1 .. 3) is complete in
+      // the band; row 2 b gets rows 4 b, 4 b + 1 here and conv row 4 b - 1
+      // from band b - 1's halo row (stem_pool_finish_kernel).  The values are
+      // Relu outputs -- never NaN, never -0 -- so their max does not depend
+      // on the order of the folds: the reference's (ky, kx) fold gives the
+      // same bits.
+      const int ch = m * 32 + j;  // (M == 64 == MT * 32)
+      const float bv = bl[ch];
+      const int PW = d.OW >> 1;
+      const int band = b - img * d.tiles_y;
+      float* yc = d.y + ((int64_t)img * d.M + ch) * (int64_t)(d.OH >> 1) * PW + (int64_t)(2 * band) * PW;
+      float* hc = d.halo + (((int64_t)img * d.M + ch) * d.tiles_y + band) * PW;
+      auto relu_v = [&](const stem_f32x16& a, int q, int r) __attribute__((always_inline)) {
+        float v = a[4 * q + r];
+        if (d.bias) v = __fadd_rn(v, bv);
+        return rust_max(v, 0.f);
+      };
+      float prev[4];
+      if (wave < 2) {  // publish column 55 (tile 6's last) for tile 7's left neighbour
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float sw = __shfl_xor(relu_v(acc[NT - 1], q, 3), 32);
+          if (half == 0) ex[(m * 4 + q) * 32 + j] = sw;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 4; q++) prev[q] = wave >= 2 ? ex[(m * 4 + q) * 32 + j] : 0.f;
+#pragma unroll
+      for (int i = 0; i < NT; i++) {
+        const int t = (wave >> 1) * NT + i;
+        float hm[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float v0 = relu_v(acc[i], q, 0), v1 = relu_v(acc[i], q, 1);
+          const float v2 = relu_v(acc[i], q, 2), v3 = relu_v(acc[i], q, 3);
+          const float sw = __shfl_xor(v3, 32);  // h = 1: column 8 t + 3; h = 0: 8 t + 7 (next tile's left)
+          const float left = half ? sw : prev[q];
+          float h0 = fmaxf(v0, v1);
+          if (half || t > 0) h0 = fmaxf(left, h0);
+          hm[q][0] = h0;
+          hm[q][1] = fmaxf(fmaxf(v1, v2), v3);
+          prev[q] = sw;
+        }
+        const int px = 4 * t + 2 * half;
+        *reinterpret_cast<float2*>(yc + PW + px) =
+            make_float2(fmaxf(fmaxf(hm[1][0], hm[2][0]), hm[3][0]), fmaxf(fmaxf(hm[1][1], hm[2][1]), hm[3][1]));
+        *reinterpret_cast<float2*>(yc + px) = make_float2(fmaxf(hm[0][0], hm[1][0]), fmaxf(hm[0][1], hm[1][1]));
+        if (band + 1 < d.tiles_y) *reinterpret_cast<float2*>(hc + px) = make_float2(hm[3][0], hm[3][1]);
+      }
+    } else if constexpr (!PXR) {
       // (channels as rows: element 4 q + r is channel m 32 + 8 q + 4 half + r,
       // pixel j of the tile)
 #pragma unroll
@@ -300,6 +368,27 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
       band_store(xv);
     }
   }
+}
+
+// Pooled row 2 b of every (image, channel), b >= 1: the band's partial (conv
+// rows 4 b, 4 b + 1) and band b - 1's halo (conv row 4 b - 1, row-pooled),
+// 16 bytes per thread.  (Pooled row 0's window has only padding above.)
+__global__ void stem_pool_finish_kernel(float* __restrict__ y, const float* __restrict__ halo, int64_t n4,
+                                        int PW4, int tiles_y) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  const int c4 = (int)(i % PW4);
+  const int64_t r = i / PW4;                  // (image, channel) * (tiles_y - 1) + b - 1
+  const int64_t plane = r / (tiles_y - 1);
+  const int b = (int)(r - plane * (tiles_y - 1)) + 1;
+  float4* yp = reinterpret_cast<float4*>(y) + (plane * (2 * tiles_y) + 2 * b) * PW4 + c4;
+  const float4 h = reinterpret_cast<const float4*>(halo)[(plane * tiles_y + b - 1) * PW4 + c4];
+  float4 v = *yp;
+  v.x = fmaxf(v.x, h.x);
+  v.y = fmaxf(v.y, h.y);
+  v.z = fmaxf(v.z, h.z);
+  v.w = fmaxf(v.w, h.w);
+  *yp = v;
 }
 
 // w [M][K] -> [KP / 2][2][MT * 32], zero past M and K.
@@ -365,6 +454,81 @@ int stem_grid_cap() {
 }
 
 }  // namespace
+
+// Stem + MaxPool 3x3 / 2 / pads 1 in one pass (conv_stem_kernel<..., POOL>):
+// ResNet-50's 7x7 / 2 stem (C = 3, M = 64, 112 x 112 outputs) with a fused
+// Relu, at batches whose bands are 4 output rows of 7 items per wave.
+bool conv_stem_pool_eligible(const ConvPlan& g) {
+  if (!(g.C == 3 && g.kh == 7 && g.kw == 7 && g.sh == 2 && g.sw == 2 && g.O == 64 && g.groups == 1 && g.dh == 1 &&
+        g.dw == 1 && g.ow == 112 && g.oh % 4 == 0 && !g.one_d))
+    return false;
+  const StemShape e = stem_shape((int)g.C, (int)g.kh, (int)g.kw, (int)g.sh, (int)g.oh, (int)g.ow, g.O, g.N,
+                                 stem_grid_cap() / 2);
+  const int64_t KP = 148;
+  return e.TR == 4 && e.NT == kStemNT && KP * 64 + e.stage_n + 1 + 64 + 256 <= kStemLdsFloats &&
+         g.C * g.H * g.W < (int64_t(1) << 29) && g.N * e.tiles_y < (int64_t(1) << 31);
+}
+
+int64_t stem_pool_halo_floats(const ConvPlan& g) { return g.N * g.O * (g.oh / 4) * (g.ow / 2); }
+
+rtenhip_status conv_stem_pool(const ConvDmaArgs& a, float* pooled, float* halo, hipStream_t s) {
+  ConvPlan g{};
+  g.N = a.N;
+  g.C = a.C;
+  g.H = a.H;
+  g.W = a.W;
+  g.O = a.O;
+  g.kh = a.kh;
+  g.kw = a.kw;
+  g.sh = a.sh;
+  g.sw = a.sw;
+  g.dh = a.dh;
+  g.dw = a.dw;
+  g.oh = a.oh;
+  g.ow = a.ow;
+  g.groups = a.groups;
+  if (!conv_stem_pool_eligible(g) || !a.x_unpadded || a.residual || a.bn || a.act != RTENHIP_ACT_RELU ||
+      ((uintptr_t)pooled & 15) || ((uintptr_t)halo & 15))
+    return fail(RTENHIP_INVALID_VALUE, "stem + max pool: unsupported layout");
+  const StemShape e = stem_shape((int)a.C, (int)a.kh, (int)a.kw, (int)a.sh, (int)a.oh, (int)a.ow, a.O, a.N,
+                                 stem_grid_cap() / 2);
+  StemDesc d{};
+  d.x = a.x_unpadded;
+  d.wp = a.packed_w;
+  d.bias = a.bias;
+  d.y = pooled;
+  d.halo = halo;
+  d.M = (int)a.O;
+  d.H = (int)a.H;
+  d.W = (int)a.W;
+  d.OH = (int)a.oh;
+  d.OW = (int)a.ow;
+  d.pt = (int)a.pad_t;
+  d.pl = (int)a.pad_l;
+  d.TR = e.TR;
+  d.R = e.R;
+  d.LW = e.LW;
+  d.tiles_y = e.tiles_y;
+  d.nbands = (int)(a.N * e.tiles_y);
+  d.stage_n = e.stage_n;
+  d.act = a.act;
+  d.vec = 1;
+  const size_t lds = (size_t)(148 * 64 + e.stage_n + 1 + 64 + 256) * 4;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_stem_kernel<3, 7, 7, 2, 2, kStemNT, true>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, kStemLdsFloats * 4);
+  RTENHIP_HIP_CHECK(attr);
+  hipLaunchKernelGGL((conv_stem_kernel<3, 7, 7, 2, 2, kStemNT, true>),
+                     dim3((unsigned)std::min(d.nbands, stem_grid_cap())), dim3(kStemThreads), lds, s, d);
+  RTENHIP_LAUNCH_CHECK();
+  const int PW4 = (int)(a.ow / 2 / 4);
+  const int64_t n4 = a.N * a.O * (e.tiles_y - 1) * PW4;
+  if (n4 > 0) {
+    hipLaunchKernelGGL(stem_pool_finish_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, pooled, halo,
+                       n4, PW4, e.tiles_y);
+    RTENHIP_LAUNCH_CHECK();
+  }
+  return RTENHIP_OK;
+}
 
 bool conv_stem_eligible(const ConvPlan& g, bool padded_out) {
   const bool resnet = g.C == 3 && g.kh == 7 && g.kw == 7 && g.sh == 2 && g.sw == 2;

@@ -128,6 +128,11 @@ bool conv_stem_eligible(const ConvPlan& g, bool padded_out);
 int64_t stem_weight_floats(int64_t M, int64_t K);
 rtenhip_status pack_stem_weights(const float* w, int64_t M, int64_t K, float* out, hipStream_t s);
 rtenhip_status conv_stem(const ConvDmaArgs& a, hipStream_t s);
+// ResNet stem + its MaxPool 3x3 / 2 / pads 1 (requires the fused Relu):
+// pooled [N, 64, oh / 2, ow / 2]; halo: stem_pool_halo_floats scratch.
+bool conv_stem_pool_eligible(const ConvPlan& g);
+int64_t stem_pool_halo_floats(const ConvPlan& g);
+rtenhip_status conv_stem_pool(const ConvDmaArgs& a, float* pooled, float* halo, hipStream_t s);
 rtenhip_status conv_pw_valu(const ConvDmaArgs& a, int variant, hipStream_t s);
 // DMA-config numbers at and above this select the pointwise VALU kernel,
 // variant cfg - kPwCfgBase (graph tuner).

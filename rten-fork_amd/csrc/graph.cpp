@@ -90,6 +90,10 @@ Plan::~Plan() {
     if (kv.second.w3p) (void)hipFree(kv.second.w3p);
     if (kv.second.w1p) (void)hipFree(kv.second.w1p);
   }
+  for (auto& kv : stem_pool_exec) {
+    if (kv.second.packed) (void)hipFree(kv.second.packed);
+    if (kv.second.halo) (void)hipFree(kv.second.halo);
+  }
   for (auto& kv : matmuls) {
     if (kv.second.ws) (void)hipFree(kv.second.ws);
     if (kv.second.counters) (void)hipFree(kv.second.counters);
@@ -856,6 +860,49 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.dwpw_fused[op] = dn.inputs[0];
       drop.push_back(n.fd_op);
     }
+    // Stem -> MaxPool (conv_stem.hip POOL): ResNet's 7x7 / 2 stem with its
+    // fused Relu, read only by a 3x3 / 2 / pads 1 MaxPool, at batches whose
+    // bands are 4 output rows; the conv op leaves the plan, the pool op runs
+    // both and the stem's output is never written.
+    const bool stem_pool_off = (getenv("RTENHIP_STEM_POOL") && getenv("RTENHIP_STEM_POOL")[0] == '0') ||
+                                      (getenv("RTENHIP_STEM") && getenv("RTENHIP_STEM")[0] == '0');  // A/B runs (read per plan)
+    for (int op : p.ops) {
+      const Node& n = nodes[op];
+      if (stem_pool_off || n.op_type != "MaxPool" || n.inputs.empty() || n.outputs.size() != 1) continue;
+      const int v = n.inputs[0];
+      int cop = -1;
+      for (int o : p.ops)
+        if (nodes[o].op_type == "Conv" && nodes[o].outputs.size() == 1 && nodes[o].outputs[0] == v) cop = o;
+      if (cop < 0 || std::find(drop.begin(), drop.end(), cop) != drop.end() || p.expand_fused.count(cop) ||
+          p.dwpw_fused.count(cop))
+        continue;
+      const Node& cn = nodes[cop];
+      if (outset0.count(v) || uses_of_value(p.ops, v) != 1 || cn.fused_act != RTENHIP_ACT_RELU ||
+          cn.fused_residual >= 0 || cn.fused_bn >= 0 || cn.inputs.size() < 2 ||
+          nodes[cn.inputs[1]].kind != NodeKind::Constant ||
+          (cn.inputs.size() > 2 && cn.inputs[2] >= 0 && nodes[cn.inputs[2]].kind != NodeKind::Constant))
+        continue;
+      const Shape* xs = shape_of(cn.inputs[0]);
+      const Shape* ws = shape_of(cn.inputs[1]);
+      if (!xs || !ws || xs->size() != 4 || p.dtypes[cn.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
+      ConvAttrs ca = conv_attrs(cn, false);
+      rtenhip_tensor xt = desc(nullptr, *xs), wt = desc(nullptr, *ws);
+      ConvPlan g;
+      if (plan_conv(&xt, &wt, ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(), ca.groups, g) !=
+              RTENHIP_OK ||
+          !conv_stem_pool_eligible(g))
+        continue;
+      std::string ap = n.attrs.str("auto_pad", "notset");
+      const bool fixed = !(ap == "same" || ap == "SAME_UPPER" || ap == "Same");
+      const Shape& ys = shapes[n.outputs[0]];
+      if (!fixed || n.attrs.ints("kernel_size", {1, 1}) != std::vector<int64_t>{3, 3} ||
+          n.attrs.ints("strides", {1, 1}) != std::vector<int64_t>{2, 2} ||
+          n.attrs.ints("pads", {0, 0, 0, 0}) != std::vector<int64_t>{1, 1, 1, 1} || ys.size() != 4 ||
+          ys[0] != g.N || ys[1] != g.O || ys[2] != g.oh / 2 || ys[3] != g.ow / 2)
+        continue;
+      p.stem_pool[op] = cop;
+      drop.push_back(cop);
+    }
     if (!drop.empty()) {
       std::vector<int> kept;
       for (int op : p.ops)
@@ -1096,6 +1143,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       if (ef != p.expand_fused.end()) readers[ef->second].push_back(op);
       auto df = p.dwpw_fused.find(op);
       if (df != p.dwpw_fused.end()) readers[df->second].push_back(op);
+      auto sp = p.stem_pool.find(op);
+      if (sp != p.stem_pool.end()) readers[nodes[sp->second].inputs[0]].push_back(op);
     }
     for (auto& kv : p.convs) {
       if (kv.second.fc) continue;
@@ -1336,6 +1385,8 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (ef != p.expand_fused.end()) drop_use(ef->second);
     auto df = p.dwpw_fused.find(op);
     if (df != p.dwpw_fused.end()) drop_use(df->second);
+    auto spf = p.stem_pool.find(op);
+    if (spf != p.stem_pool.end()) drop_use(nodes[spf->second].inputs[0]);
     auto cdu = p.conv_dual.find(op);
     if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
     auto ph = p.pair_hold.find(op);
@@ -1438,6 +1489,7 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
       return rtenhip_cast_f32_to_i32(c, &x, reinterpret_cast<rtenhip_tensor_i32*>(&y));
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
   }
+  if (t == "MaxPool" && p.stem_pool.count(op_id)) return exec_stem_pool(p, op_id);
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_project(p, op_id);
   if (t == "Conv" && p.conv_pair.count(op_id)) return exec_conv_pair(p, op_id);
@@ -1719,6 +1771,52 @@ rtenhip_status Graph::exec_dw_project(Plan& p, int op_id) {
   return launch_dw_project(ptr_of(p, xv), ptr_of(p, dn.inputs[1]), bd, dn.fused_act, dn.act_lo, dn.act_hi,
                            ptr_of(p, n.inputs[1]), bp, res, n.fused_act, n.act_lo, n.act_hi, ptr_of(p, n.outputs[0]),
                            (int)xs[0], (int)xs[1], (int)xs[2], (int)xs[3], (int)ys[1], ctx->stream);
+}
+
+// Stem conv + MaxPool (Plan::stem_pool) as one conv_stem.hip POOL launch and
+// its halo pass, at the pool op's position.
+rtenhip_status Graph::exec_stem_pool(Plan& p, int op_id) {
+  const Node& pn = nodes[op_id];
+  const Node& cn = nodes[p.stem_pool.at(op_id)];
+  const Shape* xsp = plan_shape(*this, p, cn.inputs[0]);
+  if (!xsp || p.padded.count(pn.outputs[0])) return fail(RTENHIP_HIP_ERROR, "stem + max pool: unexpected layout");
+  const Shape& xs = *xsp;
+  const Shape& wsh = nodes[cn.inputs[1]].shape;
+  ConvAttrs ca = conv_attrs(cn, false);
+  rtenhip_tensor xt = desc(nullptr, xs), wt = desc(nullptr, wsh);
+  ConvPlan g;
+  rtenhip_status st = plan_conv(&xt, &wt, ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(), ca.groups, g);
+  if (st) return st;
+  hipStream_t s = ctx->stream;
+  const int64_t K = g.C * g.kh * g.kw;
+  Plan::StemPoolExec& se = p.stem_pool_exec[op_id];
+  if (!se.packed) {
+    RTENHIP_HIP_CHECK(hipMalloc(&se.packed, (size_t)stem_weight_floats(g.O, K) * 4));
+    RTENHIP_HIP_CHECK(hipMalloc(&se.halo, (size_t)std::max<int64_t>(stem_pool_halo_floats(g), 4) * 4));
+    if ((st = pack_stem_weights(ptr_of(p, cn.inputs[1]), g.O, K, se.packed, s))) return st;
+  }
+  ConvDmaArgs a{};
+  a.x_unpadded = ptr_of(p, cn.inputs[0]);
+  a.N = g.N;
+  a.C = g.C;
+  a.H = g.H;
+  a.W = g.W;
+  a.O = g.O;
+  a.kh = g.kh;
+  a.kw = g.kw;
+  a.sh = g.sh;
+  a.sw = g.sw;
+  a.dh = g.dh;
+  a.dw = g.dw;
+  a.oh = g.oh;
+  a.ow = g.ow;
+  a.groups = g.groups;
+  a.pad_t = g.pads[0];
+  a.pad_l = g.pads[1];
+  a.packed_w = se.packed;
+  a.bias = cn.inputs.size() > 2 && cn.inputs[2] >= 0 ? ptr_of(p, cn.inputs[2]) : nullptr;
+  a.act = cn.fused_act;
+  return conv_stem_pool(a, ptr_of(p, pn.outputs[0]), se.halo, s);
 }
 
 // conv3 -> next conv1 pair (Plan::conv_pair) as one conv_pair.hip launch.
@@ -3017,6 +3115,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+project)";
         if (plan->conv_pair.count(plan->ops[i])) key = "Conv(conv3+conv1)";
         if (plan->pair_hold.count(plan->ops[i])) key = "Conv(in_pair)";
+        if (plan->stem_pool.count(plan->ops[i])) key = "Conv(stem+pool)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
@@ -3065,6 +3164,17 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           os << "  (in its conv3's dual GEMM)";
         } else if (plan->pair_hold.count(plan->ops[i])) {
           os << "  (in its conv3's pair kernel)";
+        } else if (plan->stem_pool.count(plan->ops[i])) {
+          // The stem conv's FLOPs (the pool is the kernel's epilogue); the
+          // conv's output is never written (stem_out = its floats).
+          const Node& cn = nodes[plan->stem_pool.at(plan->ops[i])];
+          const Shape& ws = nodes[cn.inputs[1]].shape;
+          const Shape& ps = plan->slots[n.outputs[0]].shape;
+          const double npx = (double)ps[0] * ps[2] * ps[3] * 4;
+          const double fl = 2.0 * ws[0] * (double)ws[1] * ws[2] * ws[3] * npx;
+          snprintf(buf, sizeof buf, "  stem+pool M=%lld N=%lld K=%lld stem_out=%.0f %.1f TF/s", (long long)ws[0],
+                   (long long)npx, (long long)(ws[1] * ws[2] * ws[3]), npx * ws[0], ms > 0 ? fl / (ms * 1e9) : 0.0);
+          os << buf;
         } else if (pr != plan->conv_pair.end() && ce != plan->convs.end()) {
           // One launch computes both convs of the pair: its time and FLOPs are
           // booked here together (the conv1's row has none).

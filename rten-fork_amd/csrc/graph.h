@@ -215,6 +215,15 @@ struct Plan {
   // Projection convs running their depthwise conv too (see Node::fd_op): op id
   // -> the depthwise conv's input value, which the projection op then reads.
   std::map<int, int> dwpw_fused;
+  // MaxPool ops running their stem conv too (conv_stem.hip POOL): pool op ->
+  // the conv op (out of the plan; its output never exists); the weights
+  // packed for the stem kernel and the halo rows between bands.
+  std::map<int, int> stem_pool;
+  struct StemPoolExec {
+    float* packed = nullptr;
+    float* halo = nullptr;
+  };
+  std::map<int, StemPoolExec> stem_pool_exec;
   // Grouped MatMuls (MatMulExec::nseg): leader op -> members (leader first),
   // members run by their leader; the members' outputs are segments of one
   // arena block of [nseg][M][N].
@@ -399,6 +408,7 @@ struct Graph {
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_dw_project(Plan& p, int op_id);
   rtenhip_status exec_conv_pair(Plan& p, int op_id);
+  rtenhip_status exec_stem_pool(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   // The packed-A store a producer of value v makes this run, or false.
