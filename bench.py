@@ -402,7 +402,7 @@ class Workload:
             self.hold_timeouts += "hold timed out" in report.splitlines()[0]
             for line in report.splitlines()[1:]:
                 name = line.split()[0]
-                if name.startswith(("Conv", "MatMul", "FusedAttention")) or name == "Gemm":
+                if name.startswith(("Conv", "MatMul", "FusedAttention", "Gemm")):
                     ms += float(line.split()[1])
         g.set_timing(False)
         self.report = report
