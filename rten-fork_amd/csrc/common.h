@@ -113,12 +113,6 @@ rtenhip_status launch_gemm(const GemmDesc& d, hipStream_t s);
 // gemv with the reference's summation order (gemm.rs:651-704, kernels.rs:26-194).
 // cin (optional): the beta * C operand read from cin[c * cin_stride] instead
 // of out (a broadcast Gemm C without materialising it into out first).
-// GlobalAveragePool -> Flatten -> Gemm (transposed weights, one row) in one
-// launch (gemm_mfma.hip gap_gemv_t_kernel): x [K][HW] planes, b [N][K].
-bool gap_gemv_eligible(int64_t K, int64_t HW, int64_t b_rs);
-rtenhip_status launch_gap_gemv(int64_t N, int64_t K, const float* x, int64_t HW, const float* b, int64_t b_cs,
-                               float* out, float alpha, float beta, int64_t ref_threads, hipStream_t s,
-                               const float* cin, int64_t cin_stride);
 rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b, int64_t b_rs,
                            int64_t b_cs, float* out, float alpha, float beta, const float* bias,
                            int64_t ref_threads, hipStream_t s, const float* cin = nullptr,

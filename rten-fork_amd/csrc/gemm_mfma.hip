@@ -587,8 +587,7 @@ __global__ void gemv_kernel(int64_t N, int64_t K, const float* __restrict__ a,
 // block's remainder k's are chained by the group's first lane, and lane 0
 // folds the blocks in K order (alpha*acc + eb*out, eb = beta then 1).  Columns
 // in a chunk's partial 8-wide tile take simd_gemv_fallback on lane 0.
-// One output column c of the transposed gemv (the body of gemv_t_kernel; a
-// may point into LDS, see gap_gemv_t_kernel).
+// One output column c of the transposed gemv (the body of gemv_t_kernel).
 __device__ __forceinline__ void gemv_t_column(const int64_t c, int64_t N, int64_t K, const float* a,
                                               const float* __restrict__ b, int64_t b_cs, float* __restrict__ out,
                                               float alpha, float beta, const float* __restrict__ bias, int64_t bbs,
@@ -621,6 +620,20 @@ __device__ __forceinline__ void gemv_t_column(const int64_t c, int64_t N, int64_
       const int64_t nfull = (k1 - k0) / 8 * 8;
       float l = 0.f;
       int64_t d = 0;
+      if (nfull == KB) {
+        // A whole 512-deep block: all 64 of the lane's operand pairs are
+        // loaded before its chain runs (one memory round trip instead of one
+        // per 64 k); the same fma order as the loop below.
+        float av[64], bv[64];
+#pragma unroll
+        for (int u = 0; u < 64; u++) {
+          av[u] = a[k0 + 8 * u + j];
+          bv[u] = col[k0 + 8 * u + j];
+        }
+#pragma unroll
+        for (int u = 0; u < 64; u++) l = __fmaf_rn(av[u], bv[u], l);
+        d = KB;
+      }
       for (; d + 64 <= nfull; d += 64) {
         float av[8], bv[8];
 #pragma unroll
@@ -661,80 +674,6 @@ __global__ __launch_bounds__(256) void gemv_t_kernel(int64_t N, int64_t K,
   const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= N) return;  // whole wave
   gemv_t_column(c, N, K, a, b, b_cs, out, alpha, beta, bias, bbs, cin, cin_stride);
-}
-
-// GlobalAveragePool -> Flatten -> Gemm at batch 1 (the classifier head) in
-// one launch: every 1024-thread workgroup first forms the whole pooled vector
-// a[k] = (x[k][0] + x[k][1] + ... + x[k][HW-1]) / HW in LDS -- the same
-// sequential chain from +0 and the same division as gap_lds_kernel
-// (pooling.rs:294-342) -- from coalesced loads staged 512 planes at a time,
-// then each of its 16 waves runs one column of gemv_t_kernel's reduction
-// (simd_gemv_transposed's order) on it.  The pooled vector never goes to HBM
-// and the two launches become one.
-constexpr int kGapGemvThreads = 1024, kGapGemvChunk = 512;
-__global__ __launch_bounds__(kGapGemvThreads) void gap_gemv_t_kernel(int64_t N, int64_t K, const float* __restrict__ x,
-                                                                    int HW, const float* __restrict__ b, int64_t b_cs,
-                                                                    float* __restrict__ out, float alpha, float beta,
-                                                                    int64_t bbs, const float* __restrict__ cin,
-                                                                    int64_t cin_stride) {
-  extern __shared__ float gg_lds[];
-  float* av = gg_lds;              // [K]
-  float* st = gg_lds + K;          // [kGapGemvChunk][HW]
-  const int t = threadIdx.x;
-  for (int64_t k0 = 0; k0 < K; k0 += kGapGemvChunk) {
-    const int np = (int)min((int64_t)kGapGemvChunk, K - k0);
-    const int n = np * HW;
-    const float* src = x + k0 * HW;
-    // (all of a thread's loads issued before its LDS stores)
-    constexpr int U = 8;
-    for (int e0 = 0; e0 < n; e0 += U * kGapGemvThreads) {
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int e = e0 + u * kGapGemvThreads + t;
-        v[u] = e < n ? src[e] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int e = e0 + u * kGapGemvThreads + t;
-        if (e < n) st[e] = v[u];
-      }
-    }
-    __syncthreads();
-    if (t < np) {
-      const float* p = st + t * HW;
-      float acc = 0.f;
-      for (int q = 0; q < HW; q++) acc = __fadd_rn(acc, p[q]);
-      av[k0 + t] = __fdiv_rn(acc, (float)HW);
-    }
-    __syncthreads();
-  }
-  const int64_t c = (int64_t)blockIdx.x * (kGapGemvThreads / 64) + (t >> 6);
-  if (c >= N) return;  // whole wave
-  gemv_t_column(c, N, K, av, b, b_cs, out, alpha, beta, nullptr, bbs, cin, cin_stride);
-}
-
-bool gap_gemv_eligible(int64_t K, int64_t HW, int64_t b_rs) {
-  return b_rs == 1 && K > 0 && HW > 0 && HW <= 64 && (K + kGapGemvChunk * HW) * 4 <= 160 * 1024 - 1024;
-}
-
-rtenhip_status launch_gap_gemv(int64_t N, int64_t K, const float* x, int64_t HW, const float* b, int64_t b_cs,
-                               float* out, float alpha, float beta, int64_t ref_threads, hipStream_t s,
-                               const float* cin, int64_t cin_stride) {
-  if (!gap_gemv_eligible(K, HW, 1)) return fail(RTENHIP_UNSUPPORTED_VALUE, "pool + gemv: unsupported shape");
-  if (N <= 0) return RTENHIP_OK;
-  int64_t t = ref_threads > 0 ? ref_threads : 1;
-  int64_t bbs = (N + t - 1) / t;  // gemm.rs:673, as launch_gemv
-  if (bbs < 128) bbs = 128;
-  const size_t lds = (size_t)(K + kGapGemvChunk * HW) * 4;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)gap_gemv_t_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  RTENHIP_HIP_CHECK(attr);
-  const int64_t cols = kGapGemvThreads / 64;
-  hipLaunchKernelGGL(gap_gemv_t_kernel, dim3((unsigned)((N + cols - 1) / cols)), dim3(kGapGemvThreads), lds, s, N, K,
-                     x, (int)HW, b, b_cs, out, alpha, beta, bbs, cin, cin_stride);
-  RTENHIP_LAUNCH_CHECK();
-  return RTENHIP_OK;
 }
 
 rtenhip_status launch_gemv(int64_t N, int64_t K, const float* a, const float* b, int64_t b_rs,

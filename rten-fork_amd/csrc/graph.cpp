@@ -903,41 +903,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.stem_pool[op] = cop;
       drop.push_back(cop);
     }
-    // GlobalAveragePool -> Flatten -> Gemm at batch 1 (the classifier head):
-    // the pool and the Flatten leave the plan, the Gemm runs all three
-    // (gap_gemv_t_kernel, the gemv order rtenhip_gemm_op_f32 takes there).
-    const bool gap_fc_off = getenv("RTENHIP_POOL_FC") && getenv("RTENHIP_POOL_FC")[0] == '0';  // A/B runs
-    for (int op : p.ops) {
-      const Node& n = nodes[op];
-      if (gap_fc_off || n.op_type != "GlobalAveragePool" || n.inputs.empty() || n.outputs.size() != 1) continue;
-      const int gv = n.outputs[0];
-      if (outset0.count(gv) || uses_of_value(p.ops, gv) != 1) continue;
-      int fop = -1, mop = -1;
-      for (int o : p.ops)
-        if (nodes[o].op_type == "Flatten" && !nodes[o].inputs.empty() && nodes[o].inputs[0] == gv) fop = o;
-      if (fop < 0 || nodes[fop].outputs.size() != 1 || nodes[fop].attrs.num("axis", 1) != 1) continue;
-      const int fv = nodes[fop].outputs[0];
-      if (outset0.count(fv) || uses_of_value(p.ops, fv) != 1) continue;
-      for (int o : p.ops)
-        if (nodes[o].op_type == "Gemm" && !nodes[o].inputs.empty() && nodes[o].inputs[0] == fv) mop = o;
-      if (mop < 0) continue;
-      const Node& m = nodes[mop];
-      const Shape* xs = shape_of(n.inputs[0]);
-      if (!xs || xs->size() != 4 || (*xs)[0] != 1 || p.dtypes[n.inputs[0]] == RTENHIP_DTYPE_INT32) continue;
-      const int64_t K = (*xs)[1], HW = (*xs)[2] * (*xs)[3];
-      if (m.inputs.size() < 3 || m.inputs[1] < 0 || m.inputs[2] < 0 ||
-          nodes[m.inputs[1]].kind != NodeKind::Constant || nodes[m.inputs[2]].kind != NodeKind::Constant ||
-          m.attrs.num("transA", 0) != 0 || m.attrs.num("transB", 0) != 1 || m.attrs.num("beta", 1.0) == 0.0)
-        continue;
-      const Shape& ws = nodes[m.inputs[1]].shape;
-      const Shape& cs = nodes[m.inputs[2]].shape;
-      if (ws.size() != 2 || ws[1] != K || !(cs == Shape{ws[0]} || cs == Shape{1, ws[0]}) ||
-          !gap_gemv_eligible(K, HW, 1))
-        continue;
-      p.gap_fc[mop] = op;
-      drop.push_back(op);
-      drop.push_back(fop);
-    }
     if (!drop.empty()) {
       std::vector<int> kept;
       for (int op : p.ops)
@@ -1180,8 +1145,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       if (df != p.dwpw_fused.end()) readers[df->second].push_back(op);
       auto sp = p.stem_pool.find(op);
       if (sp != p.stem_pool.end()) readers[nodes[sp->second].inputs[0]].push_back(op);
-      auto gf = p.gap_fc.find(op);
-      if (gf != p.gap_fc.end()) readers[nodes[gf->second].inputs[0]].push_back(op);
     }
     for (auto& kv : p.convs) {
       if (kv.second.fc) continue;
@@ -1424,8 +1387,6 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (df != p.dwpw_fused.end()) drop_use(df->second);
     auto spf = p.stem_pool.find(op);
     if (spf != p.stem_pool.end()) drop_use(nodes[spf->second].inputs[0]);
-    auto gff = p.gap_fc.find(op);
-    if (gff != p.gap_fc.end()) drop_use(nodes[gff->second].inputs[0]);
     auto cdu = p.conv_dual.find(op);
     if (cdu != p.conv_dual.end()) drop_use(nodes[cdu->second].inputs[0]);
     auto ph = p.pair_hold.find(op);
@@ -1529,7 +1490,6 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
     return rtenhip_cast_i32_to_f32(c, reinterpret_cast<const rtenhip_tensor_i32*>(&x), &y);
   }
   if (t == "MaxPool" && p.stem_pool.count(op_id)) return exec_stem_pool(p, op_id);
-  if (t == "Gemm" && p.gap_fc.count(op_id)) return exec_gap_fc(p, op_id);
   if (t == "Conv" && p.expand_fused.count(op_id)) return exec_expand_dw(p, op_id);
   if (t == "Conv" && p.dwpw_fused.count(op_id)) return exec_dw_project(p, op_id);
   if (t == "Conv" && p.conv_pair.count(op_id)) return exec_conv_pair(p, op_id);
@@ -1857,21 +1817,6 @@ rtenhip_status Graph::exec_stem_pool(Plan& p, int op_id) {
   a.bias = cn.inputs.size() > 2 && cn.inputs[2] >= 0 ? ptr_of(p, cn.inputs[2]) : nullptr;
   a.act = cn.fused_act;
   return conv_stem_pool(a, ptr_of(p, pn.outputs[0]), se.halo, s);
-}
-
-// GlobalAveragePool -> Flatten -> Gemm at batch 1 (Plan::gap_fc) as one
-// gap_gemv_t_kernel launch: the arguments rtenhip_gemm_op_f32 passes to the
-// gemv for this Gemm (alpha, beta, C read in place), the pool's input as A.
-rtenhip_status Graph::exec_gap_fc(Plan& p, int op_id) {
-  const Node& m = nodes[op_id];
-  const Node& gn = nodes[p.gap_fc.at(op_id)];
-  const Shape* xsp = plan_shape(*this, p, gn.inputs[0]);
-  if (!xsp) return fail(RTENHIP_HIP_ERROR, "pool + gemm: missing shapes");
-  const Shape& xs = *xsp;
-  const Shape& ws = nodes[m.inputs[1]].shape;
-  return launch_gap_gemv(ws[0], xs[1], ptr_of(p, gn.inputs[0]), xs[2] * xs[3], ptr_of(p, m.inputs[1]), ws[1],
-                         ptr_of(p, m.outputs[0]), (float)m.attrs.num("alpha", 1.0), (float)m.attrs.num("beta", 1.0),
-                         ctx->ref_threads, ctx->stream, ptr_of(p, m.inputs[2]), 1);
 }
 
 // conv3 -> next conv1 pair (Plan::conv_pair) as one conv_pair.hip launch.
@@ -3171,7 +3116,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (plan->conv_pair.count(plan->ops[i])) key = "Conv(conv3+conv1)";
         if (plan->pair_hold.count(plan->ops[i])) key = "Conv(in_pair)";
         if (plan->stem_pool.count(plan->ops[i])) key = "Conv(stem+pool)";
-        if (plan->gap_fc.count(plan->ops[i])) key = "Gemm(pool+fc)";
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";

@@ -224,9 +224,6 @@ struct Plan {
     float* halo = nullptr;
   };
   std::map<int, StemPoolExec> stem_pool_exec;
-  // Gemm ops running their GlobalAveragePool (and the Flatten between) too at
-  // batch 1 (gap_gemv_t_kernel): Gemm op -> the pool op (out of the plan).
-  std::map<int, int> gap_fc;
   // Grouped MatMuls (MatMulExec::nseg): leader op -> members (leader first),
   // members run by their leader; the members' outputs are segments of one
   // arena block of [nseg][M][N].
@@ -412,7 +409,6 @@ struct Graph {
   rtenhip_status exec_dw_project(Plan& p, int op_id);
   rtenhip_status exec_conv_pair(Plan& p, int op_id);
   rtenhip_status exec_stem_pool(Plan& p, int op_id);
-  rtenhip_status exec_gap_fc(Plan& p, int op_id);
   rtenhip_status exec_matmul(Plan& p, int op_id, rtenhip_tensor a, rtenhip_tensor b, rtenhip_tensor y);
   rtenhip_status exec_attention(Plan& p, int op_id, rtenhip_tensor y);
   // The packed-A store a producer of value v makes this run, or false.

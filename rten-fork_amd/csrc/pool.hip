@@ -203,7 +203,12 @@ __global__ __launch_bounds__(256) void gap_lds_kernel(const float* __restrict__ 
 
 rtenhip_status launch_gap(const float* x, float* y, int64_t NC, int64_t HW, hipStream_t s) {
   if (NC == 0) return RTENHIP_OK;
-  const int64_t ppb = std::min<int64_t>(256, HW > 0 ? 12288 / HW : 0);
+  // Planes per block: at most 256 and 12288 floats of LDS; fewer when that
+  // would leave most CUs idle (ResNet-50's 2048 planes of 7 x 7 at batch 1:
+  // 64 blocks of 32 planes, one memory round trip each, instead of 9 blocks
+  // staging 12250 floats in six).
+  int64_t ppb = std::min<int64_t>(256, HW > 0 ? 12288 / HW : 0);
+  if (ppb >= 32 && NC < 256 * ppb) ppb = std::max<int64_t>(32, std::min(ppb, (NC + 255) / 256));
   if (HW > 0 && ppb >= 32 && NC / ppb < (int64_t(1) << 31)) {
     const int64_t blocks = (NC + ppb - 1) / ppb;
     hipLaunchKernelGGL(gap_lds_kernel, dim3((unsigned)blocks), dim3(256),

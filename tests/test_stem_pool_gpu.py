@@ -1,6 +1,4 @@
-"""Fusions at the two ends of ResNet-50.
-
-1. The stem (Conv 7x7 / 2, pads 3, + bias, Relu) and its MaxPool 3x3 / 2
+"""The stem (Conv 7x7 / 2, pads 3, + bias, Relu) and its MaxPool 3x3 / 2
 / pads 1 as one pass (csrc/conv_stem.hip POOL + stem_pool_finish_kernel)
 against the CPU oracle running the two operators apart: conv_2d (src/ops/
 conv.rs:86-280, one KC block) then pool_impl's (ky, kx) f32::max fold
@@ -8,14 +6,7 @@ conv.rs:86-280, one KC block) then pool_impl's (ky, kx) f32::max fold
 2b takes the band's two rows and band b - 1's halo row.  Bar: bit-exact,
 eager and replayed, with and without bias, with NaN / inf / large negative
 inputs (Relu maps them to +0 / +inf, so every pooled value is a max over
-non-negative, non-NaN numbers), and with RTENHIP_STEM_POOL=0 (apart).
-
-2. The classifier head at batch 1 -- GlobalAveragePool -> Flatten -> Gemm
-(transB) -- as one launch (gemm_mfma.hip gap_gemv_t_kernel): the pool's
-sequential per-plane sum and division (pooling.rs:294-342), then the gemv
-order RTen takes for one row (gemm.rs:651-704, simd_gemv_transposed).
-Bit-exact against the oracle, with alpha / beta != 1, a [1, N] C, and with
-RTENHIP_POOL_FC=0 (apart)."""
+non-negative, non-NaN numbers), and with RTENHIP_STEM_POOL=0 (apart)."""
 import numpy as np
 import pytest
 
@@ -112,43 +103,3 @@ def test_stem_pool_not_taken_off_shape(rh):
         torch.cuda.synchronize()
         assert "Conv(stem+pool)" not in g.timing_report()
 
-
-def _head_net(K, N, alpha, beta, c2d, seed=9):
-    from rten_hip.graph import ModelSpec
-
-    rng = np.random.default_rng(seed)
-    m = ModelSpec("head")
-    x = m.value("x")
-    m.inputs = ["x"]
-    w = m.const("w", rng.uniform(-0.05, 0.05, (N, K)).astype(np.float32))
-    c = m.const("c", rng.uniform(-0.1, 0.1, (1, N) if c2d else (N,)).astype(np.float32))
-    f = m.op("Flatten", [m.op("GlobalAveragePool", [x])], {"axis": 1})
-    m.outputs = [m.op("Gemm", [f, w, c], {"transB": 1, "alpha": alpha, "beta": beta})]
-    return m
-
-
-@pytest.mark.parametrize("K,HW,N,alpha,beta,c2d,policy", [
-    (2048, 7, 1000, 1.0, 1.0, False, "on"),    # ResNet-50's head
-    (512, 4, 300, 0.5, 2.0, True, "on"),
-    (1280, 7, 1000, 1.0, 1.0, False, "off"),   # MobileNetV2's head, apart
-])
-def test_pool_fc_batch1_bitexact(rh, monkeypatch, K, HW, N, alpha, beta, c2d, policy):
-    import torch
-    import graph_runner
-
-    if policy == "off":
-        monkeypatch.setenv("RTENHIP_POOL_FC", "0")
-    spec = _head_net(K, N, alpha, beta, c2d)
-    x = np.random.default_rng(K).uniform(0, 2, (1, K, HW, HW)).astype(np.float32)
-    exp = graph_runner.run(spec, {"x": x})[spec.outputs[0]]
-    g = spec.to_graph()
-    xd = torch.from_numpy(x).cuda()
-    out = None
-    for r in range(3):
-        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
-        torch.cuda.synchronize()
-        assert _bits_equal(out[0].cpu().numpy(), exp), f"run {r}"
-    g.set_timing(True)
-    g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
-    torch.cuda.synchronize()
-    assert ("Gemm(pool+fc)" in g.timing_report()) == (policy == "on")
