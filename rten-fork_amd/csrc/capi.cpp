@@ -249,7 +249,7 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     }
     set_conv_bvec(a, cfg, tile, d);
     if (a.split) {
-      const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg, a.split);
+      const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
       if (sp.split_tiles > 0 && a.ws && a.counters && sp.ws_floats <= a.ws_cap && sp.counters <= a.cnt_cap) {
         d.split_tiles = sp.split_tiles;
         d.nkb = sp.nkb;
@@ -530,7 +530,7 @@ rtenhip_status conv_impl(Ctx* c, const rtenhip_tensor* x, const rtenhip_tensor* 
         a.ws = c->scratch_floats((size_t)sp.ws_floats, 3);
         a.counters = c->split_counters((size_t)sp.counters);
         if (!a.ws || !a.counters) return fail(RTENHIP_HIP_ERROR, "scratch allocation failed");
-        a.split = 1;
+        a.split = true;
         a.ws_cap = sp.ws_floats;
         a.cnt_cap = sp.counters;
       }
@@ -726,7 +726,7 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
     d.kstride = (int)a.b_rs;
   }
   if (a.split) {
-    const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg, a.split);
+    const DmaSplit sp = dma_split_plan(d.M, d.N, d.K, cfg);
     if (sp.split_tiles > 0) {
       float* ws = a.ws;
       int* cnt = a.counters;
@@ -799,7 +799,7 @@ rtenhip_status gemm_impl(Ctx* c, int64_t m, int64_t n, int64_t k, const float* a
     da.bias = bias;
     da.act = act;
     da.cfg = -1;
-    da.split = g_split_enabled ? 1 : 0;
+    da.split = g_split_enabled;
     return gemm_dense_dma(c, da);
   }
   return launch_gemm(d, s);

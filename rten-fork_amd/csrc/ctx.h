@@ -87,7 +87,7 @@ struct ConvDmaArgs {
   int cfg;                      // DMA kernel configuration, -1 = default
   // KC split of the remainder tiles (dma_split_plan): enabled when split is
   // set and the caller's workspace / zeroed counters are large enough.
-  int split;  // 0 off, else the split round (dma_split_plan)
+  bool split;
   float* ws;
   int64_t ws_cap;
   int* counters;
@@ -196,7 +196,7 @@ struct DenseDmaArgs {
   int cfg;         // -1 = dma_default_cfg
   float* pk;       // packed-A buffer (nullptr: ctx scratch slot 2)
   bool pack;       // pack A into pk first (false: pk already holds it)
-  int split;       // KC split of the remainder tiles: 0 off, else the round (dma_split_plan)
+  bool split;      // KC split of the remainder tiles
   float* ws;       // split workspace / zeroed counters (nullptr: ctx scratch)
   int64_t ws_cap;
   int* counters;

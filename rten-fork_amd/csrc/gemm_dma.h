@@ -97,9 +97,7 @@ struct DmaSplit {
   int split_tiles, nkb;
   int64_t ws_floats, counters;
 };
-// round: the remainder is taken over rounds of round * 256 tiles (one tile per
-// CU and round, or `round` per CU when that many run on a CU at once).
-DmaSplit dma_split_plan(int M, int N, int K, int cfg, int round = 1);
+DmaSplit dma_split_plan(int M, int N, int K, int cfg);
 
 // Tile order of dense MatMul DMA GEMMs (DmaDesc::swz; gemm_dma.hip).
 int dma_dense_swz();

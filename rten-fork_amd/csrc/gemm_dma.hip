@@ -77,7 +77,7 @@ int dma_default_cfg(int M, int N, int K) {
   return 7;
 }
 
-DmaSplit dma_split_plan(int M, int N, int K, int cfg, int round) {
+DmaSplit dma_split_plan(int M, int N, int K, int cfg) {
   DmaSplit sp{0, 0, 0, 0};
   const DmaCfgInfo& c = kDmaCfgs[cfg];
   const int tiles = ((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
@@ -86,7 +86,7 @@ DmaSplit dma_split_plan(int M, int N, int K, int cfg, int round) {
   // Whole tiles fill complete rounds of one tile per CU; the remainder would
   // run as a partial round, so it is split into KC blocks.
   constexpr int CUS = 256;
-  const int rem = tiles % (CUS * (round > 1 ? round : 1));
+  const int rem = tiles % CUS;
   if (rem == 0) return sp;
   sp.split_tiles = rem;
   sp.nkb = nkb;

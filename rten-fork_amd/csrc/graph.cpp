@@ -2078,18 +2078,6 @@ struct TuneScratch {
 // RTENHIP_PERSIST=k (k >= 0) restricts the tuner to launch mode k (any k >= 1
 // is a valid persistent launch: the kernel caps k at its occupancy).
 static const int kPersistModes[4] = {0, 4, 5, 6};
-static std::string split_tag(int split) {
-  return split <= 0 ? std::string() : split == 1 ? std::string(" split") : " split" + std::to_string(split);
-}
-
-// Whether the KC split at this round is worth timing: it splits something,
-// and (round > 1) something else than round 1 does.
-static bool split_useful(int64_t M, int64_t N, int64_t K, int cfg, int round) {
-  const DmaSplit sp = dma_split_plan((int)M, (int)N, (int)K, cfg, round);
-  if (sp.split_tiles == 0) return false;
-  return round <= 1 || sp.split_tiles != dma_split_plan((int)M, (int)N, (int)K, cfg, 1).split_tiles;
-}
-
 static std::vector<int> persist_candidates(int forced) {
   if (forced >= 0) return {forced};
   return std::vector<int>(kPersistModes, kPersistModes + 4);
@@ -2137,10 +2125,10 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
     }
     return RTENHIP_OK;
   };
-  auto set_split = [&](MatMulExec& e, int cfg, int split) -> rtenhip_status {
-    e.split = 0;
+  auto set_split = [&](MatMulExec& e, int cfg, bool split) -> rtenhip_status {
+    e.split = false;
     if (!split) return RTENHIP_OK;
-    const DmaSplit sp = dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg, split);
+    const DmaSplit sp = dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg);
     if (sp.split_tiles == 0) return RTENHIP_OK;
     if (sp.ws_floats > e.ws_floats) {
       if (e.ws) RTENHIP_HIP_CHECK(hipFree(e.ws));
@@ -2155,7 +2143,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
       RTENHIP_HIP_CHECK(hipMemsetAsync(e.counters, 0, (size_t)sp.counters * 4, s));
       e.n_counters = sp.counters;
     }
-    e.split = split;
+    e.split = true;
     return RTENHIP_OK;
   };
   auto bind = [&](const MatMulExec& e, int cfg) {
@@ -2170,7 +2158,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
   };
   if (me.cfg < 0) {
     int chosen = dma_default_cfg((int)me.M, (int)me.N, (int)me.K);
-    int chosen_split = 0;
+    bool chosen_split = false;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
     // A MatMul with the same A value and shape already tuned (the Q/K/V
@@ -2204,10 +2192,10 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
         rtenhip_status st = ensure_pack(cfg);
         if (st) return st;
         for (int pm : persist_candidates(persist_mode)) {
-          for (int split : {0, 1, 4}) {
-            if (split && !split_useful(me.M, me.N, me.K, cfg, split)) continue;
+          for (int split = 0; split < 2; split++) {
+            if (split && dma_split_plan((int)me.M, (int)me.N, (int)me.K, cfg).split_tiles == 0) continue;
             trial.persist = pm;
-            st = set_split(trial, cfg, split);
+            st = set_split(trial, cfg, split != 0);
             if (st) return st;
             bind(trial, cfg);
             st = gemm_dense_dma(ctx, da);  // warm-up (the output is rewritten below)
@@ -2226,7 +2214,7 @@ rtenhip_status Graph::exec_matmul_dma(Plan& p, int op_id, const rtenhip_tensor& 
             if (ms < best_ms) {
               best_ms = ms;
               chosen = cfg;
-              chosen_split = split;
+              chosen_split = split != 0;
               chosen_persist = trial.persist;
             }
           }
@@ -2396,11 +2384,11 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   const float* w = ptr_of(p, n.inputs[1]);
   const int64_t opg = g.O / g.groups, K = (g.C / g.groups) * g.kh * g.kw;
   // KC-split buffers for (cfg, split), plan-owned.
-  auto set_split = [&](ConvExec& e, int cfg, int split) -> rtenhip_status {
-    e.split = 0;
+  auto set_split = [&](ConvExec& e, int cfg, bool split) -> rtenhip_status {
+    e.split = false;
     if (!split) return RTENHIP_OK;
     const DmaSplit sp = is_lat_cfg(cfg) ? lat_split_plan((int)opg, (int)(g.N * P), (int)K, cfg - kLatCfgBase)
-                                        : dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg, split);
+                                        : dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg);
     if (sp.split_tiles == 0) return RTENHIP_OK;
     if (sp.ws_floats > e.ws_floats) {
       if (e.ws) RTENHIP_HIP_CHECK(hipFree(e.ws));
@@ -2415,7 +2403,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       RTENHIP_HIP_CHECK(hipMemsetAsync(e.counters, 0, (size_t)sp.counters * 4, s));
       e.n_counters = sp.counters;
     }
-    e.split = split;
+    e.split = true;
     return RTENHIP_OK;
   };
   // Pointwise VALU kernel (conv_pointwise.hip) as a further tuner candidate.
@@ -2476,7 +2464,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   };
   if (ce.cfg < 0) {
     int chosen = dma_default_cfg((int)opg, (int)(g.N * P), (int)K);
-    int chosen_split = 0;
+    bool chosen_split = false;
     int chosen_persist = 0;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     (void)hipStreamIsCapturing(s, &cs);
@@ -2499,7 +2487,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
                             (slab_ok || lat_mode < 60 || lat_mode >= 70);
     if (lat_forced) {
       chosen = kLatCfgBase + lat_mode;
-      chosen_split = 1;
+      chosen_split = true;
     }
     if (autotune && cs == hipStreamCaptureStatusNone && !pw_forced && !lat_forced) {
       // Candidates are timed alone, after the work queued before them.
@@ -2555,12 +2543,12 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         bufs.push_back(pk);
         rtenhip_status st = pack_conv_weights(ctx, w, g, cfg, pk);
         if (st) return st;
-        static const int kSplits[] = {0, 1, 4};
-        for (int mode = 0; mode < 3 * (int)persist_candidates(persist_mode).size(); mode++) {
-          const int split = kSplits[mode % 3];
-          if (split && !split_useful(opg, g.N * P, K, cfg, split)) continue;
-          trial.persist = persist_candidates(persist_mode)[mode / 3];
-          st = set_split(trial, cfg, split);
+        for (int mode = 0; mode < 2 * (int)persist_candidates(persist_mode).size(); mode++) {
+          const int split = mode & 1;
+          if (split && dma_split_plan((int)opg, (int)(g.N * P), (int)K, cfg).split_tiles == 0)
+            continue;
+          trial.persist = persist_candidates(persist_mode)[mode >> 1];
+          st = set_split(trial, cfg, split != 0);
           if (st) return st;
           bind(trial);
           a.packed_w = pk;
@@ -2588,7 +2576,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           rtenhip_status st = pack_for(cfg, pk);
           if (st) return st;
           trial.persist = 0;
-          st = set_split(trial, cfg, 1);
+          st = set_split(trial, cfg, true);
           if (st) return st;
           bind(trial);
           a.packed_w = pk;
@@ -2609,7 +2597,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           rtenhip_status st = pack_for(cfg, pk);
           if (st) return st;
           trial.persist = 0;
-          st = set_split(trial, cfg, 0);
+          st = set_split(trial, cfg, false);
           if (st) return st;
           bind(trial);
           a.packed_w = pk;
@@ -2654,7 +2642,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
           rtenhip_status st = pack_for(cfg, pk);
           if (st) return st;
           trial.persist = 0;
-          st = set_split(trial, cfg, 0);
+          st = set_split(trial, cfg, false);
           if (st) return st;
           bind(trial);
           a.packed_w = pk;
@@ -2673,7 +2661,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
       for (size_t i = 0; i < cands.size() && i < 3; i++) {
         const Cand& c = cands[i];
         trial.persist = c.persist;
-        rtenhip_status st = set_split(trial, c.cfg, c.split);
+        rtenhip_status st = set_split(trial, c.cfg, c.split != 0);
         if (st) return st;
         bind(trial);
         a.packed_w = c.pk;
@@ -2685,7 +2673,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
         if (ms < best_ms) {
           best_ms = ms;
           chosen = c.cfg;
-          chosen_split = c.split;
+          chosen_split = c.split != 0;
           chosen_persist = c.persist;
         }
       }
@@ -2696,7 +2684,7 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
     RTENHIP_HIP_CHECK(hipMalloc(&ce.packed, (size_t)weight_floats(chosen) * 4));
     rtenhip_status st = pack_for(chosen, ce.packed);
     if (st) return st;
-    st = set_split(ce, chosen, chosen < kPwCfgBase ? chosen_split : 0);
+    st = set_split(ce, chosen, chosen_split && chosen < kPwCfgBase);
     if (st) return st;
     ce.cfg = chosen;
     ce.persist = (chosen >= kPwCfgBase || is_lat_cfg(chosen)) ? 0 : persist_mode >= 0 ? persist_mode : chosen_persist;
@@ -3218,7 +3206,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
                                     : is_lat_cfg(cc) ? "lat" + std::to_string(cc - kLatCfgBase)
                                                      : std::to_string(cc);
           snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%s%s%s %.1f TF/s", gm, gn, gk,
-                   cname.c_str(), split_tag(ce->second.split).c_str(), pers_tag(ce->second.persist), ms > 0 ? fl / (ms * 1e9) : 0.0);
+                   cname.c_str(), ce->second.split ? " split" : "", pers_tag(ce->second.persist), ms > 0 ? fl / (ms * 1e9) : 0.0);
           os << buf;
         }
         auto me = plan->matmuls.find(plan->ops[i]);
@@ -3228,7 +3216,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           const MatMulExec& m = me->second;
           const double fl = 2.0 * m.M * (double)m.N * m.K;
           snprintf(buf, sizeof buf, "  M=%lld N=%lld K=%lld cfg=%d%s%s%s %.1f TF/s", (long long)m.M,
-                   (long long)m.N, (long long)m.K, m.cfg, split_tag(m.split).c_str(), pers_tag(m.persist),
+                   (long long)m.N, (long long)m.K, m.cfg, m.split ? " split" : "", pers_tag(m.persist),
                    m.nseg > 1 ? (" group" + std::to_string(m.nseg)).c_str() : "", ms > 0 ? fl / (ms * 1e9) : 0.0);
           os << buf;
         }

@@ -139,7 +139,7 @@ struct ConvExec {
   ConvPlan g;
   int cfg = -1;             // kernel configuration (chosen on the first run)
   float* packed = nullptr;  // weights packed for cfg, owned by the plan
-  int split = 0;            // KC split of the remainder tiles: 0 off, else its round (dma_split_plan)
+  bool split = false;       // KC split of the remainder tiles (dma_split_plan)
   float* ws = nullptr;      // its workspace and arrival counters, plan-owned
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
@@ -159,7 +159,7 @@ struct ConvExec {
 struct MatMulExec {
   int64_t M, N, K, b_rs;
   int cfg = -1;          // kernel configuration (chosen on the first run)
-  int split = 0;         // 0 off, else the split round (dma_split_plan)
+  bool split = false;
   float* ws = nullptr;   // split workspace and arrival counters, plan-owned
   int* counters = nullptr;
   int64_t ws_floats = 0, n_counters = 0;
