@@ -390,7 +390,7 @@ class Workload:
         import torch
 
         g = self.g
-        g.set_timing(2)  # per-op times inside a replayed capture of the step
+        g.set_timing(True)
         ms, report = 0.0, ""
         self.hold_timeouts = 0
         for _ in range(runs):
@@ -477,9 +477,8 @@ class Workload:
         common = {"traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_desc,
                   "kernel_ms_per_step": round(kms, 4), "kernel_ms_eager_events": round(kernel_ms_eager, 4),
                   "capped": capped, "hold_timeouts": getattr(self, "hold_timeouts", 0),
-                  "timing": "per-op hipEvents recorded between the ops of a replayed hipGraph capture of the "
-                            "step (executor stream), dominant families summed; capped at ms_per_step when larger "
-                            "(capped: true)"}
+                  "timing": "per-op hipEvents on the executor stream over eager runs (stream held until the "
+                            "plan is queued), capped at ms_per_step when larger (capped: true)"}
         rp = rocprof_kernel_ms(self.model, self.B)
         if rp:
             # (the summary's commit vs the last commit that changed the sources)

@@ -329,11 +329,7 @@ rtenhip_status rtenhip_graph_synchronize(rtenhip_graph* g);
 rtenhip_status rtenhip_graph_set_deferred_checks(rtenhip_graph* g, int enabled);
 /* Output shape of a value after the last run (or -1). */
 int32_t rtenhip_graph_value_shape(rtenhip_graph* g, int32_t id, int64_t* shape);
-/* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled:
- * 1 = eager runs with an event pair around each op (stream held until the
- * plan is queued); 2 = a capture of the plan with a timing event between
- * consecutive ops, replayed like the step's hipGraph (the times of the
- * replayed kernels, inter-kernel gaps included). */
+/* Per-op timing table like RTEN_TIMING (graph.rs:1039-1055), when enabled. */
 rtenhip_status rtenhip_graph_set_timing(rtenhip_graph* g, int enabled);
 const char* rtenhip_graph_timing_report(rtenhip_graph* g);
 

@@ -2962,12 +2962,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     arena_cap = plan->arena_bytes;
   }
   const bool replay = use_hip_graph && !timing && plan->eager_runs >= 1;
-  // Timing mode 2: the per-op times of a REPLAYED plan -- a capture of the
-  // ops with a timing event recorded between consecutive ops, launched like
-  // the step's own hipGraph (no host launch pace, no per-op dispatch gaps of
-  // eager runs).
-  const bool replay_timing = timing && timing_mode == 2 && use_hip_graph && plan->eager_runs >= 1;
-  if (replay || replay_timing) {
+  if (replay) {
     // The ctx scratch buffers a capture bakes in must not move afterwards:
     // grow them to this plan's recorded needs now (outside any capture), and
     // re-capture when any of them was reallocated since this plan's capture
@@ -3068,45 +3063,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     // Timing run of a tuned plan: hold the stream until every op is queued,
     // so the event pairs measure the kernels, not the host's launch rate.
     // (Not on the plan's first run: its tuner synchronizes inside the ops.)
-    const bool hold = timing && plan->eager_runs >= 1 && !replay_timing;
-    std::vector<float> per_op_replay;
-    if (replay_timing) {
-      // Events between the ops of a capture of the plan; launched twice (the
-      // first launch of a fresh executable graph pays its upload), the
-      // second timed.
-      const size_t n_ops = plan->ops.size();
-      std::vector<hipEvent_t> tev(n_ops + 1, nullptr);
-      for (auto& e : tev) RTENHIP_HIP_CHECK(hipEventCreate(&e));
-      hipGraph_t tg = nullptr;
-      hipGraphExec_t tx = nullptr;
-      hipError_t e = hipStreamBeginCapture(exec_stream, hipStreamCaptureModeThreadLocal);
-      if (e == hipSuccess) {
-        for (size_t i = 0; i < n_ops && !st; i++) {
-          if (hipEventRecord(tev[i], exec_stream) != hipSuccess) st = fail(RTENHIP_HIP_ERROR, "timing event");
-          if (!st) st = run_op(plan->ops[i]);
-        }
-        if (!st && hipEventRecord(tev[n_ops], exec_stream) != hipSuccess) st = fail(RTENHIP_HIP_ERROR, "timing event");
-        if (!st) st = copy_static_outputs();
-        ctx->stream = exec_stream;
-        hipError_t e2 = hipStreamEndCapture(exec_stream, &tg);
-        if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&tx, tg, nullptr, nullptr, 0);
-        if (!st && e2 != hipSuccess) st = hip_fail(e2, "timing capture");
-      } else {
-        st = hip_fail(e, "hipStreamBeginCapture");
-      }
-      for (int rep = 0; rep < 2 && !st; rep++) {
-        hipError_t e3 = hipGraphLaunch(tx, exec_stream);
-        if (e3 == hipSuccess) e3 = hipStreamSynchronize(exec_stream);
-        if (e3 != hipSuccess) st = hip_fail(e3, "timing replay");
-      }
-      if (!st) {
-        per_op_replay.assign(n_ops, 0.f);
-        for (size_t i = 0; i < n_ops; i++) (void)hipEventElapsedTime(&per_op_replay[i], tev[i], tev[i + 1]);
-      }
-      if (tx) (void)hipGraphExecDestroy(tx);
-      if (tg) (void)hipGraphDestroy(tg);
-      for (auto& ev : tev) (void)hipEventDestroy(ev);
-    }
+    const bool hold = timing && plan->eager_runs >= 1;
     if (hold) {
       if (!hold_word) RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&hold_word), 2 * sizeof(int), hipHostMallocCoherent));
       __atomic_store_n(hold_word, 0, __ATOMIC_SEQ_CST);
@@ -3114,7 +3071,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       st = launch_hold(hold_word, 100.0, exec_stream);
     }
     for (int op : plan->ops) {
-      if (st || replay_timing) break;
+      if (st) break;
       hipEvent_t a = nullptr, b = nullptr;
       // (a downsample computed by its conv3's dual GEMM launches nothing: no events)
       // (nor does a conv1 computed by its conv3's pair kernel)
@@ -3138,18 +3095,16 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     if (hold) __atomic_store_n(hold_word, 1, __ATOMIC_SEQ_CST);  // release the queued plan
     ctx->scratch_log = nullptr;
     ctx->stream = exec_stream;
-    if (!st && !replay_timing) st = copy_static_outputs();
-    if (!replay_timing) plan->eager_runs++;
+    if (!st) st = copy_static_outputs();
+    plan->eager_runs++;
     if (timing && !st) {
       (void)hipStreamSynchronize(exec_stream);
       std::map<std::string, std::pair<double, int>> tot;
       double total = 0;
-      const size_t n_rows = replay_timing ? per_op_replay.size() : evs.size();
-      std::vector<float> per_op(n_rows, 0.f);
-      for (size_t i = 0; i < n_rows; i++) {
+      std::vector<float> per_op(evs.size(), 0.f);
+      for (size_t i = 0; i < evs.size(); i++) {
         float ms = 0;
-        if (replay_timing) ms = per_op_replay[i];
-        else if (evs[i].first) (void)hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
+        if (evs[i].first) (void)hipEventElapsedTime(&ms, evs[i].first, evs[i].second);
         per_op[i] = ms;
         const Node& n = nodes[plan->ops[i]];
         std::string key = n.op_type;
@@ -3180,9 +3135,8 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       // A hold that gave up before the plan was queued (word 1) leaves host
       // launch time inside the event pairs: the report says so.
       const bool hold_timeout = hold && __atomic_load_n(hold_word + 1, __ATOMIC_SEQ_CST) != 0;
-      snprintf(buf, sizeof buf, "Graph run of %zu ops finished in %.3f ms (device time%s)%s\n",
-               plan->ops.size(), total, replay_timing ? ", replayed hipGraph" : "",
-               hold_timeout ? " (hold timed out: times include host launch pace)" : "");
+      snprintf(buf, sizeof buf, "Graph run of %zu ops finished in %.3f ms (device time)%s\n",
+               plan->ops.size(), total, hold_timeout ? " (hold timed out: times include host launch pace)" : "");
       os << buf;
       for (auto& r : rows) {
         snprintf(buf, sizeof buf, "%-22s %10.3f ms (%5.2f%%)  x%d\n", r.second.c_str(), r.first,
@@ -3191,7 +3145,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       }
       // Per-op rows (RTEN_TIMING "by-shape" analogue): name, type, output shape.
       os << "--- per op ---\n";
-      for (size_t i = 0; i < per_op.size(); i++) {
+      for (size_t i = 0; i < evs.size(); i++) {
         const Node& n = nodes[plan->ops[i]];
         const float ms = per_op[i];
         std::string shp;
@@ -3917,7 +3871,6 @@ rtenhip_status rtenhip_graph_set_deferred_checks(rtenhip_graph* g, int enabled) 
 
 rtenhip_status rtenhip_graph_set_timing(rtenhip_graph* g, int enabled) {
   G_(g)->timing = enabled != 0;
-  G_(g)->timing_mode = enabled;
   return RTENHIP_OK;
 }
 

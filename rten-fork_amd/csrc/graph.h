@@ -336,7 +336,6 @@ struct Graph {
   hipStream_t exec_stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool timing = false;
-  int timing_mode = 0;  // 1: eager runs with per-op events; 2: a replayed capture with events between ops
   int* hold_word = nullptr;  // pinned coherent host words: [0] releases launch_hold, [1] set when it timed out
   bool use_hip_graph = true;
   // Gather index checks (Plan::gchk): false = each run waits for its own

@@ -126,10 +126,7 @@ class Graph:
     def node_id(self, name: str) -> int:
         return self.names[name]
 
-    def set_timing(self, enabled):
-        """RTEN_TIMING-style per-op report (rtenhip_graph_set_timing): True / 1
-        times eager runs op by op; 2 times a replayed capture of the plan
-        (timing events between its ops), as the hipGraph replay runs it."""
+    def set_timing(self, enabled: bool):
         check(lib().rtenhip_graph_set_timing(C.c_void_p(self.ptr), C.c_int(int(enabled))))
 
     def timing_report(self) -> str:
