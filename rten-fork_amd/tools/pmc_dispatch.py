@@ -24,8 +24,13 @@ def main():
             if "Start_Timestamp" in r:
                 d["dur"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
     ids = sorted(disp)
-    mark = max((i for i in ids if "rtenhip" not in disp[i]["name"]), default=-1)
-    after = [i for i in ids if i > mark and "rtenhip" in disp[i]["name"]]
+    # The marker is model_once's torch fill; the runtime's own copy / fill
+    # kernels (__amd_rocclr_*, e.g. BERT's int32 inputs) belong to the forwards.
+    def ours(i):
+        return "rtenhip" in disp[i]["name"] or "__amd_rocclr" in disp[i]["name"]
+
+    mark = max((i for i in ids if not ours(i)), default=-1)
+    after = [i for i in ids if i > mark and ours(i)]
     per = len(after) // fw if fw else len(after)
     last = after[-per:]
     print(f"{len(after)} dispatches after the marker, {per} per forward; the last forward:")
