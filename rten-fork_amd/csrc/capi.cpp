@@ -742,7 +742,7 @@ rtenhip_status gemm_dense_dma(Ctx* c, const DenseDmaArgs& a) {
     }
   }
   d.persist_k = a.persist_k;
-  d.swz = dma_dense_swz();  // strip tile order (dense MatMuls only)
+  d.swz = dma_dense_swz(a.K, dma_cfg_info_bn(cfg));  // strip tile order (dense MatMuls only)
   return launch_gemm_dma(d, cfg, s);
 }
 

@@ -100,7 +100,7 @@ struct DmaSplit {
 DmaSplit dma_split_plan(int M, int N, int K, int cfg);
 
 // Tile order of dense MatMul DMA GEMMs (DmaDesc::swz; gemm_dma.hip).
-int dma_dense_swz();
+int dma_dense_swz(int64_t K, int BN);
 
 // Kernel configurations (all bit-identical; see gemm_dma.hip).
 int dma_num_cfgs();
@@ -109,6 +109,8 @@ bool dma_cfg_bvec(int cfg);
 bool dma_cfg_vec_epilogue(int cfg);
 int dma_default_cfg(int M, int N, int K);
 DmaTile dma_cfg_tile(int cfg);
+// Tile width (BN) of DMA configuration cfg.
+int dma_cfg_info_bn(int cfg);
 int64_t packed_a_floats(int M, int K, const DmaTile& t);
 rtenhip_status launch_pack_a(const float* a, int64_t lda, int M, int K, const DmaTile& t,
                              float* out, hipStream_t s);

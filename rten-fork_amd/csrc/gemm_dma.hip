@@ -1,3 +1,4 @@
+#include <algorithm>
 // Host side of the LDS-DMA GEMM (kernel template: gemm_dma_kernel.h; the
 // tile configurations are instantiated in gemm_dma_p*.hip): configuration
 // table, default choice, KC split plan, launch dispatch, and the A pack
@@ -58,6 +59,8 @@ bool dma_cfg_vec_epilogue(int cfg) {
   }
 }
 
+int dma_cfg_info_bn(int cfg) { return cfg >= 0 && cfg < kNumDmaCfgs ? kDmaCfgs[cfg].bn : 64; }
+
 DmaTile dma_cfg_tile(int cfg) {
   const DmaCfgInfo& c = kDmaCfgs[cfg];
   return DmaTile{c.bm, c.bk, 1};  // k-quad layout, independent of the wave tile
@@ -95,10 +98,17 @@ DmaSplit dma_split_plan(int M, int N, int K, int cfg) {
   return sp;
 }
 
-// Tile order of dense MatMul DMA GEMMs (DmaDesc::swz): RTENHIP_DMA_SWZ_MM, default 8.
-int dma_dense_swz() {
+// Tile order of dense MatMul DMA GEMMs (DmaDesc::swz): strips of g tile
+// columns, n fastest within a strip, so a strip's B columns (g * BN * K
+// floats) stay in the XCD's L2 while its tiles walk down the rows.
+// RTENHIP_DMA_SWZ_MM=g fixes g for every GEMM; RTENHIP_DMA_SWZ_MM=-b sizes
+// the strip per GEMM to at most b KiB of B (A/B experiments).  Default 8.
+int dma_dense_swz(int64_t K, int BN) {
   static const int v = [] { const char* e = getenv("RTENHIP_DMA_SWZ_MM"); return e ? atoi(e) : 8; }();
-  return v;
+  if (v >= 0) return v;
+  const int64_t per_col = (int64_t)BN * K * 4;
+  const int64_t g = ((int64_t)-v * 1024) / (per_col > 0 ? per_col : 1);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(16, g));
 }
 
 rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const DmaDesc* d2) {
