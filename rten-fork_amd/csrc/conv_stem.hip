@@ -69,22 +69,15 @@ struct StemDesc {
   float* halo;      // POOL: [N, M, tiles_y, OW / 2] row-pooled last conv row of each band
 };
 
-#ifndef RTENHIP_STEM_PXR1
-#define RTENHIP_STEM_PXR1 1
-#endif
 constexpr int kStemThreads = 256;
 // Items (32 x 32 output tiles) per wave and band: 7 for large batches; 2 when
 // the batch has too few TR-row bands to fill the chip (batch 1: one output
 // row per band, 112 workgroups instead of 28).
 constexpr int kStemNT = 7, kStemNTSmall = 2;
-// 3x3 stems (MobileNetV2): 6 items per wave -- with pixels as the MFMA's rows
-// and one channel tile, 7 spill.
-constexpr int kStemNT3 = 6;
-constexpr int stem_nt(int kh) { return kh == 3 ? kStemNT3 : kStemNT; }
 // Staged rows per wave (a bound on C R / 4, in registers while the next band
 // is loaded): ResNet-50's band (TR = 4, 3 x 13 rows of 232) needs 10;
-// MobileNetV2's gets TR = 6 (3 x 13 rows) within 10.
-constexpr int stem_rows_cap(int kh) { return 10; }
+// MobileNetV2's gets TR = 7 (3 x 15 rows) within 12.
+constexpr int stem_rows_cap(int kh) { return kh == 7 ? 10 : 12; }
 constexpr int kStemLdsFloats = 20480;  // 80 KiB: two workgroups per CU
 
 template <int... Is, class F>
@@ -101,7 +94,7 @@ __global__ __launch_bounds__(kStemThreads, 2) void conv_stem_kernel(StemDesc d) 
   constexpr int SR = stem_rows_cap(KH);
   // Pixels as the MFMA's rows (vector stores in the epilogue) with two
   // channel tiles; with one, the 4-pixel groups' addresses and guards spill.
-  constexpr bool PXR = MT == 2 || RTENHIP_STEM_PXR1;
+  constexpr bool PXR = MT == 2;
   extern __shared__ float4 stem_lds4[];
   float* lds = reinterpret_cast<float*>(stem_lds4);
   float* wl = lds;                  // [NS][2][MW]
@@ -431,7 +424,7 @@ StemShape stem_shape(int C, int kh, int kw, int S, int OH, int OW, int64_t M, in
     while (r < OH && fits(r + 1, nt)) r++;
     return r;
   };
-  int nt = stem_nt(kh), tr = rows_for(nt);
+  int nt = kStemNT, tr = rows_for(nt);
   if (tr >= 1 && N * ((OH + tr - 1) / tr) < 2 * (int64_t)cus) {
     const int trs = rows_for(kStemNTSmall);
     if (trs >= 1) {
@@ -609,9 +602,9 @@ rtenhip_status conv_stem(const ConvDmaArgs& a, hipStream_t s) {
   } else if (resnet) {
     if (small) STEM_LAUNCH(7, 1, kStemNTSmall) else STEM_LAUNCH(7, 1, kStemNT)
   } else if (mt == 1) {
-    if (small) STEM_LAUNCH(3, 1, kStemNTSmall) else STEM_LAUNCH(3, 1, kStemNT3)
+    if (small) STEM_LAUNCH(3, 1, kStemNTSmall) else STEM_LAUNCH(3, 1, kStemNT)
   } else {
-    if (small) STEM_LAUNCH(3, 2, kStemNTSmall) else STEM_LAUNCH(3, 2, kStemNT3)
+    if (small) STEM_LAUNCH(3, 2, kStemNTSmall) else STEM_LAUNCH(3, 2, kStemNT)
   }
 #undef STEM_LAUNCH
   RTENHIP_LAUNCH_CHECK();
