@@ -178,6 +178,15 @@ rtenhip_status launch_dw_project(const float* x, const float* wd, const float* b
                                  float hi_d, const float* wp, const float* bp, const float* res, int act_p,
                                  float lo_p, float hi_p, float* y, int N, int C, int H, int W, int M,
                                  hipStream_t s);
+// MobileNetV2's stem (3 -> 32 channels, 3x3 / 2, pads 1 at the top and left,
+// 224 input columns) feeding the depthwise -> projection pair above, as one
+// kernel (dw_project.hip): the stem's output never reaches HBM.
+bool stem_dw_project_eligible(int C0, int H0, int W0, int kh, int kw, int sh, int sw, int pt, int pl, int O, int OH,
+                              int OW);
+rtenhip_status launch_stem_dw_project(const float* img, const float* ws, const float* bs, int act_s, float lo_s,
+                                      float hi_s, int H0, const float* wd, const float* bd, int act_d, float lo_d,
+                                      float hi_d, const float* wp, const float* bp, const float* res, int act_p,
+                                      float lo_p, float hi_p, float* y, int N, int H, int M, hipStream_t s);
 // A bottleneck's conv3 (1x1, K 64 -> 256, + bias, residual, Relu) and the next
 // block's conv1 (1x1, K 256 -> 64, + bias, act) as one launch
 // (conv_pair.hip); weights packed [K / 2][2][M] by pack_pair_weights.

@@ -860,6 +860,44 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
       p.dwpw_fused[op] = dn.inputs[0];
       drop.push_back(n.fd_op);
     }
+    // Stem -> depthwise -> projection (dw_project.hip stem_dw_project_kernel):
+    // MobileNetV2's 3 -> 32 channel 3x3 / 2 stem, read only by a fused
+    // depthwise -> projection pair; the stem op leaves the plan, the
+    // projection op runs all three and reads the stem's input.
+    const bool stem_dwpw_off = (getenv("RTENHIP_STEM_DWPW") && getenv("RTENHIP_STEM_DWPW")[0] == '0') || dwpw_off;  // A/B runs (read per plan)
+    for (auto& kv : p.dwpw_fused) {
+      if (stem_dwpw_off) break;
+      const int v = kv.second;  // the depthwise conv's input
+      int cop = -1;
+      for (int o : p.ops)
+        if (nodes[o].op_type == "Conv" && nodes[o].outputs.size() == 1 && nodes[o].outputs[0] == v) cop = o;
+      if (cop < 0 || std::find(drop.begin(), drop.end(), cop) != drop.end() || p.expand_fused.count(cop) ||
+          p.dwpw_fused.count(cop))
+        continue;
+      const Node& cn = nodes[cop];
+      if (outset0.count(v) || uses_of_value(p.ops, v) != 1 || cn.fused_residual >= 0 || cn.fused_bn >= 0 ||
+          !(cn.fused_act == RTENHIP_ACT_NONE || cn.fused_act == RTENHIP_ACT_RELU || cn.fused_act == RTENHIP_ACT_CLIP) ||
+          cn.inputs.size() < 2 || nodes[cn.inputs[1]].kind != NodeKind::Constant ||
+          (cn.inputs.size() > 2 && cn.inputs[2] >= 0 && nodes[cn.inputs[2]].kind != NodeKind::Constant))
+        continue;
+      const Shape* xs = shape_of(cn.inputs[0]);
+      const Shape* ws = shape_of(cn.inputs[1]);
+      const Shape* vs = shape_of(v);
+      if (!xs || !ws || !vs || xs->size() != 4 || vs->size() != 4 || p.dtypes[cn.inputs[0]] == RTENHIP_DTYPE_INT32)
+        continue;
+      ConvAttrs ca = conv_attrs(cn, false);
+      rtenhip_tensor xt = desc(nullptr, *xs), wt = desc(nullptr, *ws);
+      ConvPlan g;
+      if (plan_conv(&xt, &wt, ca.mode, ca.pads.data(), ca.strides.data(), ca.dil.data(), ca.groups, g) != RTENHIP_OK ||
+          g.groups != 1 || g.dh != 1 || g.dw != 1 || (*vs)[0] != g.N || (*vs)[1] != g.O || (*vs)[2] != g.oh ||
+          (*vs)[3] != g.ow ||
+          !stem_dw_project_eligible((int)g.C, (int)g.H, (int)g.W, (int)g.kh, (int)g.kw, (int)g.sh, (int)g.sw,
+                                    (int)g.pads[0], (int)g.pads[1], (int)g.O, (int)g.oh, (int)g.ow))
+        continue;
+      p.stem_dwpw[kv.first] = cop;
+      kv.second = cn.inputs[0];
+      drop.push_back(cop);
+    }
     // Stem -> MaxPool (conv_stem.hip POOL): ResNet's 7x7 / 2 stem with its
     // fused Relu, read only by a 3x3 / 2 / pads 1 MaxPool, at batches whose
     // bands are 4 output rows; the conv op leaves the plan, the pool op runs
@@ -1768,6 +1806,17 @@ rtenhip_status Graph::exec_dw_project(Plan& p, int op_id) {
   const float* bd = dn.inputs.size() > 2 && dn.inputs[2] >= 0 ? ptr_of(p, dn.inputs[2]) : nullptr;
   const float* bp = n.inputs.size() > 2 && n.inputs[2] >= 0 ? ptr_of(p, n.inputs[2]) : nullptr;
   const float* res = n.fused_residual >= 0 ? ptr_of(p, n.fused_residual) : nullptr;
+  auto sd = p.stem_dwpw.find(op_id);
+  if (sd != p.stem_dwpw.end()) {
+    // xv is the stem's input [N, 3, H0, 224]; the projection's output rows
+    // are the stem's (and the depthwise's) output rows.
+    const Node& sn = nodes[sd->second];
+    const float* bs = sn.inputs.size() > 2 && sn.inputs[2] >= 0 ? ptr_of(p, sn.inputs[2]) : nullptr;
+    return launch_stem_dw_project(ptr_of(p, xv), ptr_of(p, sn.inputs[1]), bs, sn.fused_act, sn.act_lo, sn.act_hi,
+                                  (int)xs[2], ptr_of(p, dn.inputs[1]), bd, dn.fused_act, dn.act_lo, dn.act_hi,
+                                  ptr_of(p, n.inputs[1]), bp, res, n.fused_act, n.act_lo, n.act_hi,
+                                  ptr_of(p, n.outputs[0]), (int)xs[0], (int)ys[2], (int)ys[1], ctx->stream);
+  }
   return launch_dw_project(ptr_of(p, xv), ptr_of(p, dn.inputs[1]), bd, dn.fused_act, dn.act_lo, dn.act_hi,
                            ptr_of(p, n.inputs[1]), bp, res, n.fused_act, n.act_lo, n.act_hi, ptr_of(p, n.outputs[0]),
                            (int)xs[0], (int)xs[1], (int)xs[2], (int)xs[3], (int)ys[1], ctx->stream);
@@ -3113,6 +3162,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           key = n.op_type + "(fused)";
         if (plan->expand_fused.count(plan->ops[i])) key = "Conv(expand+dw)";
         if (plan->dwpw_fused.count(plan->ops[i])) key = "Conv(dw+project)";
+        if (plan->stem_dwpw.count(plan->ops[i])) key = "Conv(stem+dw+project)";
         if (plan->conv_pair.count(plan->ops[i])) key = "Conv(conv3+conv1)";
         if (plan->pair_hold.count(plan->ops[i])) key = "Conv(in_pair)";
         if (plan->stem_pool.count(plan->ops[i])) key = "Conv(stem+pool)";

@@ -215,6 +215,10 @@ struct Plan {
   // Projection convs running their depthwise conv too (see Node::fd_op): op id
   // -> the depthwise conv's input value, which the projection op then reads.
   std::map<int, int> dwpw_fused;
+  // ... of which those running the stem conv producing the depthwise input
+  // too (dw_project.hip stem_dw_project_kernel): projection op -> the stem
+  // conv op (out of the plan; dwpw_fused then names the stem's input).
+  std::map<int, int> stem_dwpw;
   // MaxPool ops running their stem conv too (conv_stem.hip POOL): pool op ->
   // the conv op (out of the plan; its output never exists); the weights
   // packed for the stem kernel and the halo rows between bands.

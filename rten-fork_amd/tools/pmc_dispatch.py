@@ -43,7 +43,7 @@ def main():
         w = d.get("SQ_WAIT_ANY", 0) / wc if wc else 0
         wi = d.get("SQ_WAIT_INST_ANY", 0) / wc if wc else 0
         ac = d.get("SQ_ACTIVE_INST_ANY", 0) / wc if wc else 0
-        name = d["name"].replace("void ", "").split("(")[0][:70]
+        name = d["name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:70]
         print(f"{k:3d} {d.get('dur', 0):8.1f} {mf:6.3f} {w:6.2f} {wi:6.2f} {ac:6.2f}  {name}")
 
 

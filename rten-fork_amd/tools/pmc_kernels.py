@@ -16,7 +16,7 @@ def main():
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            k = re.sub(r"^void ", "", r["Kernel_Name"])
+            k = re.sub(r"^void ", "", r["Kernel_Name"]).replace("(anonymous namespace)::", "")
             k = re.sub(r"\(.*$", "", k)
             if filt and filt not in k:
                 continue

@@ -461,3 +461,82 @@ def test_dw_project_fused_bitexact(rh, monkeypatch, case, policy):
     torch.cuda.synchronize()
     fused = "Conv(dw+project)" in g.timing_report()
     assert fused == (policy == "on" and C == 32), g.timing_report()
+
+
+# MobileNetV2's stem (3 -> 32, 3x3 / 2, pads 1) feeding the depthwise ->
+# projection pair, all three in one kernel (dw_project.hip
+# stem_dw_project_kernel): (N, H0, stem act, dw act, M, projection tail,
+# stem bias, input scale)
+STEM_DW_PROJECT = [
+    (2, 224, "clip", "clip", 16, "none", True, 1.0),     # MobileNetV2 features.0 + features.1
+    (1, 29, "relu", "relu", 24, "relu", False, 1.0),     # 15 rows: a partial band, zero bottom pad row; M = 24
+    (3, 30, "none", "clip", 32, "add_clip", True, 1.0),  # 15 rows, residual, two channel tiles
+    (1, 2, "clip", "none", 16, "add", True, 1.0),        # one output row
+    (2, 56, "clip", "clip", 16, "none", True, 1e30),     # huge sums, clamped; 2 bands
+]
+
+
+@pytest.mark.parametrize("case", STEM_DW_PROJECT, ids=lambda c: f"n{c[0]}h{c[1]}-{c[2]}-{c[3]}-m{c[4]}-{c[5]}")
+@pytest.mark.parametrize("policy", ["on", "off"])
+def test_stem_dw_project_fused_bitexact(rh, monkeypatch, case, policy):
+    """The stem -> depthwise -> projection kernel gives the three operators'
+    bits (the stem's im2col GEMM chain + bias + act, conv_2d_depthwise_block,
+    conv_2d_pointwise), eager and replayed; RTENHIP_STEM_DWPW=0 runs the stem
+    apart (and the depthwise -> projection pair fused)."""
+    import torch
+    import graph_runner
+    from rten_hip.graph import ModelSpec
+
+    N, H0, act_s, act_d, M, tail, biases, scale = case
+    if policy == "off":
+        monkeypatch.setenv("RTENHIP_STEM_DWPW", "0")
+    else:
+        monkeypatch.delenv("RTENHIP_STEM_DWPW", raising=False)
+    monkeypatch.delenv("RTENHIP_DW_PROJECT", raising=False)
+    rng = np.random.default_rng(H0 * 7 + M)
+    m = ModelSpec("stemdwpw")
+    x = m.value("x")
+    m.inputs = ["x"]
+    lo, hi = m.const("lo", np.array(0.0, np.float32)), m.const("hi", np.array(6.0, np.float32))
+
+    def act(v, a):
+        if a == "clip":
+            return m.op("Clip", [v, lo, hi])
+        if a == "relu":
+            return m.op("Relu", [v])
+        return v
+
+    ins = {"x": (rng.uniform(-1, 1, (N, 3, H0, 224)) * scale).astype(np.float32)}
+    ws = m.const("ws", rng.uniform(-0.5, 0.5, (32, 3, 3, 3)).astype(np.float32))
+    args = [x, ws] + ([m.const("bs", rng.uniform(-0.2, 0.2, (32,)).astype(np.float32))] if biases else [])
+    sv = act(m.op("Conv", args, {"pads": [1, 1, 1, 1], "strides": [2, 2]}, name="stem"), act_s)
+    wd = m.const("wd", rng.uniform(-0.5, 0.5, (32, 1, 3, 3)).astype(np.float32))
+    args = [sv, wd] + ([m.const("bd", rng.uniform(-0.2, 0.2, (32,)).astype(np.float32))] if biases else [])
+    dv = act(m.op("Conv", args, {"pads": [1, 1, 1, 1], "strides": [1, 1], "groups": 32}, name="dw"), act_d)
+    wp = m.const("wp", rng.uniform(-0.5, 0.5, (M, 32, 1, 1)).astype(np.float32))
+    args = [dv, wp] + ([m.const("bp", rng.uniform(-0.2, 0.2, (M,)).astype(np.float32))] if biases else [])
+    y = m.op("Conv", args, {"pads": [0, 0, 0, 0], "strides": [1, 1]}, name="project")
+    OH = (H0 - 1) // 2 + 1
+    if tail.startswith("add"):
+        r = m.value("r")
+        m.inputs.append("r")
+        ins["r"] = rng.uniform(-1, 1, (N, M, OH, 112)).astype(np.float32)
+        y = m.op("Add", [y, r])
+    y = act(y, tail.split("_")[-1] if "_" in tail or tail in ("relu", "clip") else "none")
+    m.outputs = [y]
+    exp = graph_runner.run(m, ins)[y]
+    g = m.to_graph()
+    dev = {g.input_ids[i]: torch.from_numpy(ins[n]).cuda() for i, n in enumerate(m.inputs)}
+    out = None
+    for _ in range(3):  # eager, capture, replay
+        out = g.run(dev, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        o = out[0].cpu().numpy()
+        bad = np.count_nonzero(o.view(np.uint32) != exp.view(np.uint32))
+        assert bad == 0, f"{bad} of {o.size} differ, max |d| {np.nanmax(np.abs(o - exp))}"
+    g.set_timing(True)
+    g.run(dev, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    rep = g.timing_report()
+    assert ("Conv(stem+dw+project)" in rep) == (policy == "on"), rep
+    assert "Conv(dw+project)" in rep or policy == "on", rep
