@@ -352,12 +352,11 @@ constexpr int kSdBuf = 4 * kSdCS;
 constexpr int kSdNT = 64 * kSdRows;
 constexpr int kSdIn4 = 3 * kSdIn * 56;   // float4s of a band's input rows
 constexpr int kSdPre = (kSdIn4 + kSdNT - 1) / kSdNT;
-constexpr int kSdItems = kSdStem * 28;   // stem items per k-step (448: waves 0..6)
 constexpr size_t kSdLdsBytes =
-    (size_t)(3 * kSdIn * kSdLrow + 2 * kSdBuf + 32 * 9 + 32 + 8 * 2 * 64 + 32 * 27 + 32 + 32) * sizeof(float);
-static_assert(kSdLdsBytes <= 160 * 1024, "one workgroup per CU");
+    (size_t)(3 * kSdIn * kSdLrow + 2 * kSdBuf + 32 * 9 + 32 + 8 * 2 * 64 + 32 * 36 + 32 + 32) * sizeof(float);
+static_assert(kSdLdsBytes <= 160 * 1024, "one workgroup per CU");  // (163,504 bytes)
 static_assert(kSdRows * 4 * 112 <= kSdBuf, "epilogue exchange fits one stem tile");
-static_assert(kSdItems % 64 == 0, "stem items fill whole waves");
+static_assert(kSdStem * 28 == 2 * 16 * kSdRows, "two 16-quad MFMA stem items per wave");
 
 // The stem's activation (as the conv epilogues: Relu = max(x, 0), Clip = clamp).
 __device__ __forceinline__ float sd_act(float x, int act, float lo, float hi) {
@@ -375,8 +374,8 @@ __global__ __launch_bounds__(kSdNT) void stem_dw_project_kernel(StemDwProjDesc s
   float* wdl = sout + 2 * kSdBuf;                   // [C][9]
   float* bdl = wdl + C * 9;                         // [C]
   float* wpl = bdl + C;                             // [G][MT][64]
-  float* wsl = wpl + G * 2 * 64;                    // stem weights [g][c][ky][4 ch][kx]
-  float* bsl = wsl + C * 27;                        // stem bias [C]
+  float* wsl = wpl + G * 2 * 64;                    // stem weights [4g + ch][c][12]
+  float* bsl = wsl + C * 36;                        // stem bias [C]
   float* bpl = bsl + C;                             // projection bias [32]
   const DwProjDesc& d = s.p;
   const int t = threadIdx.x;
@@ -418,67 +417,76 @@ __global__ __launch_bounds__(kSdNT) void stem_dw_project_kernel(StemDwProjDesc s
     }
   };
   // Stem outputs of channels 4g .. 4g + 3 on the band's rows oy0 - 1 ..
-  // oy0 + 14 (rows outside the image are not computed: the depthwise skips
-  // them) -> dst [4][kSdStem][kSdRS] at column offset 4.
+  // oy0 + 14 -> dst [4][kSdCS] (rows of kSdRS, column offset 4), on MFMA:
+  // v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4 x 1; a chain of them is
+  // bitwise the k-ordered fmaf chain, tools/probes/mfma4x4_probe.hip) with the
+  // block's rows the 4 channels and its columns the 4 pixels of a quad: lane l
+  // supplies A = W[4g + l % 4][k] and B = x(k) at pixel 4 q + l % 4 of quad
+  // (row, q) = block l / 4 of the item, and holds D for channel r in register
+  // r.  The band's 16 x 28 quads are 28 items of 16 quads, two per wave.  Rows
+  // outside the image are computed from the zero rows (the depthwise skips
+  // them).
   auto stem_step = [&](int g, int oy0, float* dst) __attribute__((always_inline)) {
-    if (tv >= kSdItems) return;  // (whole waves)
     if (s.dbg & 1) return;
-    const int sr = tv / 28, q = tv - sr * 28;
-    const int srow = oy0 - 1 + sr;
-    if (srow < 0 || srow >= H) return;
-    f32x2 acc[4][2];
+    (void)oy0;
+    const int l = tv & 63, w = tv >> 6;
+    const int ch = l & 3;
+    int px[2], rowoff[2], sro[2];
 #pragma unroll
-    for (int ch = 0; ch < 4; ch++) acc[ch][0] = acc[ch][1] = (f32x2){0.f, 0.f};
-    // (not unrolled: the scheduler would hoist all 27 windows' LDS reads)
-#pragma unroll 1
-    for (int c = 0; c < 3; c++)
-#pragma unroll 1
-      for (int ky = 0; ky < 3; ky++) {
-        const float* row = xin + (c * kSdIn + 2 * sr + ky) * kSdLrow;
-        const float* wq = wsl + ((g * 3 + c) * 3 + ky) * 12;  // [ch][kx], broadcast reads
-        const float4 ev = *reinterpret_cast<const float4*>(row + kSdEven + 4 * q);
-        const float4 od = *reinterpret_cast<const float4*>(row + 4 + 4 * q);
-        const float op = row[3 + 4 * q];
-        const f32x2 x0a = {op, od.x}, x0b = {od.y, od.z};
-        const f32x2 x1a = {ev.x, ev.y}, x1b = {ev.z, ev.w};
-        const f32x2 x2a = {od.x, od.y}, x2b = {od.z, od.w};
-#pragma unroll
-        for (int ch = 0; ch < 4; ch++) {
-          const float* wr = wq + ch * 3;
-          const f32x2 w0 = {wr[0], wr[0]}, w1 = {wr[1], wr[1]}, w2 = {wr[2], wr[2]};
-          acc[ch][0] = __builtin_elementwise_fma(w0, x0a, acc[ch][0]);
-          acc[ch][1] = __builtin_elementwise_fma(w0, x0b, acc[ch][1]);
-          acc[ch][0] = __builtin_elementwise_fma(w1, x1a, acc[ch][0]);
-          acc[ch][1] = __builtin_elementwise_fma(w1, x1b, acc[ch][1]);
-          acc[ch][0] = __builtin_elementwise_fma(w2, x2a, acc[ch][0]);
-          acc[ch][1] = __builtin_elementwise_fma(w2, x2b, acc[ch][1]);
-        }
-      }
-#pragma unroll
-    for (int ch = 0; ch < 4; ch++) {
-      float4 r = make_float4(acc[ch][0].x, acc[ch][0].y, acc[ch][1].x, acc[ch][1].y);
-      if (s.bs) {
-        const float b = bsl[4 * g + ch];
-        r.x = __fadd_rn(r.x, b);
-        r.y = __fadd_rn(r.y, b);
-        r.z = __fadd_rn(r.z, b);
-        r.w = __fadd_rn(r.w, b);
-      }
-      r.x = sd_act(r.x, s.act_s, s.lo_s, s.hi_s);
-      r.y = sd_act(r.y, s.act_s, s.lo_s, s.hi_s);
-      r.z = sd_act(r.z, s.act_s, s.lo_s, s.hi_s);
-      r.w = sd_act(r.w, s.act_s, s.lo_s, s.hi_s);
-      *reinterpret_cast<float4*>(dst + ch * kSdCS + sr * kSdRS + 4 + 4 * q) = r;
+    for (int it = 0; it < 2; it++) {
+      const int f = 16 * (w + kSdRows * it) + (l >> 2);
+      const int sr = f / 28, q = f - 28 * sr;
+      px[it] = 4 * q + (l & 3);
+      rowoff[it] = 2 * sr * kSdLrow;
+      sro[it] = sr * kSdRS;
     }
+    dp_f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // (c not unrolled: the scheduler would hoist every window's LDS reads)
+#pragma unroll 1
+    for (int c = 0; c < 3; c++) {
+      float wk[12];  // W[4g + ch][9c .. 9c + 8] (+3 pad)
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const float4 q4 = *reinterpret_cast<const float4*>(wsl + ((g * 4 + ch) * 3 + c) * 12 + 4 * i);
+        wk[4 * i] = q4.x;
+        wk[4 * i + 1] = q4.y;
+        wk[4 * i + 2] = q4.z;
+        wk[4 * i + 3] = q4.w;
+      }
+#pragma unroll
+      for (int ky = 0; ky < 3; ky++) {
+        float x[2][3];
+#pragma unroll
+        for (int it = 0; it < 2; it++) {
+          const float* row = xin + (c * kSdIn + ky) * kSdLrow + rowoff[it];
+          x[it][0] = row[3 + px[it]];          // input column 2 px - 1: odd[px - 1]
+          x[it][1] = row[kSdEven + px[it]];    // 2 px: even[px]
+          x[it][2] = row[4 + px[it]];          // 2 px + 1: odd[px]
+        }
+#pragma unroll
+        for (int kx = 0; kx < 3; kx++)
+#pragma unroll
+          for (int it = 0; it < 2; it++)
+            acc[it] = __builtin_amdgcn_mfma_f32_4x4x1f32(wk[3 * ky + kx], x[it][kx], acc[it], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < 2; it++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        float v = acc[it][r];
+        if (s.bs) v = __fadd_rn(v, bsl[4 * g + r]);
+        dst[r * kSdCS + sro[it] + 4 + px[it]] = sd_act(v, s.act_s, s.lo_s, s.hi_s);
+      }
   };
 
   for (int i = t; i < 3 * kSdIn; i += kSdNT) *reinterpret_cast<float4*>(xin + i * kSdLrow) = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int i = t; i < C * 9; i += kSdNT) wdl[i] = d.wd[i];
   // (in LDS: the stem weights are re-read every band, after the band's
   // stores, so the compiler will not make them scalar loads)
-  for (int i = t; i < C * 27; i += kSdNT) {
-    const int kx = i % 3, ch = (i / 3) % 4, ky = (i / 12) % 3, c = (i / 36) % 3, g = i / 108;
-    wsl[i] = s.ws[(4 * g + ch) * 27 + c * 9 + ky * 3 + kx];
+  for (int i = t; i < C * 36; i += kSdNT) {  // [4g + ch][c][12]: k = 9c + i12 for i12 < 9
+    const int i12 = i % 12, c = (i / 12) % 3, oc = i / 36;
+    wsl[i] = i12 < 9 ? s.ws[oc * 27 + c * 9 + i12] : 0.f;
   }
   for (int i = t; i < C; i += kSdNT) bdl[i] = d.bd ? d.bd[i] : 0.f;
   // (biases in LDS too: a global load inside the band loop waits, vmcnt being

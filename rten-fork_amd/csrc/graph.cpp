@@ -1306,7 +1306,9 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
   std::vector<Block> blocks;
   std::map<int, int> block_of;  // value -> block index (arena values only)
   std::vector<std::pair<size_t, size_t>> free_list;  // (off, size)
-  size_t top = 0;
+  // (RTENHIP_ARENA_PAD_MB: layout experiments only -- every arena offset shifted by that much)
+  static const size_t arena_pad = getenv("RTENHIP_ARENA_PAD_MB") ? (size_t)atol(getenv("RTENHIP_ARENA_PAD_MB")) << 20 : 0;
+  size_t top = arena_pad;
   auto alloc = [&](size_t bytes) -> size_t {
     bytes = (bytes + 255) & ~size_t(255);
     if (bytes == 0) bytes = 256;
