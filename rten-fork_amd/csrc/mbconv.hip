@@ -84,8 +84,16 @@ __device__ __forceinline__ int ed_col(int ix, int W) {
 // w.  A channel with a non-finite tap weight takes the select path instead.
 // CLIPS: both activations are Clip (MobileNetV2's ReLU6), compiled in rather
 // than selected per value at run time.
-template <int CIN, int S, int CP, int PLANE, int NQ, bool CLIPS>
+// MX (CP == 4): the expand on v_mfma_f32_4x4x1_16b_f32 (a chain of them is
+// bitwise the k-ordered fmaf chain, tools/probes/mfma4x4_probe.hip): the
+// block's 4 rows are the pass's 4 channels (lane l supplies the weight of
+// channel c0 + l % 4), its columns 4 lanes' pixels, one MFMA chain per pixel
+// of the lane's float4; lane l then holds channel c0 + r of its 4 pixels in
+// register r of the 4 chains.  Every lane of the wave takes part (lanes
+// outside the band run on zeros and store nothing).
+template <int CIN, int S, int CP, int PLANE, int NQ, bool CLIPS, bool MX = false>
 __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
+  static_assert(!MX || CP == 4, "MFMA expand passes are 4 channels");
   extern __shared__ float4 ed_lds4[];
   float* lds = reinterpret_cast<float*>(ed_lds4);
   const int plane = PLANE > 0 ? PLANE : ed_plane(d.rows_in, d.W);
@@ -118,6 +126,10 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   const bool e_on = er < d.rows_in && iy >= 0 && iy < d.H;
   const int64_t HW = (int64_t)d.H * d.W;
   float4 xr[CIN];
+  if (MX && !e_on) {
+#pragma unroll
+    for (int k = 0; k < CIN; k++) xr[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (e_on) {
     const float* xp = d.x + ((int64_t)n * CIN) * HW + (int64_t)iy * d.W + ec;
 #pragma unroll
@@ -163,7 +175,45 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
   auto pass = [&](const int c0, auto Bc) __attribute__((always_inline)) {
     constexpr int B = decltype(Bc)::value;
     float* ebuf = lds + B * CP * plane;
-    if (e_on) {
+    if constexpr (MX) {
+      typedef float ed_f32x4 __attribute__((ext_vector_type(4)));
+      const int lane = t & 63;
+      const float* __restrict__ wl = w_e + (min(c0 + (lane & 3), c_end - 1) - c_begin) * CIN;
+      ed_f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int k = 0; k < CIN; k++) {
+        const float w = wl[k];
+        acc[0] = __builtin_amdgcn_mfma_f32_4x4x1f32(w, xr[k].x, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_4x4x1f32(w, xr[k].y, acc[1], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_f32_4x4x1f32(w, xr[k].z, acc[2], 0, 0, 0);
+        acc[3] = __builtin_amdgcn_mfma_f32_4x4x1f32(w, xr[k].w, acc[3], 0, 0, 0);
+      }
+      if (e_on) {
+#pragma unroll
+        for (int j = 0; j < CP; j++) {
+          const int cl = min(c0 + j, c_end - 1) - c_begin;
+          float4 v = make_float4(acc[0][j], acc[1][j], acc[2][j], acc[3][j]);
+          if (d.be) {
+            const float b = b_e[cl];
+            v.x = __fadd_rn(v.x, b);
+            v.y = __fadd_rn(v.y, b);
+            v.z = __fadd_rn(v.z, b);
+            v.w = __fadd_rn(v.w, b);
+          }
+          v.x = act(v.x, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+          v.y = act(v.y, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+          v.z = act(v.z, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+          v.w = act(v.w, e_act_relu, e_act_clip, d.lo_e, d.hi_e);
+          float* erow = ebuf + j * plane + kEdZs + er * d.W;
+          if constexpr (S == 2) {
+            *(float2*)(erow + (ec >> 1)) = make_float2(v.x, v.z);
+            *(float2*)(erow + (d.W >> 1) + (ec >> 1)) = make_float2(v.y, v.w);
+          } else {
+            *(float4*)(erow + ec) = v;
+          }
+        }
+      }
+    } else if (e_on) {
 #pragma unroll
       for (int j = 0; j < CP; j++) {
         const int cl = min(c0 + j, c_end - 1) - c_begin;  // a pass past c_end recomputes the last channel (unused)
@@ -208,20 +258,27 @@ __global__ __launch_bounds__(256) void expand_dw_kernel(ExpandDwDesc d) {
     // Depthwise products and sums as packed pairs (v_pk_mul / v_pk_add: each
     // component rounds exactly as the scalar op): two outputs of a channel
     // when a thread has several (stride 1), else the pass's two channels.
-    if constexpr (NQ == 1 && CP == 2) {
+    if constexpr (NQ == 1 && (CP == 2 || CP == 4)) {
       const int cl0 = c0 - c_begin;
-      if (c0 + 1 < c_end && fin[cl0] && fin[cl0 + 1]) {
-        if (tmask[0] >> 9) {
-          vm_f32x2 acc = {b_d[cl0], b_d[cl0 + 1]};
+      bool all = c0 + CP - 1 < c_end;
 #pragma unroll
-          for (int i = 0; i < 9; i++) {
-            const vm_f32x2 v = {ebuf[taddr[0][i]], ebuf[plane + taddr[0][i]]};
-            const vm_f32x2 w = {w_d[cl0 * 9 + i], w_d[cl0 * 9 + 9 + i]};
-            acc = acc + v * w;
+      for (int j = 0; j < CP; j++) all = all && fin[min(cl0 + j, c_end - 1 - c_begin)];
+      if (all) {
+        if (tmask[0] >> 9) {
+#pragma unroll
+          for (int jp = 0; jp < CP; jp += 2) {
+            const int cl = cl0 + jp;
+            vm_f32x2 acc = {b_d[cl], b_d[cl + 1]};
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+              const vm_f32x2 v = {ebuf[jp * plane + taddr[0][i]], ebuf[(jp + 1) * plane + taddr[0][i]]};
+              const vm_f32x2 w = {w_d[cl * 9 + i], w_d[cl * 9 + 9 + i]};
+              acc = acc + v * w;
+            }
+            float* y0 = d.y + ((int64_t)n * d.hidden + c0 + jp) * d.OH * d.OW + (int64_t)oy0 * d.OW + t;
+            y0[0] = act(acc.x, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
+            y0[(int64_t)d.OH * d.OW] = act(acc.y, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
           }
-          float* y0 = d.y + ((int64_t)n * d.hidden + c0) * d.OH * d.OW + (int64_t)oy0 * d.OW + t;
-          y0[0] = act(acc.x, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
-          y0[(int64_t)d.OH * d.OW] = act(acc.y, d_act_relu, d_act_clip, d.lo_d, d.hi_d);
         }
         return;
       }
@@ -474,6 +531,13 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
   constexpr int CP = 2;
   const int plane = ed_plane(d.rows_in, W);
   const size_t lds = (2 * CP * (size_t)plane + (size_t)d.cpb * (cin + 9 + 3)) * sizeof(float);
+  // The expand on MFMA (MX, 4-channel passes) for the compile-time planes with
+  // one depthwise output per thread and C_in >= 24 (MobileNetV2 b128 replayed:
+  // features.4 103.6 vs 107.8 us, features.7 45.2 vs 46.3; features.2, C_in =
+  // 16, 170.4 vs 165.9 keeps the VALU expand); RTENHIP_EDW_MX=0: the VALU
+  // expand everywhere (A/B runs).
+  static const bool mx_off = getenv("RTENHIP_EDW_MX") && getenv("RTENHIP_EDW_MX")[0] == '0';
+  const size_t lds_mx = (2 * 4 * (size_t)plane + (size_t)d.cpb * (cin + 9 + 3)) * sizeof(float);
   if (lds > 64 * 1024 || N > 65535 || chunks > 65535 || (int64_t)d.TR * OW > 256 * kEdMaxQ)
     return fail(RTENHIP_UNSUPPORTED_VALUE, "expand+depthwise tile too large");
   dim3 grid((unsigned)bands, (unsigned)N, (unsigned)chunks);
@@ -482,6 +546,14 @@ rtenhip_status launch_expand_dw(const float* x, const float* we, const float* be
   const bool clips = act_e == RTENHIP_ACT_CLIP && act_d == RTENHIP_ACT_CLIP;
 #define ED_PL(C, SS, PL, Q)                                                                       \
   if (cin == C && S == SS && plane == PL && nq <= Q) {                                           \
+    if (!mx_off && Q == 1 && C >= 24 && lds_mx <= 64 * 1024) {                                   \
+      if (clips)                                                                                 \
+        hipLaunchKernelGGL((expand_dw_kernel<C, SS, 4, PL, Q, true, true>), grid, dim3(256), lds_mx, s, d); \
+      else                                                                                       \
+        hipLaunchKernelGGL((expand_dw_kernel<C, SS, 4, PL, Q, false, true>), grid, dim3(256), lds_mx, s, d); \
+      RTENHIP_LAUNCH_CHECK();                                                                    \
+      return RTENHIP_OK;                                                                         \
+    }                                                                                            \
     if (clips)                                                                                   \
       hipLaunchKernelGGL((expand_dw_kernel<C, SS, CP, PL, Q, true>), grid, dim3(256), lds, s, d);  \
     else                                                                                         \
