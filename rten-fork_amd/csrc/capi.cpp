@@ -208,6 +208,53 @@ static void set_conv_bvec(const ConvDmaArgs& a, int cfg, const DmaTile& tile, Dm
   }
 }
 
+// The latency GEMM's K-block workspace and 16-byte B copies for variant v
+// (gemm_lat2 / gemm_lat3, variants 7x / 8x: pointwise stride-1 convs whose
+// 4-column groups stay inside one image).
+static rtenhip_status lat_conv_split_bvec(const ConvDmaArgs& a, int v, DmaDesc& d) {
+  const DmaSplit sp = lat_split_plan(d.M, d.N, d.K, v);
+  if (sp.split_tiles > 0) {
+    if (!a.split || !a.ws || !a.counters || sp.ws_floats > a.ws_cap || sp.counters > a.cnt_cap)
+      return fail(RTENHIP_INVALID_VALUE, "latency conv: K-block workspace missing or too small");
+    d.ws = a.ws;
+    d.counters = a.counters;
+  }
+  static const bool no_bvec = getenv("RTENHIP_LAT_NO_BVEC") != nullptr;  // A/B experiments
+  const bool pw = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.Hp == a.oh && a.Wp == a.ow;
+  if (!no_bvec && v >= 70 && v < 90 && pw && d.P % 4 == 0 && d.x_img % 4 == 0 && d.kstride % 4 == 0 &&
+      (uintptr_t)d.x % 16 == 0)
+    d.bvec = 1;
+  return RTENHIP_OK;
+}
+
+bool conv_lat_pair_ok(const ConvDmaArgs& a0, const ConvDmaArgs& a1) {
+  const auto one = [](const ConvDmaArgs& a) {
+    return a.groups == 1 && a.kh == 1 && a.kw == 1 && is_lat_cfg(a.cfg) && a.packed_w &&
+           conv_dma_eligible(a.N, a.C, a.Hp, a.Wp, a.O, 1, a.C);
+  };
+  // a0 with 16-byte B copies (lat_conv_split_bvec's conditions)
+  static const bool no_bvec = getenv("RTENHIP_LAT_NO_BVEC") != nullptr;
+  const int64_t P = a0.oh * a0.ow;
+  const bool bvec0 = !no_bvec && a0.sh == 1 && a0.sw == 1 && a0.Hp == a0.oh && a0.Wp == a0.ow && P % 4 == 0 &&
+                     (a0.C * a0.Hp * a0.Wp) % 4 == 0 && (a0.Hp * a0.Wp) % 4 == 0 && (uintptr_t)a0.xin % 16 == 0;
+  return bvec0 && one(a0) && one(a1) && lat_pair_variants_ok(a0.cfg - kLatCfgBase, a1.cfg - kLatCfgBase);
+}
+
+// Two ungrouped 1x1 latency convs in one launch (gemm_lat2_pair_kernel): a0
+// must take 16-byte B copies (a pointwise stride-1 conv).
+rtenhip_status conv_lat_pair(Ctx* c, const ConvDmaArgs& a0, const ConvDmaArgs& a1) {
+  if (!conv_lat_pair_ok(a0, a1)) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency conv pair: unsupported");
+  const DmaTile tile{16, 256, 1};
+  DmaDesc d0, d1;
+  fill_conv_desc(a0, 0, true, tile, nullptr, d0);
+  fill_conv_desc(a1, 0, true, tile, nullptr, d1);
+  rtenhip_status st = lat_conv_split_bvec(a0, a0.cfg - kLatCfgBase, d0);
+  if (!st) st = lat_conv_split_bvec(a1, a1.cfg - kLatCfgBase, d1);
+  if (st) return st;
+  if (!d0.bvec) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency conv pair: first conv without 16-byte B copies");
+  return launch_gemm_lat_pair(d0, a0.cfg - kLatCfgBase, d1, a1.cfg - kLatCfgBase, c->stream);
+}
+
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
   const int64_t opg = a.O / a.groups, ipg = a.C / a.groups;
   const int64_t K = ipg * a.kh * a.kw, P = a.oh * a.ow;
@@ -226,24 +273,8 @@ rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a) {
     DmaDesc d;
     fill_conv_desc(a, g, lat, tile, tab, d);
     if (lat) {
-      const DmaSplit sp = lat_split_plan(d.M, d.N, d.K, cfg - kLatCfgBase);
-      if (sp.split_tiles > 0) {
-        if (!a.split || !a.ws || !a.counters || sp.ws_floats > a.ws_cap || sp.counters > a.cnt_cap)
-          return fail(RTENHIP_INVALID_VALUE, "latency conv: K-block workspace missing or too small");
-        d.ws = a.ws;
-        d.counters = a.counters;
-      }
-      {
-        // gemm_lat2 / gemm_lat3 (variants 7x / 8x): 16-byte B copies for pointwise stride-1
-        // convs whose 4-column groups stay inside one image.
-        static const bool no_bvec = getenv("RTENHIP_LAT_NO_BVEC") != nullptr;  // A/B experiments
-        const int v = cfg - kLatCfgBase;
-        const bool pw = a.kh == 1 && a.kw == 1 && a.sh == 1 && a.sw == 1 && a.Hp == a.oh && a.Wp == a.ow;
-        if (!no_bvec && v >= 70 && v < 90 && pw && d.P % 4 == 0 && d.x_img % 4 == 0 && d.kstride % 4 == 0 &&
-            (uintptr_t)d.x % 16 == 0)
-          d.bvec = 1;
-      }
-      rtenhip_status st = launch_gemm_lat(d, cfg - kLatCfgBase, c->stream);
+      rtenhip_status st = lat_conv_split_bvec(a, cfg - kLatCfgBase, d);
+      if (!st) st = launch_gemm_lat(d, cfg - kLatCfgBase, c->stream);
       if (st) return st;
       continue;
     }

@@ -98,6 +98,10 @@ struct ConvDmaArgs {
   int64_t H, W, pad_t, pad_l;
 };
 rtenhip_status conv_dma(Ctx* c, const ConvDmaArgs& a);
+// Two ungrouped 1x1 latency-GEMM convs (cfg = kLatCfgBase + 71 / 72 / 74, packed
+// weights and K-block workspaces bound) in one launch; a0 pointwise stride 1.
+bool conv_lat_pair_ok(const ConvDmaArgs& a0, const ConvDmaArgs& a1);
+rtenhip_status conv_lat_pair(Ctx* c, const ConvDmaArgs& a0, const ConvDmaArgs& a1);
 // conv3 + downsample as one dual DMA GEMM (see capi.cpp); cfg = a3.cfg, both
 // packed for it.
 bool conv_dual_ok(const ConvDmaArgs& a3, const ConvDmaArgs& ad, int cfg);

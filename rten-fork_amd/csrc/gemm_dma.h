@@ -135,5 +135,9 @@ int64_t lat_packed_floats(int M, int K);
 rtenhip_status launch_pack_lat(const float* a, int64_t lda, int M, int K, float* out, hipStream_t s);
 DmaSplit lat_split_plan(int M, int N, int K, int variant);
 rtenhip_status launch_gemm_lat(const DmaDesc& d, int variant, hipStream_t s);
+// Two latency GEMMs in one launch (LDS-staged variants 71 / 72 / 74; d0 with
+// 16-byte B copies): the bits of the two launches apart.
+bool lat_pair_variants_ok(int v0, int v1);
+rtenhip_status launch_gemm_lat_pair(const DmaDesc& d0, int v0, const DmaDesc& d1, int v1, hipStream_t s);
 
 }  // namespace rtenhip

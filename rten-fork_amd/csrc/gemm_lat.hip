@@ -71,17 +71,16 @@ __global__ __launch_bounds__(256) void gemm_lat_kernel(DmaDesc d, int wg_m, int 
 // 16 bytes per lane -- 4 adjacent columns of one k row, inside one image --
 // into a [CW][256 k][16 columns] tile, and the chains read it one float per
 // MFMA step: a quarter of the gather's load instructions.
+// The body of gemm_lat2_kernel for work id o (kb, tm, tn), its A panels and
+// B tiles staged at lds_a / lds_b (the caller's LDS: the pair kernel below
+// runs two problems' bodies over one allocation).
 template <int RW, int CW, bool BVEC>
-__global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
+__device__ __forceinline__ void lat2_body(const DmaDesc& d, int o, int wg_m, int wg_n, int nkb, int subs,
+                                          float4 (*lds_a)[LGROUPS][64], float4 (*lds_b)[LGROUPS][64]) {
   static_assert(RW * CW == 4, "one chain per wave");
-  __shared__ float4 lds_a[RW][LGROUPS][64];
-  __shared__ float4 lds_b[CW][LGROUPS][64];
   float* ldsk = reinterpret_cast<float*>(&lds_b[0][0][0]);  // BVEC: [CW][LKC][16]
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
-  const int o = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
   const int tn = o % wg_n;
   const int t2 = o / wg_n;
   const int tm = t2 % wg_m;
@@ -232,6 +231,41 @@ __global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int
   }
   const int wt = sub0 * (wg_n * CW) + (n0 >> 4);
   lat_fold_finish<1>(d, sub0, kb, nkb, wt, col, e, acc, stp);
+}
+
+// XCD-contiguous work id of this workgroup (dispatch is round-robin over the
+// 8 XCDs): XCD x owns a contiguous range of work ids.
+__device__ __forceinline__ int lat_xcd_work_id() {
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int qq = G >> 3, rr = G & 7, xcd = bid & 7;
+  return (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+}
+
+template <int RW, int CW, bool BVEC>
+__global__ __launch_bounds__(256) void gemm_lat2_kernel(DmaDesc d, int wg_m, int wg_n, int nkb, int subs) {
+  __shared__ float4 lds_a[RW][LGROUPS][64];
+  __shared__ float4 lds_b[CW][LGROUPS][64];
+  lat2_body<RW, CW, BVEC>(d, lat_xcd_work_id(), wg_m, wg_n, nkb, subs, lds_a, lds_b);
+}
+
+// Two independent latency GEMMs in one launch (a bottleneck's conv1 and its
+// downsample, which read the same input at batch 1): work ids below g0.wgs
+// run problem 0's body, the rest problem 1's, each with its own descriptor,
+// K-block workspace and fold -- the bits of the two launches apart, without
+// the second launch's ramp and drain on the critical path.
+struct LatPairGrid {
+  int wg_m, wg_n, nkb, subs, wgs;
+};
+template <int RW0, int CW0, bool BV0, int RW1, int CW1, bool BV1>
+__global__ __launch_bounds__(256) void gemm_lat2_pair_kernel(DmaDesc d0, LatPairGrid g0, DmaDesc d1, LatPairGrid g1) {
+  constexpr int RA = RW0 > RW1 ? RW0 : RW1, RB = CW0 > CW1 ? CW0 : CW1;
+  __shared__ float4 lds_a[RA][LGROUPS][64];
+  __shared__ float4 lds_b[RB][LGROUPS][64];
+  const int o = lat_xcd_work_id();
+  if (o < g0.wgs)
+    lat2_body<RW0, CW0, BV0>(d0, o, g0.wg_m, g0.wg_n, g0.nkb, g0.subs, lds_a, lds_b);
+  else
+    lat2_body<RW1, CW1, BV1>(d1, o - g0.wgs, g1.wg_m, g1.wg_n, g1.nkb, g1.subs, lds_a, lds_b);
 }
 
 // Pipelined LDS-staged variant (8x): the workgroup layout of gemm_lat2_kernel
@@ -766,6 +800,52 @@ template <int WMW, int MI>
 static void lat_launch(const DmaDesc& d, const LatGrid& g, hipStream_t s) {
   hipLaunchKernelGGL((gemm_lat_kernel<WMW, MI>), dim3((unsigned)g.wgs), dim3(256), 0, s, d, g.wg_m, g.wg_n, g.nkb,
                      g.subs);
+}
+
+// Pair launches (gemm_lat2_pair_kernel): LDS-staged variants 71 / 72 / 74 on
+// both sides, the instantiated combinations below (problem 0 with 16-byte B
+// copies -- a bottleneck's conv1 -- problem 1 either way).
+static int lat2_rw(int v) { return v == 71 ? 1 : v == 72 ? 2 : v == 74 ? 4 : 0; }
+bool lat_pair_variants_ok(int v0, int v1) {
+  const int r0 = lat2_rw(v0), r1 = lat2_rw(v1);
+  return r0 && r1 && (r0 == r1 || (r0 == 2 && r1 == 4) || (r0 == 4 && r1 == 2));
+}
+
+rtenhip_status launch_gemm_lat_pair(const DmaDesc& d0, int v0, const DmaDesc& d1, int v1, hipStream_t s) {
+  if (!lat_pair_variants_ok(v0, v1) || !d0.bvec) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM pair: variants");
+  const DmaDesc* ds[2] = {&d0, &d1};
+  const int vs[2] = {v0, v1};
+  LatPairGrid pg[2];
+  for (int i = 0; i < 2; i++) {
+    const DmaDesc& d = *ds[i];
+    if (d.M <= 0 || d.N <= 0 || d.K <= 0) return fail(RTENHIP_INVALID_VALUE, "empty latency GEMM");
+    if (d.cin) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM: beta * C not supported");
+    if (d.kstride <= 0 && !d.k3x3) return fail(RTENHIP_UNSUPPORTED_VALUE, "LDS latency GEMM: 1x1 or 3x3 windows only");
+    const LatGrid g = lat_grid(d.M, d.N, d.K, vs[i]);
+    if (g.nkb > 1 && (!d.ws || !d.counters)) return fail(RTENHIP_INVALID_VALUE, "latency GEMM needs its K-block workspace");
+    pg[i] = {g.wg_m, g.wg_n, g.nkb, g.subs, (int)g.wgs};
+  }
+  const int64_t wgs = (int64_t)pg[0].wgs + pg[1].wgs;
+  if (wgs > 0x7fffffff) return fail(RTENHIP_UNSUPPORTED_VALUE, "latency GEMM pair grid too large");
+  const dim3 grid((unsigned)wgs), blk(256);
+  DmaDesc a = d0, b = d1;
+  a.stamps = b.stamps = nullptr;
+  const int r0 = lat2_rw(v0), r1 = lat2_rw(v1);
+#define LATP(R0, R1)                                                                                         \
+  if (r0 == R0 && r1 == R1) {                                                                                \
+    if (b.bvec)                                                                                              \
+      hipLaunchKernelGGL((gemm_lat2_pair_kernel<R0, 4 / R0, true, R1, 4 / R1, true>), grid, blk, 0, s, a, pg[0], b, pg[1]);   \
+    else                                                                                                     \
+      hipLaunchKernelGGL((gemm_lat2_pair_kernel<R0, 4 / R0, true, R1, 4 / R1, false>), grid, blk, 0, s, a, pg[0], b, pg[1]);  \
+  }
+  LATP(1, 1)
+  LATP(2, 2)
+  LATP(4, 4)
+  LATP(2, 4)
+  LATP(4, 2)
+#undef LATP
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
 }
 
 rtenhip_status launch_gemm_lat(const DmaDesc& d0, int v, hipStream_t s) {

@@ -105,6 +105,11 @@ Plan::~Plan() {
     if (kv.second.pk3) (void)hipFree(kv.second.pk3);
     if (kv.second.pkd) (void)hipFree(kv.second.pkd);
   }
+  for (auto& kv : lat_pair_exec)
+    for (int i = 0; i < 2; i++) {
+      if (kv.second.ws[i]) (void)hipFree(kv.second.ws[i]);
+      if (kv.second.cnt[i]) (void)hipFree(kv.second.cnt[i]);
+    }
   for (auto& kv : conv_unfused)
     if (kv.second.first) (void)hipFree(kv.second.first);
 }
@@ -1298,6 +1303,50 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     }
   }
 
+  // Batch-1 conv1 + downsample pairs (Plan::lat_pair): a 1x1 downsample read
+  // only as a conv3's fused residual, and the block's conv1 (1x1, stride 1,
+  // unpadded) reading the same input earlier in the plan.  The downsample op
+  // moves right after conv1 (both read only the block input).
+  {
+    const bool lat_pair_off = getenv("RTENHIP_LAT_PAIR") && getenv("RTENHIP_LAT_PAIR")[0] == '0';  // A/B runs (read per plan)
+    // (a downsample of a conv_dual pair too: the pair is decided first, at the
+    // downsample op, and conv3 then tunes no dual GEMM for it)
+    std::set<int> busy;
+    for (auto& kv : p.conv_dual) busy.insert(kv.first);
+    for (auto& kv : p.conv_pair) busy.insert(kv.first), busy.insert(kv.second);
+    auto plain = [&](int op) {
+      if (nodes[op].op_type != "Conv" || !p.convs.count(op) || busy.count(op) || p.conv_unfused.count(op) ||
+          p.expand_fused.count(op) || p.dwpw_fused.count(op) || p.lat_pair.count(op) || p.lat_pair_of.count(op))
+        return false;
+      const ConvPlan& g = p.convs.at(op).g;
+      return g.N <= 4 && g.kh == 1 && g.kw == 1 && g.groups == 1 && !g.pads[0] && !g.pads[1] && !g.pads[2] &&
+             !g.pads[3] && !p.padded.count(nodes[op].inputs[0]);
+    };
+    for (int i = 0; !lat_pair_off && i < (int)p.ops.size(); i++) {
+      const int d_op = p.ops[i];
+      if (!plain(d_op)) continue;
+      const Node& dn = nodes[d_op];
+      const int v = dn.outputs[0];
+      bool residual_only = uses[v] == 1 && !outset.count(v);
+      bool read_as_residual = false;
+      for (int o : p.ops) read_as_residual |= nodes[o].fused_residual == v && nodes[o].op_type == "Conv";
+      if (!residual_only || !read_as_residual) continue;
+      int j = i - 1;
+      for (; j >= 0; j--) {
+        const int c_op = p.ops[j];
+        if (!plain(c_op) || nodes[c_op].inputs[0] != dn.inputs[0]) continue;
+        const ConvPlan& gc = p.convs.at(c_op).g;
+        if (gc.sh == 1 && gc.sw == 1 && gc.N == p.convs.at(d_op).g.N) break;
+      }
+      if (j < 0) continue;
+      const int c_op = p.ops[j];
+      p.lat_pair[c_op] = d_op;
+      p.lat_pair_of[d_op] = c_op;
+      p.ops.erase(p.ops.begin() + i);
+      p.ops.insert(p.ops.begin() + j + 1, d_op);
+    }
+  }
+
   // Storage blocks with best-fit reuse; aliases share their base's block.
   struct Block {
     size_t off, size;
@@ -1535,6 +1584,21 @@ rtenhip_status Graph::exec_op(Plan& p, int op_id) {
   if (t == "Conv" && p.conv_pair.count(op_id)) return exec_conv_pair(p, op_id);
   if (t == "Conv" && p.pair_hold.count(op_id)) return RTENHIP_OK;  // run by its conv3's op
   if (t == "Conv" && p.dual_skip.count(op_id)) return RTENHIP_OK;  // computed by its conv3 (dual GEMM)
+  if (t == "Conv" && p.lat_pair.count(op_id)) {
+    auto le = p.lat_pair_exec.find(op_id);
+    if (le != p.lat_pair_exec.end() && le->second.on) return exec_lat_pair(p, op_id);
+  }
+  if (t == "Conv" && p.lat_pair_of.count(op_id)) {
+    const int c_op = p.lat_pair_of.at(op_id);
+    auto le = p.lat_pair_exec.find(c_op);
+    if (le != p.lat_pair_exec.end() && le->second.on) return RTENHIP_OK;  // computed by its conv1's pair launch
+    auto cit = p.convs.find(op_id);
+    if (cit != p.convs.end() && ctx->use_dma) {
+      rtenhip_status st = exec_conv_dma(p, op_id, cit->second);
+      if (st) return st;
+      return tune_lat_pair(p, c_op);
+    }
+  }
   if (t == "MatMul" && p.mm_group_skip.count(op_id)) return RTENHIP_OK;  // computed by its group's leader
   if (t == "Conv" && p.conv_dual.count(op_id)) {
     bool handled = false;
@@ -2764,6 +2828,150 @@ rtenhip_status Graph::exec_conv_dma(Plan& p, int op_id, ConvExec& ce) {
   return launch();
 }
 
+// conv1 + downsample of a Plan::lat_pair as one gemm_lat2_pair_kernel launch
+// (both convs' weights packed for the latency GEMM on the first run).
+rtenhip_status Graph::exec_lat_pair(Plan& p, int c_op) {
+  const int d_op = p.lat_pair.at(c_op);
+  Plan::LatPairExec& le = p.lat_pair_exec.at(c_op);
+  const ConvExec& cc = p.convs.at(c_op);
+  const ConvExec& cd = p.convs.at(d_op);
+  ConvDmaArgs a0{}, a1{};
+  conv_io_args(p, c_op, a0);
+  conv_io_args(p, d_op, a1);
+  a0.packed_w = cc.packed;
+  a1.packed_w = cd.packed;
+  a0.cfg = kLatCfgBase + le.v0;
+  a1.cfg = kLatCfgBase + le.v1;
+  ConvDmaArgs* as[2] = {&a0, &a1};
+  for (int i = 0; i < 2; i++) {
+    as[i]->split = true;
+    as[i]->ws = le.ws[i];
+    as[i]->ws_cap = le.ws_floats[i];
+    as[i]->counters = le.cnt[i];
+    as[i]->cnt_cap = le.n_cnt[i];
+  }
+  return conv_lat_pair(ctx, a0, a1);
+}
+
+// First run, at the downsample op (both convs tuned and run): when both took
+// latency GEMMs, time the pair launch's variants against the two launches
+// as tuned (median of 7, 8 back-to-back launches per sample); keep the best
+// pair only if it is at least 3% faster.  Outputs are rewritten with the same
+// bits by every candidate.
+rtenhip_status Graph::tune_lat_pair(Plan& p, int c_op) {
+  Plan::LatPairExec& le = p.lat_pair_exec[c_op];
+  if (le.decided) return RTENHIP_OK;
+  hipStream_t s = ctx->stream;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cs);
+  if (!autotune || cs != hipStreamCaptureStatusNone) return RTENHIP_OK;
+  le.decided = true;
+  const int d_op = p.lat_pair.at(c_op);
+  ConvExec& cc = p.convs.at(c_op);
+  ConvExec& cd = p.convs.at(d_op);
+  if (!is_lat_cfg(cc.cfg) || !is_lat_cfg(cd.cfg)) return RTENHIP_OK;
+  static const int kPairs[][2] = {{72, 72}, {74, 74}, {71, 71}, {72, 74}, {74, 72}};
+  // RTENHIP_LAT_PAIR="v0/v1": that pair on every planned pair, untimed (tests).
+  int force0 = 0, force1 = 0;
+  if (const char* e = getenv("RTENHIP_LAT_PAIR")) {
+    if (sscanf(e, "%d/%d", &force0, &force1) != 2 || !lat_pair_variants_ok(force0, force1)) force0 = force1 = 0;
+  }
+  // Workspaces sized for every candidate (counters start at zero and every
+  // launch leaves them so).
+  const ConvExec* ce[2] = {&cc, &cd};
+  for (int i = 0; i < 2; i++) {
+    const ConvPlan& g = ce[i]->g;
+    int64_t wsf = 0, nc = 0;
+    for (auto& pv : kPairs) {
+      const DmaSplit sp = lat_split_plan((int)g.O, (int)(g.N * g.oh * g.ow), (int)(g.C * g.kh * g.kw), pv[i]);
+      wsf = std::max<int64_t>(wsf, sp.ws_floats);
+      nc = std::max<int64_t>(nc, sp.counters);
+    }
+    le.ws_floats[i] = std::max<int64_t>(wsf, 4);
+    le.n_cnt[i] = std::max<int64_t>(nc, 1);
+    RTENHIP_HIP_CHECK(hipMalloc(&le.ws[i], (size_t)le.ws_floats[i] * 4));
+    RTENHIP_HIP_CHECK(hipMalloc(&le.cnt[i], (size_t)le.n_cnt[i] * 4));
+    RTENHIP_HIP_CHECK(hipMemsetAsync(le.cnt[i], 0, (size_t)le.n_cnt[i] * 4, s));
+  }
+  hipEvent_t e0, e1;
+  RTENHIP_HIP_CHECK(hipEventCreate(&e0));
+  RTENHIP_HIP_CHECK(hipEventCreate(&e1));
+  auto time_ms = [&](const std::function<rtenhip_status()>& f, float& out) -> rtenhip_status {
+    rtenhip_status st = f();  // warm-up
+    if (st) return st;
+    std::vector<float> ts;
+    for (int r = 0; r < 7; r++) {
+      RTENHIP_HIP_CHECK(hipEventRecord(e0, s));
+      for (int k = 0; k < 8; k++)
+        if ((st = f())) return st;
+      RTENHIP_HIP_CHECK(hipEventRecord(e1, s));
+      RTENHIP_HIP_CHECK(hipEventSynchronize(e1));
+      float t = 0;
+      RTENHIP_HIP_CHECK(hipEventElapsedTime(&t, e0, e1));
+      ts.push_back(t / 8);
+    }
+    std::sort(ts.begin(), ts.end());
+    out = ts[ts.size() / 2];
+    return RTENHIP_OK;
+  };
+  rtenhip_status st = RTENHIP_OK;
+  // (A forced latency / VALU variant keeps every conv on it, as for the dual GEMM.)
+  if (!force0 && (lat_mode > 0 || pw_valu_mode > 0)) return RTENHIP_OK;
+  // (A forced dual GEMM, RTENHIP_DUAL=1, keeps its downsample.)
+  const bool dual_forced = getenv("RTENHIP_DUAL") && atoi(getenv("RTENHIP_DUAL")) > 0;
+  bool in_dual = false;
+  for (auto& kv : p.conv_dual) in_dual |= kv.second == d_op;
+  if (!force0 && dual_forced && in_dual) return RTENHIP_OK;
+  if (force0) {
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    le.on = true;
+    le.v0 = force0;
+    le.v1 = force1;
+    return exec_lat_pair(p, c_op);  // (fails loudly if the pair cannot take these convs)
+  }
+  float apart = 0;
+  st = time_ms([&]() -> rtenhip_status {
+    rtenhip_status q = exec_conv_dma(p, c_op, cc);
+    return q ? q : exec_conv_dma(p, d_op, cd);
+  }, apart);
+  float best = 1e30f;
+  int bv0 = 0, bv1 = 0;
+  for (auto& pv : kPairs) {
+    if (st) break;
+    le.v0 = pv[0];
+    le.v1 = pv[1];
+    ConvDmaArgs a0{}, a1{};
+    conv_io_args(p, c_op, a0);
+    conv_io_args(p, d_op, a1);
+    a0.packed_w = cc.packed;
+    a1.packed_w = cd.packed;
+    a0.cfg = kLatCfgBase + pv[0];
+    a1.cfg = kLatCfgBase + pv[1];
+    if (!conv_lat_pair_ok(a0, a1)) continue;
+    float ms = 0;
+    st = time_ms([&]() { return exec_lat_pair(p, c_op); }, ms);
+    if (!st && ms < best) {
+      best = ms;
+      bv0 = pv[0];
+      bv1 = pv[1];
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (st) return st;
+  if (getenv("RTENHIP_LAT_PAIR_DEBUG"))
+    fprintf(stderr, "lat pair %s + %s: apart %.4f ms, pair %d/%d %.4f ms\n", nodes[c_op].name.c_str(),
+            nodes[d_op].name.c_str(), apart, bv0, bv1, best);
+  if (bv0 && best < 0.97f * apart) {
+    le.on = true;
+    le.v0 = bv0;
+    le.v1 = bv1;
+  }
+  RTENHIP_HIP_CHECK(hipStreamSynchronize(s));
+  return RTENHIP_OK;
+}
+
 rtenhip_status Graph::exec_conv_dual(Plan& p, int op_id, bool& handled) {
   handled = false;
   if (!ctx->use_dma) return RTENHIP_OK;
@@ -2779,6 +2987,14 @@ rtenhip_status Graph::exec_conv_dual(Plan& p, int op_id, bool& handled) {
     a3.cfg = ad.cfg = de.cfg;
     a3.persist_k = de.persist;
   };
+  {
+    // A downsample computed by its conv1's latency pair launch: conv3 alone.
+    auto lo = p.lat_pair_of.find(ds);
+    if (lo != p.lat_pair_of.end()) {
+      auto le = p.lat_pair_exec.find(lo->second);
+      if (le != p.lat_pair_exec.end() && le->second.on) return RTENHIP_OK;
+    }
+  }
   auto on = p.dual_on.find(op_id);
   if (on != p.dual_on.end()) {
     handled = true;
@@ -3171,6 +3387,14 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         if (plan->dual_skip.count(plan->ops[i])) key = "Conv(in_dual)";
         if (plan->mm_group_skip.count(plan->ops[i])) key = "MatMul(in_group)";
         if (plan->dual_on.count(plan->ops[i])) key = "Conv(dual)";
+        {
+          auto le = plan->lat_pair_exec.find(plan->ops[i]);
+          if (le != plan->lat_pair_exec.end() && le->second.on) key = "Conv(lat_pair)";
+          auto lo = plan->lat_pair_of.find(plan->ops[i]);
+          if (lo != plan->lat_pair_of.end() && plan->lat_pair_exec.count(lo->second) &&
+              plan->lat_pair_exec.at(lo->second).on)
+            key = "Conv(in_lat_pair)";
+        }
         tot[key].first += ms;
         tot[key].second++;
         total += ms;
@@ -3216,6 +3440,20 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
           os << "  (in its conv3's dual GEMM)";
         } else if (plan->pair_hold.count(plan->ops[i])) {
           os << "  (in its conv3's pair kernel)";
+        } else if (plan->lat_pair_of.count(plan->ops[i]) && plan->lat_pair_exec.count(plan->lat_pair_of.at(plan->ops[i])) &&
+                   plan->lat_pair_exec.at(plan->lat_pair_of.at(plan->ops[i])).on) {
+          os << "  (in its conv1's latency pair launch)";
+        } else if (plan->lat_pair_exec.count(plan->ops[i]) && plan->lat_pair_exec.at(plan->ops[i]).on &&
+                   ce != plan->convs.end()) {
+          // One launch computes both convs: time and FLOPs booked here together.
+          const Plan::LatPairExec& le = plan->lat_pair_exec.at(plan->ops[i]);
+          const ConvPlan& c1 = ce->second.g;
+          const ConvPlan& cd = plan->convs.at(plan->lat_pair.at(plan->ops[i])).g;
+          const double fl = 2.0 * ((double)c1.N * c1.oh * c1.ow * c1.O * (double)c1.C + (double)cd.N * cd.oh * cd.ow * cd.O * (double)cd.C);
+          snprintf(buf, sizeof buf, "  lat pair conv1 M=%lld N=%lld K=%lld + downsample M=%lld N=%lld K=%lld cfg=lat%d/lat%d %.1f TF/s",
+                   (long long)c1.O, (long long)(c1.N * c1.oh * c1.ow), (long long)c1.C, (long long)cd.O,
+                   (long long)(cd.N * cd.oh * cd.ow), (long long)cd.C, le.v0, le.v1, ms > 0 ? fl / (ms * 1e9) : 0.0);
+          os << buf;
         } else if (plan->stem_pool.count(plan->ops[i])) {
           // The stem conv's FLOPs (the pool is the kernel's epilogue); the
           // conv's output is never written (stem_out = its floats).

@@ -251,6 +251,21 @@ struct Plan {
   };
   std::map<int, DualExec> dual_on;   // conv3 op -> its dual launch
   std::set<int> dual_skip;           // downsample ops computed by their conv3
+  // Batch-1 bottleneck conv1 + downsample (both 1x1, reading the block
+  // input) in one latency-GEMM launch (gemm_lat2_pair_kernel): conv1 op ->
+  // downsample op, which the plan moves right after conv1.  On the first run,
+  // once both are tuned onto latency GEMMs, the pair variants are timed
+  // against the two launches; when one wins (on) conv1's op runs both.
+  std::map<int, int> lat_pair;
+  std::map<int, int> lat_pair_of;  // downsample op -> its conv1 op
+  struct LatPairExec {
+    bool decided = false, on = false;
+    int v0 = 0, v1 = 0;              // the pair's variants (conv1, downsample)
+    float* ws[2] = {nullptr, nullptr};
+    int* cnt[2] = {nullptr, nullptr};
+    int64_t ws_floats[2] = {0, 0}, n_cnt[2] = {0, 0};
+  };
+  std::map<int, LatPairExec> lat_pair_exec;  // conv1 op ->
   float* mm_pack = nullptr;           // packed-A buffer shared by the plan's MatMuls
   int64_t mm_pack_floats = 0;
   // What mm_pack holds during a run: the A value it was packed from (value
@@ -408,6 +423,10 @@ struct Graph {
   // conv3 of a Plan::conv_dual pair: the dual launch, or (first run) the
   // choice between it and the unfused pair.
   rtenhip_status exec_conv_dual(Plan& p, int op_id, bool& handled);
+  // conv1 + downsample of a Plan::lat_pair: the pair launch, and (first run,
+  // at the downsample op) the choice between it and the two launches.
+  rtenhip_status exec_lat_pair(Plan& p, int c_op);
+  rtenhip_status tune_lat_pair(Plan& p, int c_op);
   void conv_io_args(Plan& p, int op_id, ConvDmaArgs& a);
   rtenhip_status exec_expand_dw(Plan& p, int op_id);
   rtenhip_status exec_dw_project(Plan& p, int op_id);

@@ -181,3 +181,37 @@ def test_resnet50_batch1_forced_variant(rh, monkeypatch, mode):
         out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
         torch.cuda.synchronize()
         assert _bits_equal(out[0].cpu().numpy(), exp)
+
+
+@pytest.mark.parametrize("pair", ["72/72", "74/74", "71/71", "72/74", "74/72", "0"])
+def test_resnet50_batch1_conv1_downsample_pair(rh, monkeypatch, pair):
+    """ResNet-50 at batch 1 with each bottleneck's conv1 and downsample in one
+    gemm_lat2_pair_kernel launch (RTENHIP_LAT_PAIR="v0/v1" forces that
+    variant pair; "0" plans none): the oracle's bits, eager and replayed, and
+    the downsample ops run inside their conv1's launch."""
+    import torch
+    import graph_runner
+    from rten_hip import models
+
+    monkeypatch.setenv("RTENHIP_LAT_PAIR", pair)
+    spec = models.resnet50()
+    x = np.random.default_rng(13).random((1, 3, 224, 224), dtype=np.float32)
+    exp = graph_runner.run(spec, {spec.inputs[0]: x})[spec.outputs[0]]
+    g = spec.to_graph()
+    xd = torch.from_numpy(x).cuda()
+    out = None
+    for _ in range(3):
+        out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+        torch.cuda.synchronize()
+        assert _bits_equal(out[0].cpu().numpy(), exp)
+    g.set_timing(True)
+    g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+    torch.cuda.synchronize()
+    rep = g.timing_report()
+    if pair == "0":
+        assert "lat_pair" not in rep, rep
+    else:
+        v0, v1 = pair.split("/")
+        # (a downsample the tuner put on a non-latency kernel is not paired)
+        assert rep.count(f"cfg=lat{v0}/lat{v1}") >= 1, rep
+        assert rep.count("(in its conv1's latency pair launch)") == rep.count(f"cfg=lat{v0}/lat{v1}"), rep
