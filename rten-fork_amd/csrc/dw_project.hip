@@ -480,32 +480,53 @@ __global__ __launch_bounds__(kSdNT) void stem_dw_project_kernel(StemDwProjDesc s
       }
   };
 
-  for (int i = t; i < 3 * kSdIn; i += kSdNT) *reinterpret_cast<float4*>(xin + i * kSdLrow) = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int i = t; i < C * 9; i += kSdNT) wdl[i] = d.wd[i];
-  // (in LDS: the stem weights are re-read every band, after the band's
-  // stores, so the compiler will not make them scalar loads)
-  for (int i = t; i < C * 36; i += kSdNT) {  // [4g + ch][c][12]: k = 9c + i12 for i12 < 9
-    const int i12 = i % 12, c = (i / 12) % 3, oc = i / 36;
-    wsl[i] = i12 < 9 ? s.ws[oc * 27 + c * 9 + i12] : 0.f;
-  }
-  for (int i = t; i < C; i += kSdNT) bdl[i] = d.bd ? d.bd[i] : 0.f;
-  // (biases in LDS too: a global load inside the band loop waits, vmcnt being
-  // in order, for every store and prefetch load issued before it)
-  for (int i = t; i < C; i += kSdNT) bsl[i] = s.bs ? s.bs[i] : 0.f;
-  for (int i = t; i < 32; i += kSdNT) bpl[i] = d.bp && i < d.M ? d.bp[i] : 0.f;
-  // The projection's A operands W[16 mt + j][4 g + kq] (0 past M) as
-  // wpl[g][mt][lane], read per k-step (registers are the limit here).
-  for (int i = t; i < G * MT * 64; i += kSdNT) {
-    const int l = i & 63, mt = (i >> 6) % MT, g = (i >> 6) / MT;
-    const int m = 16 * mt + (l & 15);
-    wpl[i] = m < d.M ? d.wp[(int64_t)m * C + 4 * g + (l >> 4)] : 0.f;
+  // Prologue: the stem / depthwise / projection weights and biases into LDS
+  // (the stem's and the biases there because a global load inside the band
+  // loop would wait -- vmcnt is in order -- for every store and prefetch load
+  // issued before it; the projection's A operands W[16 mt + j][4 g + kq], 0
+  // past M, as wpl[g][mt][lane]) and the first band's input rows: every load
+  // issued before any LDS store, one memory round trip for all of them.
+  constexpr int NWS = C * 36, NWD = C * 9, NWP = G * MT * 64;
+  constexpr int NST = NWS + NWD + 3 * C + NWP;
+  constexpr int NSU = (NST + kSdNT - 1) / kSdNT;
+  float sv[NSU];
+  float* sdst[NSU];
+#pragma unroll
+  for (int u = 0; u < NSU; u++) {
+    int e = t + kSdNT * u;
+    sv[u] = 0.f;
+    sdst[u] = nullptr;
+    if (e < NWS) {  // [4g + ch][c][12]: k = 9c + i12 for i12 < 9
+      const int i12 = e % 12, c = (e / 12) % 3, oc = e / 36;
+      if (i12 < 9) sv[u] = s.ws[oc * 27 + c * 9 + i12];
+      sdst[u] = wsl + e;
+    } else if ((e -= NWS) < NWD) {
+      sv[u] = d.wd[e];
+      sdst[u] = wdl + e;
+    } else if ((e -= NWD) < C) {
+      if (d.bd) sv[u] = d.bd[e];
+      sdst[u] = bdl + e;
+    } else if ((e -= C) < C) {
+      if (s.bs) sv[u] = s.bs[e];
+      sdst[u] = bsl + e;
+    } else if ((e -= C) < C) {
+      if (d.bp && e < d.M) sv[u] = d.bp[e];
+      sdst[u] = bpl + e;
+    } else if ((e -= C) < NWP) {
+      const int l = e & 63, mt = (e >> 6) % MT, g = (e >> 6) / MT;
+      const int m = 16 * mt + (l & 15);
+      if (m < d.M) sv[u] = d.wp[(int64_t)m * C + 4 * g + (l >> 4)];
+      sdst[u] = wpl + e;
+    }
   }
   dp_f32x4 pre[kSdPre];
   int band = blockIdx.x;
-  if (band < s.nbands) {
-    load_in(band, pre);
-    store_in(pre);
-  }
+  if (band < s.nbands) load_in(band, pre);
+#pragma unroll
+  for (int u = 0; u < NSU; u++)
+    if (sdst[u]) *sdst[u] = sv[u];
+  for (int i = t; i < 3 * kSdIn; i += kSdNT) *reinterpret_cast<float4*>(xin + i * kSdLrow) = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (band < s.nbands) store_in(pre);
   __syncthreads();
   const int64_t plane = (int64_t)H * W;
   for (; band < s.nbands; band += gridDim.x) {
