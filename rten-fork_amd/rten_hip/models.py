@@ -197,6 +197,17 @@ def _dw_project_fused(c: int, h: int, w: int, m: int, stride: int) -> bool:
     return c == 32 and w == 112 and m <= 32 and stride == 1
 
 
+def _stem_dw_project_fused(stem, xshape, consts) -> bool:
+    """Whether csrc/dw_project.hip also runs the stem conv feeding a fused
+    depthwise -> projection pair (stem_dw_project_eligible: 3 -> 32 channels,
+    3x3 / 2, pads 1 at the top and left, 224 input columns)."""
+    o, ci, kh, kw = consts[stem.inputs[1]]
+    p, s = stem.attrs["pads"], stem.attrs["strides"]
+    return (ci == 3 and (kh, kw) == (3, 3) and list(s) == [2, 2] and p[0] == 1 and p[1] == 1 and o == 32 and
+            stem.attrs.get("groups", 1) == 1 and xshape[1] == 3 and xshape[3] == 224 and
+            (xshape[3] + p[1] + p[3] - 3) // 2 + 1 == 112)
+
+
 def expand_dw_pairs(spec: ModelSpec, batch: int = 1, hw: int = 224) -> int:
     """Expand -> depthwise pairs of ``spec`` the executor fuses by default."""
     return int(conv_io_bytes(spec, batch, hw, count_pairs=True))
@@ -218,7 +229,8 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224, count_pairs: bool 
     a residual Add fused into the conv's epilogue reads its other operand once;
     Relu / Clip ride in the epilogue (no traffic); an expand -> depthwise pair
     run as one kernel (mbconv.hip) neither writes nor reads the expand output,
-    nor a depthwise -> projection pair (dw_project.hip) the depthwise output.
+    nor a depthwise -> projection pair (dw_project.hip) the depthwise output,
+    nor MobileNetV2's stem fused into that pair the stem output.
     The HBM-roofline figure for bandwidth-bound models (MobileNetV2,
     SURVEY.md §8d)."""
     shapes = {spec.inputs[0]: (batch, 3, hw, hw)}
@@ -264,6 +276,9 @@ def conv_io_bytes(spec: ModelSpec, batch: int, hw: int = 224, count_pairs: bool 
                 if dx[2:] == (H, W) and _dw_project_fused(C, H, W, o, d.attrs["strides"][0]):
                     rd = 0  # the depthwise output never reaches HBM
                     total -= 4.0 * N * C * H * W  # nor is written by the depthwise conv
+                    st = source_conv(d.inputs[0], (3, 3))
+                    if st is not None and _stem_dw_project_fused(st, shapes[st.inputs[0]], consts):
+                        total -= 2 * 4.0 * float(np.prod(dx))  # the stem output: neither written nor read
             total += 4.0 * (rd + wr + o * ci * kh * kw + o)
             shapes[n.outputs[0]] = (N, o, oh, ow)
         elif n.op_type == "Add":

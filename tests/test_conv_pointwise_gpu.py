@@ -121,7 +121,8 @@ def test_mobilenet_v2_pointwise_valu(rh, monkeypatch, mode):
         m = re.search(r"Conv\(expand\+dw\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
         fused = int(m.group(1)) if m else 0
         # and the depthwise -> projection pair (dw_project.hip), features.1
-        m2 = re.search(r"Conv\(dw\+project\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
+        # (with the stem, features.0, in the same kernel by default)
+        m2 = re.search(r"Conv\((?:stem\+)?dw\+project\)\s+[\d.]+ ms \([^)]*\)\s+x(\d+)", rep)
         assert m2 and int(m2.group(1)) == 1, rep
         fused += 1
         # bench.py's HBM bytes (models.conv_io_bytes) assume the executor's pairs
@@ -372,12 +373,15 @@ def test_stem_mfma_bitexact(rh, monkeypatch, case):
 @pytest.mark.parametrize("model", ["resnet50", "mobilenet_v2"])
 def test_model_stem_mfma(rh, monkeypatch, model):
     """ResNet-50 / MobileNetV2 (batch 2) with the stem forced onto the MFMA
-    stem kernel (every other conv tuned as usual): oracle bits."""
+    stem kernel (every other conv tuned as usual): oracle bits.  (MobileNetV2's
+    stem runs inside the stem -> depthwise -> projection kernel by default;
+    RTENHIP_STEM_DWPW=0 keeps it a conv of its own here.)"""
     import torch
     import graph_runner
     from rten_hip import models
 
     monkeypatch.setenv("RTENHIP_PW_VALU", "800")
+    monkeypatch.setenv("RTENHIP_STEM_DWPW", "0")
     spec = getattr(models, model)()
     x = np.random.default_rng(21).random((2, 3, 224, 224), dtype=np.float32)
     exp = graph_runner.run(spec, {spec.inputs[0]: x})[spec.outputs[0]]
