@@ -140,6 +140,12 @@ rtenhip_status launch_pool(int is_max, const float* x, float* y, int64_t NC, int
                            int OH, int OW, int kh, int kw, int sh, int sw, int pt, int pl,
                            int count_include_pad, hipStream_t s);
 rtenhip_status launch_gap(const float* x, float* y, int64_t NC, int64_t HW, hipStream_t s);
+// Streaming depthwise (dw_stream.hip) for 14x14 / 7x7 planes; false when the
+// shape is not one it handles.
+bool launch_depthwise_stream(const float* x, const float* w, const float* bias, float* y, int N, int C, int H,
+                             int W, int OH, int OW, int kh, int kw, int sh, int sw, int dh, int dw, int pt, int pl,
+                             const int* omin, const int* omax, const float* residual, int act, float lo, float hi,
+                             hipStream_t s, rtenhip_status& st);
 rtenhip_status launch_depthwise(const float* x, const float* w, const float* bias, float* y,
                                 int N, int C, int H, int W, int OH, int OW, int kh, int kw,
                                 int sh, int sw, int dh, int dw, int pt, int pl,

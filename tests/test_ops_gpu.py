@@ -229,6 +229,40 @@ def test_depthwise_flat_residual_clip(rh, oracle, shape):
     assert_bits(got, exp, "depthwise flat residual clip")
 
 
+DW_STREAM_CASES = [
+    # (N, C, H, stride, act): MobileNetV2's 14x14 / 7x7 / 14 -> 7 depthwise
+    # layers and ragged batches (blocks with one or several groups, the ring's
+    # short tails)
+    (3, 384, 14, 1, "clip"), (5, 576, 14, 1, "clip"), (3, 960, 7, 1, "clip"), (2, 576, 14, 2, "clip"),
+    (9, 32, 14, 1, "relu"), (7, 64, 7, 1, None), (11, 16, 14, 2, "relu"), (1, 16, 14, 1, None),
+]
+
+
+@pytest.mark.parametrize("case", DW_STREAM_CASES, ids=lambda c: "x".join(map(str, c[:4])) + f"-{c[4]}")
+def test_depthwise_stream_bitexact(rh, oracle, case):
+    """Streaming depthwise kernel (dw_stream.hip: persistent blocks, LDS-DMA
+    ring of plane groups) == the reference depthwise + activation, and the
+    kernel is the one that ran (its launch counter moves)."""
+    import ctypes as C
+
+    N, Ch, H, s, act = case
+    x = rnd(oracle, 51, N, Ch, H, H)
+    w = rnd(oracle, 52, Ch, 1, 3, 3, scale=0.6)
+    b = rnd(oracle, 53, Ch)
+    exp = oracle.conv(x, w, b, pads=(1, 1, 1, 1), strides=(s, s), groups=Ch)
+    if act == "clip":
+        exp = oracle.clip(exp, 0.0, 0.25)
+    elif act == "relu":
+        exp = np.maximum(exp, np.float32(0.0))
+    lib = rh.lib()
+    lib.rtenhip_debug_dw_stream_launches.restype = C.c_longlong
+    before = lib.rtenhip_debug_dw_stream_launches()
+    kw = {"act": act, "act_range": (0.0, 0.25)} if act == "clip" else ({"act": act} if act else {})
+    got = host(rh.conv(dev(x), dev(w), dev(b), padding=(1, 1, 1, 1), strides=(s, s), groups=Ch, **kw))
+    assert lib.rtenhip_debug_dw_stream_launches() == before + 1
+    assert_bits(got, exp, f"dw stream {case}")
+
+
 def test_conv_fused_residual_relu(rh, oracle):
     """Conv -> Add(residual) -> Relu fused epilogue == the three reference ops."""
     x = rnd(oracle, 31, 2, 64, 14, 14)
