@@ -70,7 +70,8 @@ struct DwsDesc {
   float lo, hi;
 };
 
-template <int H, int S, int PB, int NBUF>
+// NSEG: output row segments per row (a thread owns SEG = OW / NSEG outputs).
+template <int H, int S, int PB, int NSEG, int NBUF>
 __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
   using Sh = DwsShape<H, S>;
   constexpr int W = Sh::W, OH = Sh::OH, OW = Sh::OW;
@@ -81,7 +82,10 @@ __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
   constexpr int BUF = NDMA * DWS_NW * 256;           // floats per ring slot
   constexpr int GO4 = PB * OHW / 4;                  // output float4s per group
   constexpr int NST = (GO4 + DWS_NT - 1) / DWS_NT;   // 16-byte stores per lane and group
-  static_assert(PB * OH <= DWS_NT, "one output row per thread");
+  static_assert(OW % NSEG == 0 && PB * OH * NSEG <= DWS_NT, "one row segment per thread");
+  static_assert(NSEG == 1 || S == 1, "segmented rows at stride 1");
+  constexpr int SEG = OW / NSEG;
+  constexpr int WC = (SEG - 1) * S + 3;  // input columns of a segment's window
   static_assert(NBUF == 3, "wait counts below assume a ring of 3");
   static_assert((GF * 4) % 16 == 0 && (PB * OHW) % 4 == 0, "whole float4s per group");
   static_assert(PB * OHW <= BUF, "outputs staged in the slot");
@@ -91,7 +95,8 @@ __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
   const int chunk = blockIdx.x % d.nch;
   const int n0 = blockIdx.x / d.nch;
   const int ng = n0 < d.N ? (d.N - n0 + d.step - 1) / d.step : 0;
-  const int pp = tid / OH, oy = tid - pp * OH;
+  const int pp = tid / (OH * NSEG), rem = tid - pp * (OH * NSEG);
+  const int oy = rem / NSEG, sg = rem - oy * NSEG;
   const bool active = pp < PB;
   const int c = chunk * PB + (active ? pp : 0);
 
@@ -149,6 +154,11 @@ __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
   const bool row2_ok = oy * S + 1 < H;
   const int iy0 = row0_ok ? oy * S - 1 : 0;
   const int iy2 = row2_ok ? oy * S + 1 : 0;
+  // Window columns ix = x0 + j, j < WC; only the first and the last can fall
+  // outside the image (compile-time with whole rows, per segment otherwise).
+  const int x0 = sg * SEG * S - 1;
+  const bool colL_ok = x0 >= 0;
+  const bool colR_ok = x0 + WC - 1 < W;
 
   for (int i = 0; i < ng; i++) {
     const int slot = i % NBUF;
@@ -157,24 +167,34 @@ __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
     asm volatile("" ::: "memory");  // no LDS read moves above the barrier
     if (i + 2 < ng) issue(i + 2, (i + 2) % NBUF);
     const float* tp = ring + slot * BUF + (active ? pp : 0) * HW;
-    float rw[3][W];
+    float rw[3][WC];
 #pragma unroll
-    for (int x = 0; x < W; x++) {
-      rw[0][x] = tp[iy0 * W + x];
-      rw[1][x] = tp[oy * S * W + x];
-      rw[2][x] = tp[iy2 * W + x];
+    for (int j = 0; j < WC; j++) {
+      const int ix = NSEG == 1 ? min(max(j - 1, 0), W - 1) : min(max(x0 + j, 0), W - 1);
+      rw[0][j] = tp[iy0 * W + ix];
+      rw[1][j] = tp[oy * S * W + ix];
+      rw[2][j] = tp[iy2 * W + ix];
     }
-    float out[OW];
+    float out[SEG];
 #pragma unroll
-    for (int ox = 0; ox < OW; ox++) {
+    for (int ox = 0; ox < SEG; ox++) {
       float acc = b0;
 #pragma unroll
       for (int ky = 0; ky < 3; ky++) {
         float t = acc;
 #pragma unroll
         for (int kx = 0; kx < 3; kx++) {
-          const int ix = ox * S - 1 + kx;
-          if (ix >= 0 && ix < W) t = __fadd_rn(t, __fmul_rn(rw[ky][ix], wk[ky * 3 + kx]));
+          const int j = ox * S + kx;
+          const float v = __fadd_rn(t, __fmul_rn(rw[ky][j], wk[ky * 3 + kx]));
+          if constexpr (NSEG == 1) {
+            if (j - 1 >= 0 && j - 1 < W) t = v;  // whole rows: x0 = -1
+          } else if (j == 0) {
+            t = colL_ok ? v : t;
+          } else if (j == WC - 1) {
+            t = colR_ok ? v : t;
+          } else {
+            t = v;
+          }
         }
         acc = ky == 0 ? (row0_ok ? t : acc) : ky == 2 ? (row2_ok ? t : acc) : t;
       }
@@ -190,7 +210,7 @@ __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
     float* op = ring + slot * BUF;
     if (active) {
 #pragma unroll
-      for (int ox = 0; ox < OW; ox++) op[pp * OHW + oy * OW + ox] = out[ox];
+      for (int ox = 0; ox < SEG; ox++) op[pp * OHW + oy * OW + sg * SEG + ox] = out[ox];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -210,11 +230,11 @@ __global__ __launch_bounds__(DWS_NT) void dw_stream_kernel(DwsDesc d) {
 
 long long g_dws_launches = 0;  // host-side count (tests: the kernel ran, not the fallback)
 
-template <int H, int S, int PB>
+template <int H, int S, int PB, int NSEG>
 bool launch_dws(const float* x, const float* w, const float* bias, float* y, int N, int C, int act, float lo,
                 float hi, hipStream_t s, rtenhip_status& st) {
   if (C % PB != 0) return false;
-  auto kern = dw_stream_kernel<H, S, PB, 3>;
+  auto kern = dw_stream_kernel<H, S, PB, NSEG, 3>;
   static int cus = 0, occ = 0;
   if (cus == 0) {
     int dev = 0;
@@ -258,6 +278,10 @@ bool launch_depthwise_stream(const float* x, const float* w, const float* bias, 
   if (!on || residual || kh != 3 || kw != 3 || dh != 1 || dw != 1 || sh != sw || pt != 1 || pl != 1 || H != W ||
       N <= 0 || C <= 0)
     return false;
+  static const bool dws28 = [] {
+    const char* e = getenv("RTENHIP_DW_STREAM28");  // A/B: 0 leaves 28x28 to depthwise_lds4_kernel
+    return !(e && atoi(e) == 0);
+  }();
   const int S = sh, OE = (H + 2 - 3) / S + 1;
   if (OH != OE || OW != OE) return false;
   // The kernel skips exactly the columns outside the image; the caller's
@@ -270,9 +294,10 @@ bool launch_depthwise_stream(const float* x, const float* w, const float* bias, 
   }
   if ((uintptr_t)x % 16 != 0 || (uintptr_t)y % 16 != 0) return false;
   if ((int64_t)N * C * H * W >= (int64_t(1) << 29)) return false;
-  if (H == 14 && S == 1) return launch_dws<14, 1, 16>(x, w, bias, y, N, C, act, lo, hi, s, st);
-  if (H == 7 && S == 1) return launch_dws<7, 1, 32>(x, w, bias, y, N, C, act, lo, hi, s, st);
-  if (H == 14 && S == 2) return launch_dws<14, 2, 16>(x, w, bias, y, N, C, act, lo, hi, s, st);
+  if (H == 14 && S == 1) return launch_dws<14, 1, 16, 1>(x, w, bias, y, N, C, act, lo, hi, s, st);
+  if (H == 7 && S == 1) return launch_dws<7, 1, 32, 1>(x, w, bias, y, N, C, act, lo, hi, s, st);
+  if (H == 14 && S == 2) return launch_dws<14, 2, 16, 1>(x, w, bias, y, N, C, act, lo, hi, s, st);
+  if (H == 28 && S == 1 && dws28) return launch_dws<28, 1, 4, 2>(x, w, bias, y, N, C, act, lo, hi, s, st);
   return false;
 }
 

@@ -639,6 +639,13 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
       b.omax[kx] = omax > OW ? OW : omax;
     }
     const int planes = N * C;
+    // Small square planes (28x28, 14x14, 7x7) without a residual: the streaming
+    // kernel (dw_stream.hip), copies of later plane groups in flight while a
+    // group computes.
+    rtenhip_status dws_st = RTENHIP_OK;
+    if (launch_depthwise_stream(x, w, bias, y, N, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, b.omin, b.omax,
+                                residual, act, lo, hi, s, dws_st))
+      return dws_st;
     // 4 output columns per thread (depthwise_lds4_kernel) where it applies:
     // stride 1 (3.1 -> 4.1 TB/s on MobileNetV2's s1 layers).  The stride-2
     // instance is bit-exact too but slower than depthwise_lds_kernel there
@@ -666,13 +673,6 @@ rtenhip_status launch_depthwise(const float* x, const float* w, const float* bia
         return RTENHIP_OK;
       }
     }
-    // Small square planes (14x14, 7x7) without a residual: the streaming
-    // kernel (dw_stream.hip), copies of later plane groups in flight while a
-    // group computes.
-    rtenhip_status dws_st = RTENHIP_OK;
-    if (launch_depthwise_stream(x, w, bias, y, N, C, H, W, OH, OW, kh, kw, sh, sw, dh, dw, pt, pl, b.omin, b.omax,
-                                residual, act, lo, hi, s, dws_st))
-      return dws_st;
     // LDS tiling (depthwise_lds_kernel): PB planes x OW columns of threads,
     // TH output rows each, at most 16 KB of staged input per block.
     if (OW <= 256 && kh * kw <= 64) {

@@ -11,7 +11,7 @@ tail -3 $O/tests.log; grep -E "^FAILED|Error" $O/tests.log | head -20
 B="python -u bench.py --model mobilenet_v2 --batch 128 --no-cpu-baseline --no-secondary --steps 30 --warmup 5"
 for r in 1 2; do
   for v in 0 1; do
-    RTENHIP_DW_STREAM=$v timeout -k 10 300 $B > $O/b_${v}_$r.json 2> $O/b_${v}_$r.err || { echo "bench failed"; tail -20 $O/b_${v}_$r.err; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'])" $O/b_${v}_$r.json "stream=$v run$r"
+    env "RTENHIP_DW_STREAM${DWS_VAR:-}=$v" timeout -k 10 300 $B > $O/b_${v}_$r.json 2> $O/b_${v}_$r.err || { echo "bench failed"; tail -20 $O/b_${v}_$r.err; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'])" $O/b_${v}_$r.json "${DWS_VAR:-stream}=$v run$r"
   done
 done

@@ -235,6 +235,8 @@ DW_STREAM_CASES = [
     # short tails)
     (3, 384, 14, 1, "clip"), (5, 576, 14, 1, "clip"), (3, 960, 7, 1, "clip"), (2, 576, 14, 2, "clip"),
     (9, 32, 14, 1, "relu"), (7, 64, 7, 1, None), (11, 16, 14, 2, "relu"), (1, 16, 14, 1, None),
+    # 28x28: two row segments per thread (window edges per segment)
+    (3, 192, 28, 1, "clip"), (2, 8, 28, 1, "relu"), (5, 12, 28, 1, None),
 ]
 
 
