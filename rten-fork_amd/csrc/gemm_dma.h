@@ -70,9 +70,6 @@ struct DmaDesc {
   // consecutive tiles -- what one XCD's resident blocks work on together --
   // is a compact block of A rows and B columns in that XCD's L2.
   int swz;
-  // Persistent launches: prefetch the next item's first K tiles before the
-  // epilogue stores (gemm_dma_kernel PFT; set by launch_gemm_dma).
-  int pf;
   // Dual GEMM (set by launch_gemm_dma): 1 = one continuous K loop over both
   // segments (segment 2's first tiles stream in while segment 1 finishes),
   // 0 = two passes with a drain between them.

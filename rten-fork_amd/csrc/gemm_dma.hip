@@ -133,18 +133,6 @@ rtenhip_status launch_gemm_dma(const DmaDesc& d, int cfg, hipStream_t s, const D
     static const int swz_all = [] { const char* e = getenv("RTENHIP_DMA_SWZ"); return e ? atoi(e) : -1; }();
     if (swz_all >= 0) dd.swz = swz_all;
   }
-  {
-    // Cross-item prefetch of persistent launches (gemm_dma_kernel PFT; the
-    // kernel applies it only where its compile-time shape allows).  Output
-    // offsets must fit the 31-bit buffer range its stores use.
-    // RTENHIP_DMA_PF=0 disables it (A/B experiments).
-    static const int pf_env = [] { const char* e = getenv("RTENHIP_DMA_PF"); return e ? atoi(e) : 1; }();
-    const int64_t imgs = d.P > 0 ? ((int64_t)d.N + d.P - 1) / d.P : 0;
-    const int64_t last = (imgs - 1) * d.out_img + (d.P - 1) + (int64_t)(d.M - 1) * d.out_c + d.out_off;
-    dd.pf = pf_env && d.persist_k > 0 && !d2 && !d.pk_out && d.vec4 && !d.cin && !d.residual && d.split_tiles == 0 &&
-            d.K <= DKC &&
-            d.out_off == 0 && last >= 0 && (last + 4) * 4 < (int64_t(1) << 31);
-  }
   const DmaCfgInfo& ci = kDmaCfgs[cfg];
   const int tiles = ((d.M + ci.bm - 1) / ci.bm) * ((d.N + ci.bn - 1) / ci.bn);
   if (d.split_tiles > 0) {

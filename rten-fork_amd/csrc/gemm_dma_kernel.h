@@ -67,7 +67,6 @@ constexpr int DKC = 256;
 // stricter.)  M0 holds the wave-uniform LDS destination; one wait state
 // separates the M0 write from the DMA.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t dws4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 make_rsrc(const void* base, uint32_t num_records) {
   const uint64_t a = (uint64_t)base;
   return (u32x4){(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, num_records, 0x00020000u};
@@ -79,12 +78,12 @@ __device__ __forceinline__ uint32_t lds_addr(const float* p) {
 #pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void lds_dma16(u32x4 r, uint32_t dst, uint32_t voff, uint32_t soff) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(soff))
+               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(soff)
                : "memory", "m0");
 }
 __device__ __forceinline__ void lds_dma4(u32x4 r, uint32_t dst, uint32_t voff, uint32_t soff) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %3 offen lds"
-               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(soff))
+               ::"s"(__builtin_amdgcn_readfirstlane(dst)), "v"(voff), "s"(r), "s"(soff)
                : "memory", "m0");
 }
 #pragma clang diagnostic pop
@@ -163,25 +162,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   };
   __shared__ int last_arrival;  // split tiles: this block folds (see process)
 
-  // Cross-item prefetch (persistent launches, d.pf): a block issues its next
-  // item's first PFT K tiles (stages 0 .. PFT-1) right before the current
-  // item's epilogue stores, so they land while it stores and the next K loop
-  // starts on them.  The vectorised epilogue's transpose slots sit above those
-  // stages.  Single-KC items with one 32x32 block per wave, vectorised
-  // epilogue only (a fixed number of stores per lane: see the waits).
-  constexpr bool VEC_FITS_K = NW * 1024 <= STAGES * STAGE;
-  constexpr int SLOT_STAGES = (NW * 1024 + STAGE - 1) / STAGE;
-  constexpr int PFT = (!DUAL && !MULTI_KB && VEC_FITS_K && MI * NI == 1 && STAGES > SLOT_STAGES)
-                          ? STAGES - SLOT_STAGES : 0;
-  constexpr bool RES_PRE_K = VEC_FITS_K && !MULTI_KB && MI * NI == 1 && BK == 16 && MINW <= 4;
-  // Operations a block issues between its prefetched tiles and the rest of
-  // the next item: the epilogue's 4 stores, then the next item's bias
-  // prefetch (RES_PRE: 4 loads, made unconditional under d.pf).  Items with a
-  // residual are not prefetched (launch_gemm_dma): its loads would reuse the
-  // stores' data registers, and the compiler's wait for those stores would
-  // drain the prefetched tiles.
-  constexpr int PF_EXTRA = 4 + (RES_PRE_K ? 4 : 0);
-
   // One work item: output tile wg (kb_split < 0), or K block kb_split of split
   // tile split_idx (wg = n_full + split_idx).
   // Dual: segment 1's folded values, carried into segment 2's epilogue.
@@ -193,7 +173,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   // refill DMAs running on across the boundary, so segment 2's first tiles
   // are in flight while segment 1 finishes; segment 1's fold is the carry.
   auto process = [&](const KDesc& d, const int wg, const int kb_split, const int split_idx, const int mode,
-                     const KDesc& e, const int pre, const int nxt) __attribute__((always_inline)) {
+                     const KDesc& e) __attribute__((always_inline)) {
   // Lane-derived values are recomputed per item: hoisted out of the item loop
   // they would stay live across it and spill.
   int tid = tid_o;
@@ -203,20 +183,17 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   const int wm = (wave / WAVES_N) * WM;
   const int wn = (wave % WAVES_N) * WN;
   const int M = d.M, N = d.N, K = d.K;
-  auto tile_of = [&](const int w, int& tmi_, int& tni_) __attribute__((always_inline)) {
-    if (d.swz > 0) {  // strips of swz tile columns, n fastest within a strip (see DmaDesc::swz)
-      const int tiles_n = (N + BN - 1) / BN, sw = d.swz * tiles_m;
-      const int st = w / sw, r = w - st * sw;
-      const int gw = min(d.swz, tiles_n - st * d.swz);
-      tmi_ = r / gw;
-      tni_ = st * d.swz + (r - tmi_ * gw);
-    } else {
-      tmi_ = w % tiles_m;
-      tni_ = w / tiles_m;
-    }
-  };
   int tmi, tni;
-  tile_of(wg, tmi, tni);
+  if (d.swz > 0) {  // strips of swz tile columns, n fastest within a strip (see DmaDesc::swz)
+    const int tiles_n = (N + BN - 1) / BN, sw = d.swz * tiles_m;
+    const int st = wg / sw, r = wg - st * sw;
+    const int gw = min(d.swz, tiles_n - st * d.swz);
+    tmi = r / gw;
+    tni = st * d.swz + (r - tmi * gw);
+  } else {
+    tmi = wg % tiles_m;
+    tni = wg / tiles_m;
+  }
   const int tm = tmi * BM;
   const int tn = tni * BN;
   const int tiles_k = (K + BK - 1) / BK;
@@ -234,48 +211,43 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   // Per-lane B offsets: one per 64-column group this wave loads.
   constexpr int NG = BN / 64;
   uint32_t vb[NG];
+#pragma unroll
+  for (int g = 0; g < NG; g++) {
+    // LDS position p of a B row holds column wn' + ni*32 + l where p = wn' + l*NI + ni,
+    // so a lane's NI B values for one k are adjacent (one ds_read).
+    const int pos = g * 64 + lane;
+    const int q = pos % WN;
+    const int n = tn + (pos - q) + (q % NI) * 32 + q / NI;
+    uint32_t off = DMA_OOB;
+    if (n < N) {
+      const int img = fdiv(n, d.fdP);
+      const int p = n - img * d.P;
+      const int oy = fdiv(p, d.fdOW);
+      const int ox = p - oy * d.OW;
+      off = (uint32_t)(((int64_t)img * d.x_img + (int64_t)oy * d.ystride + (int64_t)ox * d.xstride) * 4);
+    }
+    vb[g] = off;
+  }
   // BVEC: instruction i of this wave covers k rows 4*(wave*B_PER_W+i) .. +3 of
   // the tile; lane -> row (lane >> 4), columns 4*(lane & 15) .. +3.
   uint32_t vb4[BVEC ? B_PER_W : 1];
-  // Per-lane B offsets of the tile at column tn_ (this item's; the
-  // prefetched next item's).
-  auto set_b = [&](const int tn_) __attribute__((always_inline)) {
+  if constexpr (BVEC) {
 #pragma unroll
-    for (int g = 0; g < NG; g++) {
-      // LDS position p of a B row holds column wn' + ni*32 + l where p = wn' + l*NI + ni,
-      // so a lane's NI B values for one k are adjacent (one ds_read).
-      const int pos = g * 64 + lane;
-      const int q = pos % WN;
-      const int n = tn_ + (pos - q) + (q % NI) * 32 + q / NI;
+    for (int i = 0; i < B_PER_W; i++) {
+      const int gi = wave * B_PER_W + i;
+      const int kk = gi * 4 + (lane >> 4);
+      const int n = tn + (lane & 15) * 4;
       uint32_t off = DMA_OOB;
       if (n < N) {
         const int img = fdiv(n, d.fdP);
         const int p = n - img * d.P;
-        const int oy = fdiv(p, d.fdOW);
-        const int ox = p - oy * d.OW;
-        off = (uint32_t)(((int64_t)img * d.x_img + (int64_t)oy * d.ystride + (int64_t)ox * d.xstride) * 4);
+        off = (uint32_t)(((int64_t)img * d.x_img + p) * 4 + (int64_t)kk * d.kstride * 4);
       }
-      vb[g] = off;
+      vb4[i] = off;
     }
-    if constexpr (BVEC) {
-#pragma unroll
-      for (int i = 0; i < B_PER_W; i++) {
-        const int gi = wave * B_PER_W + i;
-        const int kk = gi * 4 + (lane >> 4);
-        const int n = tn_ + (lane & 15) * 4;
-        uint32_t off = DMA_OOB;
-        if (n < N) {
-          const int img = fdiv(n, d.fdP);
-          const int p = n - img * d.P;
-          off = (uint32_t)(((int64_t)img * d.x_img + p) * 4 + (int64_t)kk * d.kstride * 4);
-        }
-        vb4[i] = off;
-      }
-    }
-  };
-  set_b(tn);
+  }
   const uint32_t va = (uint32_t)(wave * A_PER_W * A_CHUNK + lane * A_LB);
-  uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
+  const uint32_t a_row_base = (uint32_t)tmi * (uint32_t)tiles_k * (BM * BK * 4);
   const_int_t* ktab4 = (const_int_t*)d.ktab4;
   const uint32_t lds0 = lds_addr(lds);
   u32x4 ra1 = ra, rb1 = rb;  // segment 1's resources (mode 3)
@@ -391,20 +363,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
 #pragma unroll
     for (int j = 0; j < A_PER_W + B_PER_W; j++) issue_j(stage, kt, j, 0);
   };
-  // The next item's first PFT tiles into stages 0 .. PFT-1 (its K tiles 0..;
-  // this item's B offsets and A row are no longer needed).
-  auto prefetch_next = [&]() __attribute__((always_inline)) {
-    int tmn, tnn;
-    tile_of(__builtin_amdgcn_readfirstlane(nxt), tmn, tnn);
-    set_b(__builtin_amdgcn_readfirstlane(tnn) * BN);
-    a_row_base = __builtin_amdgcn_readfirstlane((uint32_t)tmn * (uint32_t)tiles_k * (BM * BK * 4));
-#pragma unroll
-    for (int s = 0; s < PFT; s++)
-      if (s < tiles_k) {
-        load_k(s, 0);
-        issue(s, s);
-      }
-  };
 
   f32x16 acc[MI][NI];
 #pragma unroll
@@ -484,25 +442,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   };
-  // wait_dma when the tile waited for is one the previous item prefetched:
-  // the PF_EXTRA operations issued after it are younger too.
-  auto wait_dma_x = [&](int allowed_tiles, bool extra) __attribute__((always_inline)) {
-    if constexpr (PFT > 0) {
-      if (extra) {
-        if (STAGES >= 4 && allowed_tiles >= 3) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * 3 + PF_EXTRA) : "memory");
-        } else if (STAGES >= 3 && allowed_tiles >= 2) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE * 2 + PF_EXTRA) : "memory");
-        } else if (allowed_tiles >= 1) {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_TILE + PF_EXTRA) : "memory");
-        } else {
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PF_EXTRA) : "memory");
-        }
-        return;
-      }
-    }
-    wait_dma(allowed_tiles);
-  };
   auto read_tile = [&](auto set_tag, int stage) __attribute__((always_inline)) {
     constexpr int SET = decltype(set_tag)::value;
     if constexpr (RTENHIP_DMA_EXPERIMENT == 4) {
@@ -576,7 +515,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     const bool refill = kt + 1 < kt_hi && kt + STAGES < kt_hi;
     if (kt + 1 < kt_hi) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_dma_x(min(STAGES - 2, kt_hi - kt - 2), kt + 1 < pre);
+      wait_dma(min(STAGES - 2, kt_hi - kt - 2));
       if constexpr (RTENHIP_DMA_EXPERIMENT < 3) __builtin_amdgcn_s_barrier();
       stage = stage + 1 == STAGES ? 0 : stage + 1;
       read_tile(std::integral_constant<int, SET ^ 1>{}, stage);
@@ -605,16 +544,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   // (kt0 - kt_lo) % STAGES == 0 (stage of tile kt0 is 0).
   auto run = [&](int kt0, int kt1) __attribute__((always_inline)) {
     int kt = kt0;
-    if (PFT > 0 && pre > 0) {
-      // A prefetched item's first tiles wait with the extra count (body);
-      // after STAGES of them (rounded up to even: register-set parity) the
-      // fast path's stage / parity invariant holds.
-      const int k1 = min(kt0 + ((STAGES + 1) & ~1), kt1);
-      for (; kt < k1; kt += 2) {
-        body(I0{}, kt);
-        if (kt + 1 < k1) body(I1{}, kt + 1);
-      }
-    }
     if constexpr (FAST) {
       if (kt + STAGES <= kt1 && kt + 2 * STAGES - 1 < kt_hi) load_k(kt + STAGES, 0);
       for (; kt + STAGES <= kt1 && kt + 2 * STAGES - 1 < kt_hi; kt += STAGES) {
@@ -645,19 +574,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   // With RES_PRE the bias of the lane's 4 epilogue rows is prefetched too.
   float bpre[RES_PRE ? 4 : 1];
   if constexpr (RES_PRE) {
-    static_assert(!RES_PRE || RES_PRE_K, "PF_EXTRA counts these loads");
-    if (pre > 0) {
-      // Exactly 4 loads (PF_EXTRA): dummy addresses in the packed A when
-      // there is no bias, 256 bytes apart so that no two of them are merged
-      // into one load.  (No residual: d.pf is never set with one.)
-      const float* bsrc = d.bias ? d.bias : d.apk;
-#pragma unroll
-      for (int i = 0; i < 4; i++) bpre[i] = bsrc[d.bias ? min(tm + wm + i * 8 + rr, M - 1) : 64 * i];
-    } else if (d.vec4 && d.bias && !d.cin) {
+    if (d.vec4 && d.bias && !d.cin) {
 #pragma unroll
       for (int i = 0; i < 4; i++) bpre[i] = d.bias[min(tm + wm + i * 8 + rr, M - 1)];
     }
-    if (pre == 0 && d.vec4 && d.residual) {
+    if (d.vec4 && d.residual) {
       const int n = tn + wn + c4;
       const bool ncol_ok = n <= N - 1;
       const int nn = ncol_ok ? n : 0;
@@ -676,11 +597,11 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
   // Prologue: fill every stage, wait for the first tile, read it.
 #pragma unroll
   for (int s = 0; s < STAGES; s++)
-    if (s >= pre && kt_lo + s < kt_hi) {  // (tiles below pre: prefetched by the previous item)
+    if (kt_lo + s < kt_hi) {
       load_k(kt_lo + s, 0);
       issue(s, kt_lo + s);
     }
-  wait_dma_x(min(STAGES, kt_hi - kt_lo) - 1, pre > 0);
+  wait_dma(min(STAGES, kt_hi - kt_lo) - 1);
   __builtin_amdgcn_s_barrier();
   read_tile(I0{}, 0);
 
@@ -901,11 +822,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land in the slots
     __syncthreads();  // every wave is done reading the K stages
     if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_sync = __builtin_amdgcn_s_memrealtime();
-    float* slot = lds + PFT * STAGE + wave * 1024;  // (above the prefetched stages)
-    // Prefetch: the stores become raw buffer stores, out-of-range lanes at an
-    // offset the hardware drops, so every lane issues exactly 4 (PF_EXTRA).
-    const bool pf_now = PFT > 0 && nxt >= 0;
-    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(d.out, 0, 0x7fffffff, 0x00020000);
+    float* slot = lds + wave * 1024;
     // Without a C input the bias is added after the transpose: a lane then
     // needs the bias of its 4 rows only (vector loads issued together),
     // instead of two scalar loads per accumulator element.
@@ -970,24 +887,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
         for (int j = 0; j < 16; j++) slot[((j & 3) + 8 * (j >> 2) + 4 * half) * 32 + l32] = v[j];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (RTENHIP_DMA_EXPERIMENT == 5) t_bias = __builtin_amdgcn_s_memrealtime();
-        if constexpr (PFT > 0) {
-          // Every value this epilogue loaded is waited for here (a use, then a
-          // builtin s_waitcnt vmcnt(0) that the compiler's waitcnt pass sees,
-          // on every path), so no compiler wait after the prefetch DMAs
-          // drains them.
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            asm volatile("" ::"v"(bl[i]), "v"(bnm[i]), "v"(bns[i]), "v"(bnb[i]));
-            if constexpr (RES_PRE) {
-              asm volatile("" ::"v"(bpre[i]), "v"(rpre[i].x), "v"(rpre[i].y), "v"(rpre[i].z), "v"(rpre[i].w));
-            } else {
-              asm volatile("" ::"v"(rl[i].x), "v"(rl[i].y), "v"(rl[i].z), "v"(rl[i].w));
-            }
-          }
-          asm volatile("" ::"v"(cb.x), "v"(cb.y), "v"(cb.z), "v"(cb.w));
-          __builtin_amdgcn_s_waitcnt(0x0F70);
-          if (pf_now) prefetch_next();
-        }
 #pragma unroll
         for (int i = 0; i < 4; i++) {
           const int row = i * 8 + rr;
@@ -1032,11 +931,7 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
             x.z = apply_act_sel(x.z);
             x.w = apply_act_sel(x.w);
           }
-          if (PFT > 0 && pf_now) {
-            const dws4_t u = {__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)};
-            __builtin_amdgcn_raw_buffer_store_b128(u, orsrc, ok ? (int)((obase + (int64_t)m * d.out_c) * 4) : (int)DMA_OOB,
-                                                   0, 0);
-          } else if (ok) {
+          if (ok) {
             if (d.pk_out) {  // the consumer MatMul's packed A (row m, k = n .. n + 3)
               store_packed_a4(d.pk_out, d.pk_lbm, d.pk_lbk, d.pk_tiles_k, m, n, x);
             } else {
@@ -1144,12 +1039,6 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     p = bid / nq;
   }
   const int len = persistent ? f_n + st_n * d.nkb : 1;
-  // Cross-item prefetch (see PFT): whole-tile items of a persistent launch
-  // whose outputs take the vectorised epilogue.
-  const bool pf = PFT > 0 && persistent && d.pf && d.vec4 && !d.pk_out && !d.cin && !d.residual && d.split_tiles == 0 &&
-                  d.K <= DKC;
-  const int pf_tiles = min(PFT, (d.K + BK - 1) / BK);
-  int pre = 0;
   for (; p < len; p += stride) {
     int wg, kbs = -1, si = -1;
     if (!persistent) {
@@ -1176,31 +1065,22 @@ __global__ __launch_bounds__(NT, MINW) void gemm_dma_kernel(DmaDesc d, DmaDesc d
     const KDesc* dp = (const KDesc*)__builtin_amdgcn_kernarg_segment_ptr();
     asm volatile("" : "+s"(dp));
     if constexpr (DUAL && BVEC) {
-      process(dp[0], wg, -1, -1, 3, dp[1], 0, -1);  // (16-byte B copies: one K loop only)
+      process(dp[0], wg, -1, -1, 3, dp[1]);  // (16-byte B copies: one K loop only)
     } else if constexpr (DUAL) {
       if (dp[0].dual_one) {
-        process(dp[0], wg, -1, -1, 3, dp[1], 0, -1);  // d2 (the second kernel argument): segment 1
+        process(dp[0], wg, -1, -1, 3, dp[1]);  // d2 (the second kernel argument): segment 1
       } else {
-        process(dp[1], wg, -1, -1, 1, dp[1], 0, -1);  // segment 1
+        process(dp[1], wg, -1, -1, 1, dp[1]);  // segment 1
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();  // segment 1's LDS stages are free
-        process(dp[0], wg, -1, -1, 2, dp[1], 0, -1);
+        process(dp[0], wg, -1, -1, 2, dp[1]);
       }
     } else {
-      const int nxt = (pf && p + stride < f_n) ? f_lo + p + stride : -1;
-      process(*dp, wg, kbs, si, 0, *dp, pre, nxt);
-      pre = nxt >= 0 ? pf_tiles : 0;
+      process(*dp, wg, kbs, si, 0, *dp);
     }
     if (!persistent) break;
     // Every wave is done with this item's LDS before the next item's DMAs.
-    if (pf) {
-      // (no vmcnt drain: the prefetched tiles and the stores stay in flight)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();
-    }
+    __syncthreads();
   }
   stamp();
 }
