@@ -126,6 +126,45 @@ def test_resnet50_persistent_modes(rh, monkeypatch, mode):
         assert _bits_equal(o, exp), np.abs(o - exp).max()
 
 
+_CFG_EXP = {}
+
+
+@pytest.mark.parametrize("cfg", [7, 14, 17, 19, 20, 21, 22])
+def test_dma_forced_config_persistent(rh, monkeypatch, cfg):
+    """Every DMA GEMM conv of ResNet-50 at batch 3 under one forced tile
+    configuration (3- and 4-stage rings, 64- and 32-row tiles), launched
+    persistent (RTENHIP_PERSIST=4: blocks walking several items, ragged last
+    tiles, KC-split units after whole tiles), untuned: the oracle's bits in the
+    eager, captured and replayed runs."""
+    import ctypes as C
+
+    import torch
+    import graph_runner
+    from rten_hip import models
+
+    spec = models.resnet50()
+    x = np.random.default_rng(5).random((3, 3, 224, 224), dtype=np.float32)
+    if "exp" not in _CFG_EXP:
+        _CFG_EXP["exp"] = graph_runner.run(spec, {"input": x})[spec.outputs[0]]
+    exp = _CFG_EXP["exp"]
+    monkeypatch.setenv("RTENHIP_TUNE", "0")
+    monkeypatch.setenv("RTENHIP_PERSIST", "4")
+    lib = rh.lib()
+    lib.rtenhip_debug_set_dma_config.argtypes = [C.c_int]
+    lib.rtenhip_debug_set_dma_config(cfg)
+    try:
+        g = spec.to_graph()
+        xd = torch.from_numpy(x).cuda()
+        out = None
+        for _ in range(3):  # eager, capture, replay
+            out = g.run({g.input_ids[0]: xd}, g.output_ids, out=out)
+            torch.cuda.synchronize()
+            o = out[0].cpu().numpy()
+            assert _bits_equal(o, exp), (cfg, np.abs(o - exp).max())
+    finally:
+        lib.rtenhip_debug_set_dma_config(-1)
+
+
 def test_graph_errors(rh):
     import torch
     from rten_hip.graph import Graph
