@@ -82,16 +82,21 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   // for the whole staging, not one per row group).
   const bool v4 = VEC || (((uintptr_t)v % 16 == 0) && d.v_s % 4 == 0);
   const bool k4 = VEC || (d.k_d == 1 && ((uintptr_t)kt % 16 == 0) && d.k_s % 4 == 0);
+  // A query-independent mask row ([B, 1, 1, S], BERT's) is staged with K and
+  // V, so the softmax phase reads it from LDS instead of making 64 global
+  // loads per lane on the critical path.  (Loaded first: the wait for K's
+  // LDS stores then leaves Q and V in flight.)
+  const bool mask_lds = d.mask && d.m_i == 0;
+  float mv = 0.f;
+  if (mask_lds && tid < S) mv = d.mask[b * d.m_b + hd * d.m_h + (int64_t)tid * d.m_j];
   constexpr int ST = AT_S * (AT_D / 4) / AT_THREADS;  // float4 positions per thread (8)
   float4 kk[ST], vv[ST];
 #pragma unroll
   for (int u = 0; u < ST; u++) {
     const int t = tid + u * AT_THREADS;
     const int j = t >> 4, c = (t & 15) * 4;
-    kk[u] = vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    kk[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if ((FULL || j < S) && RTENHIP_ATT_EXPERIMENT != 4) {
-      const float* vp = v + (int64_t)j * d.v_s + c;
-      vv[u] = v4 ? *(const float4*)vp : make_float4(vp[0], vp[1], vp[2], vp[3]);
       if (k4) {
         kk[u] = *(const float4*)(kt + (int64_t)j * d.k_s + c);
       } else {
@@ -100,12 +105,31 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
       }
     }
   }
-  // A query-independent mask row ([B, 1, 1, S], BERT's) is staged with K and
-  // V, so the softmax phase reads it from LDS instead of making 64 global
-  // loads per lane on the critical path.
-  const bool mask_lds = d.mask && d.m_i == 0;
-  float mv = 0.f;
-  if (mask_lds && tid < S) mv = d.mask[b * d.m_b + hd * d.m_h + (int64_t)tid * d.m_j];
+  const int i0 = wave * 32;
+  const int i = i0 + l32;  // this lane's query row
+  const bool row_ok = FULL || i < S;
+  // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand),
+  // issued right behind K (32 strided dword loads; as float4s with the
+  // elements h, h + 2 selected by lane half it became a private-array round
+  // trip through scratch), so its latency overlaps K's instead of following
+  // the K stores.
+  float qf[AT_D / 2];
+  {
+    const float* qr = q + (int64_t)(row_ok ? i : 0) * d.q_s + h;
+#pragma unroll
+    for (int s = 0; s < AT_D / 2; s++)
+      qf[s] = RTENHIP_ATT_EXPERIMENT == 4 ? 1.f : row_ok ? qr[2 * s] : 0.f;
+  }
+#pragma unroll
+  for (int u = 0; u < ST; u++) {
+    const int t = tid + u * AT_THREADS;
+    const int j = t >> 4, c = (t & 15) * 4;
+    vv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((FULL || j < S) && RTENHIP_ATT_EXPERIMENT != 4) {
+      const float* vp = v + (int64_t)j * d.v_s + c;
+      vv[u] = v4 ? *(const float4*)vp : make_float4(vp[0], vp[1], vp[2], vp[3]);
+    }
+  }
 #pragma unroll
   for (int u = 0; u < ST; u++) {
     const int t = tid + u * AT_THREADS;
@@ -118,21 +142,6 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
   }
   // (V stays in registers, still in flight, until the scores are done.)
   if (mask_lds && tid < S) Ms[tid] = mv;
-  const int i0 = wave * 32;
-  const int i = i0 + l32;  // this lane's query row
-  const bool row_ok = FULL || i < S;
-  // This lane's Q fragment, qf[s] = Q[i][2s + h] (the MFMA's B operand),
-  // loaded while the K / V stores land
-  float qf[AT_D / 2];
-  // (32 strided dword loads, all in flight together.  Loading the row as
-  // float4s and selecting elements h, h + 2 by lane half turned into a
-  // private-array round trip through scratch.)
-  {
-    const float* qr = q + (int64_t)(row_ok ? i : 0) * d.q_s + h;
-#pragma unroll
-    for (int s = 0; s < AT_D / 2; s++)
-      qf[s] = RTENHIP_ATT_EXPERIMENT == 4 ? 1.f : row_ok ? qr[2 * s] : 0.f;
-  }
   __syncthreads();  // K and the mask row staged
   const bool live = i0 < S;  // a wave past S only helps stage V
 
