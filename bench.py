@@ -182,7 +182,7 @@ _ROOF_KERNELS = {
     "resnet50": ("gemm_dma_kernel", "gemm_lat", "gemv", "conv_stem_kernel", "conv_pair_kernel"),
     "bert": ("gemm_dma_kernel", "pack_a_kernel", "attention_kernel"),
     "mobilenet_v2": ("gemm_dma_kernel", "gemm_lat", "gemv", "conv_pw_valu_kernel", "conv_direct",
-                     "depthwise", "expand_dw_kernel", "dw_project_kernel", "conv_stem_kernel"),
+                     "depthwise", "dw_stream_kernel", "expand_dw_kernel", "dw_project_kernel", "conv_stem_kernel"),
 }
 
 
