@@ -247,7 +247,7 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
       for (int c = 0; c < 4; c += 2) {
         if (FULL || 32 * t + 8 * g + 4 * h + c < S) {
           const vm_f32x2 x = (vm_f32x2){acc[t][4 * g + c], acc[t][4 * g + c + 1]} - m2;
-          const vm_f32x2 ex = RTENHIP_ATT_EXPERIMENT == 1 ? x : vm_exp2(x);
+          const vm_f32x2 ex = RTENHIP_ATT_EXPERIMENT == 1 ? x : vm_exp2_nonpos(x);
           acc[t][4 * g + c] = ex[0];
           acc[t][4 * g + c + 1] = ex[1];
           part2[c / 2] = part2[c / 2] + ex;
@@ -363,7 +363,8 @@ __global__ __launch_bounds__(AT_THREADS, 2) void attention_kernel(AttnDesc d) {
 // Check of the vecmath.h shortcuts against their plain forms (tests only):
 // out[0, n) = div_by(a / b), out[n, 2n) = __fdiv_rn(a, b), out[2n, 3n) =
 // vm_exp2 on (a[i], a[i ^ 1]) component 0, out[3n, 4n) = vm_exp(a[i]),
-// out[4n, 5n) = vm_gelu2 likewise, out[5n, 6n) = vm_gelu(a[i]).
+// out[4n, 5n) = vm_gelu2 likewise, out[5n, 6n) = vm_gelu(a[i]), out[6n, 7n) =
+// vm_exp2_nonpos on the pair, component 0 (meaningful for a <= 0 or NaN).
 __global__ void vecmath_check_kernel(const float* a, const float* b, int64_t n, float* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -375,6 +376,7 @@ __global__ void vecmath_check_kernel(const float* a, const float* b, int64_t n, 
   out[3 * n + i] = vm_exp(a[i]);
   out[4 * n + i] = vm_gelu2((vm_f32x2){a[i], a[i2]})[0];
   out[5 * n + i] = vm_gelu(a[i]);
+  out[6 * n + i] = vm_exp2_nonpos((vm_f32x2){a[i], a[i2]})[0];
 }
 
 bool attention_fast_ok(const AttnDesc& d) {

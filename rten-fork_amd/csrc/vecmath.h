@@ -76,6 +76,41 @@ __device__ __forceinline__ vm_f32x2 vm_exp2(vm_f32x2 x) {
   return r;
 }
 
+// vm_exp2 for arguments that are <= 0 or NaN (softmax's x - max, GELU's
+// -z^2), bit for bit.  There k = j <= 0 (or the value is replaced), so the
+// scale split is fixed: s1 = 2^-123 and s2 = (k << 23) - 0x83000000, and k
+// comes straight from the magic-number sum's low mantissa bits (j + MAGIC =
+// 1.5 * 2^23 + k exactly while |k| < 2^22; 0x4B400000 << 23 wraps to 0), so
+// the conversion and its NaN / range guards drop out.  Values where that
+// does not hold (x <= -104, -inf) are replaced by the 0 clamp as in vm_exp;
+// x >= 104 cannot occur; a NaN stays the same NaN through the fmas and the
+// finite scales.
+__device__ __forceinline__ vm_f32x2 vm_exp2_nonpos(vm_f32x2 x) {
+  const vm_f32x2 INV_LOG2 = {1.44269504088896340736f, 1.44269504088896340736f};
+  const vm_f32x2 MAGIC = {12582912.f, 12582912.f};
+  const vm_f32x2 LN2_HI = {-6.93145752e-1f, -6.93145752e-1f}, LN2_LO = {-1.42860677e-6f, -1.42860677e-6f};
+  const vm_f32x2 jm = __builtin_elementwise_fma(x, INV_LOG2, MAGIC);
+  const vm_f32x2 j = jm - MAGIC;
+  vm_f32x2 r = __builtin_elementwise_fma(j, LN2_HI, x);
+  r = __builtin_elementwise_fma(j, LN2_LO, r);
+  vm_f32x2 t = {1.37805939e-3f, 1.37805939e-3f};
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){8.37312452e-3f, 8.37312452e-3f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){4.16695364e-2f, 4.16695364e-2f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){1.66664720e-1f, 1.66664720e-1f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){4.99999851e-1f, 4.99999851e-1f});
+  t = __builtin_elementwise_fma(t, r, (vm_f32x2){1.0f, 1.0f});
+  r = __builtin_elementwise_fma(t, r, (vm_f32x2){1.0f, 1.0f});
+  vm_f32x2 s2;
+#pragma unroll
+  for (int c = 0; c < 2; c++) s2[c] = __uint_as_float((__float_as_uint(jm[c]) << 23) + 0x7D000000u);
+  r = r * (vm_f32x2){__uint_as_float(0x02000000u), __uint_as_float(0x02000000u)};
+  r = r * s2;
+#pragma unroll
+  for (int c = 0; c < 2; c++)
+    if (x[c] <= -104.f) r[c] = 0.f;
+  return r;
+}
+
 // a / b for many a over one b (softmax's normalisation).  The compiler's f32
 // division is v_div_scale (both operands), v_rcp, two fma refinements of the
 // reciprocal, three fma quotient steps, v_div_fmas and v_div_fixup; with the
@@ -172,7 +207,7 @@ __device__ __forceinline__ vm_f32x2 vm_gelu2(vm_f32x2 x) {
   y = __builtin_elementwise_fma(y, t, (vm_f32x2){-0.284496736f, -0.284496736f});
   y = __builtin_elementwise_fma(y, t, (vm_f32x2){0.254829592f, 0.254829592f});
   const vm_f32x2 at = y * t;
-  const vm_f32x2 e = vm_exp2(zero - az * az);
+  const vm_f32x2 e = vm_exp2_nonpos(zero - az * az);
   const vm_f32x2 r = one - at * e;
   const vm_f32x2 nr = zero - r;
   vm_f32x2 erf;

@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
 O=gpurun_out/att_${1:-now}; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -q -x --timeout 300 --timeout-method thread tests/test_model_gpu.py -k "attention or bert" tests/test_full_size_gpu.py -k "attention or bert" tests/test_vecmath_gpu.py > $O/tests.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest -q -x --timeout 300 --timeout-method thread tests/test_model_gpu.py tests/test_full_size_gpu.py tests/test_vecmath_gpu.py tests/test_ops_gpu.py -k "attention or bert or vm_ or div_by or gelu or Gelu" > $O/tests.log 2>&1; rc=$?
 tail -2 $O/tests.log; grep -E "^FAILED" $O/tests.log | head; [ $rc -eq 0 ] || { echo "tests failed"; exit 1; }
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/p -o run -- python3 rten-fork_amd/tools/attn_bench.py > $O/p.log 2>&1 || { echo "rocprof fail"; tail -5 $O/p.log; exit 1; }
 f=$(find $O/p -name "run_kernel_stats.csv" | head -1)

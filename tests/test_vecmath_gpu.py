@@ -30,10 +30,10 @@ def lib():
 def _run(lib, a, b):
     import torch
     ad, bd = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
-    out = torch.empty(6 * a.size, dtype=torch.float32, device="cuda")
+    out = torch.empty(7 * a.size, dtype=torch.float32, device="cuda")
     assert lib.rtenhip_debug_vecmath_check(ad.data_ptr(), bd.data_ptr(), a.size, out.data_ptr(), None) == 0
     torch.cuda.synchronize()
-    return out.cpu().numpy().reshape(6, a.size)
+    return out.cpu().numpy().reshape(7, a.size)
 
 
 def _bits(x):
@@ -66,6 +66,20 @@ def test_vm_exp2_matches_vm_exp(lib):
     x[:6] = [np.inf, -np.inf, np.nan, 104.0, -104.0, 0.0]
     o = _run(lib, x, np.ones_like(x))
     assert np.array_equal(_bits(o[2]), _bits(o[3]))
+
+
+def test_vm_exp2_nonpos_matches_vm_exp2(lib):
+    """The softmax / GELU exp (x <= 0 or NaN: attention's x - max, GELU's
+    -z^2) equals vm_exp2 bit for bit, the clamp boundary and -inf included."""
+    rng = np.random.default_rng(4)
+    n = 1 << 22
+    x = -np.concatenate([rng.uniform(0, 110, n // 4), rng.uniform(0, 1, n // 4),
+                         rng.exponential(20, n // 4), rng.uniform(103, 105, n // 8),
+                         np.exp2(rng.uniform(-140, 120, n // 8))]).astype(np.float32)
+    x[:8] = [-np.inf, np.nan, -104.0, np.nextafter(np.float32(-104), np.float32(0)), 0.0, -0.0,
+             -1e-45, -3.4e38]
+    o = _run(lib, x, np.ones_like(x))
+    assert np.array_equal(_bits(o[6]), _bits(o[2]))
 
 
 def test_vm_gelu2_matches_vm_gelu(lib):
