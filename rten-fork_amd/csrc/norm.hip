@@ -175,24 +175,37 @@ __device__ __forceinline__ float strided_sum(const float* p, int s, int n) {
   return acc;
 }
 
-// The same fold with n known at compile time: fully unrolled, so the LDS
-// reads are issued ahead under counted waits and the chain waits on adds only
-// (the runtime-n loop drains every read at each trip).
+// The same fold over n contiguous values (n known at compile time), read as
+// 16-byte LDS loads -- a quarter of the LDS instructions of the strided form
+// (the fold's cost is its reads, not its adds).  Reads round n up to a
+// multiple of 4; the values past n are not added.
 template <int N>
-__device__ __forceinline__ float strided_sum_n(const float* p, int s) {
-  float v[N];
+__device__ __forceinline__ float contiguous_sum_n(const float* p) {
+  constexpr int NV = (N + 3) / 4;
+  float4 v[NV];
 #pragma unroll
-  for (int i = 0; i < N; i++) v[i] = p[i * s];
+  for (int i = 0; i < NV; i++) v[i] = reinterpret_cast<const float4*>(p)[i];
   float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < N; i++) acc = __fadd_rn(acc, v[i]);
+  for (int i = 0; i < N; i++) {
+    const float4& q = v[i >> 2];
+    acc = __fadd_rn(acc, (i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w);
+  }
   return acc;
+}
+
+// Row stride (floats) of the LayerNorm rows kernel's partial sums: the
+// groups rounded up to whole float4s, plus one float4 of padding.
+__host__ __device__ inline int ln_part_row_stride(int len) { return ((((len - 1) >> 2) + 3) & ~3) + 4; }
+// LDS bytes of the rows kernel: R staged rows, R rows of partials, mean / inv.
+inline size_t ln_rows_shm(int R, int64_t len) {
+  return ((size_t)R * (len + 4) + (size_t)R * ln_part_row_stride((int)len) + 2 * (size_t)R) * sizeof(float);
 }
 
 // LayerNorm for len % 8 == 0 on 16-byte aligned rows, R rows per workgroup:
 // the rows are staged in LDS with 16-byte copies, the 8-element chunk sums and
 // the 4-element groups of squares are formed in parallel into LDS as
-// [chunk][row], and thread r runs row r's two serial folds -- one VALU
+// [row][chunk], and thread r runs row r's two serial folds -- one VALU
 // instruction advances R rows' chains, where layer_norm_kernel spends a whole
 // wave instruction per add of one row.  Same operations in the same order.
 // LEN > 0: instance for that row length (folds fully unrolled); 0: any.
@@ -215,14 +228,14 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
   const int q = len >> 2;              // float4s per row
   const int nchunks = len >> 3;
   const int ngroups = (len - 1) >> 2;  // >= nchunks for len >= 8
-  const int ps = R + 1;                // [chunk][row] stride
+  const int ps = ln_part_row_stride(len);  // [row][chunk] stride
   float* xs = reinterpret_cast<float*>(lds4);
   // Rows are q + 1 float4s apart in LDS (one float4 of padding): the
   // packed-A phase reads the same column of 8 consecutive rows, which at a
   // stride of len (a multiple of 32 dwords) would share one bank.
   const int qs = q + 1;
   float* part = xs + R * (len + 4);
-  float* stat = part + ngroups * ps;   // mean[R], inv[R]
+  float* stat = part + R * ps;         // mean[R], inv[R]
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = (int64_t)blockIdx.x * R;
   const int64_t left = rows - row0;
@@ -270,18 +283,18 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
       const float4 a = lds4[r * qs + 2 * c], b = lds4[r * qs + 2 * c + 1];
       const float z0 = __fadd_rn(a.x, b.x), z1 = __fadd_rn(a.y, b.y);
       const float z2 = __fadd_rn(a.z, b.z), z3 = __fadd_rn(a.w, b.w);
-      part[c * ps + r] = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
+      part[r * ps + c] = __fadd_rn(__fadd_rn(__fadd_rn(z0, z1), z2), z3);
     }
   __syncthreads();
   if ((int)threadIdx.x < nr) {
     const int r = threadIdx.x;
     float total;
     if constexpr (RTENHIP_LN_EXPERIMENT == 2)
-      total = part[r];
+      total = part[r * ps];
     else if constexpr (LEN > 0)
-      total = strided_sum_n<LEN / 8>(part + r, ps);
+      total = contiguous_sum_n<LEN / 8>(part + r * ps);
     else
-      total = strided_sum(part + r, ps, nchunks);
+      total = strided_sum(part + r * ps, 1, nchunks);
     stat[r] = __fdiv_rn(total, (float)len);
   }
   __syncthreads();
@@ -294,7 +307,7 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
       const float d2 = __fsub_rn(v.z, mean), d3 = __fsub_rn(v.w, mean);
       const float ab = __fadd_rn(__fmul_rn(d0, d0), __fmul_rn(d1, d1));
       const float cd = __fadd_rn(__fmul_rn(d2, d2), __fmul_rn(d3, d3));
-      part[g * ps + r] = __fadd_rn(ab, cd);
+      part[r * ps + g] = __fadd_rn(ab, cd);
     }
   }
   __syncthreads();
@@ -303,11 +316,11 @@ __global__ __launch_bounds__(256) void layer_norm_rows_kernel(
     const float mean = stat[r];
     float sum;
     if constexpr (RTENHIP_LN_EXPERIMENT == 2)
-      sum = part[r];
+      sum = part[r * ps];
     else if constexpr (LEN > 0)
-      sum = strided_sum_n<(LEN - 1) / 4>(part + r, ps);
+      sum = contiguous_sum_n<(LEN - 1) / 4>(part + r * ps);
     else
-      sum = strided_sum(part + r, ps, ngroups);
+      sum = strided_sum(part + r * ps, 1, ngroups);
     for (int i = 4 * ngroups; i < len; i++) {
       const float d = __fsub_rn(xs[r * (len + 4) + i], mean);
       sum = __fadd_rn(sum, __fmul_rn(d, d));
@@ -380,8 +393,7 @@ bool layer_norm_rows_ok(const float* x, float* y, int64_t len, const float* scal
       (bias && (uintptr_t)bias % 16))
     return false;
   const int R = (int)std::max<int64_t>(1, std::min<int64_t>(16, RTENHIP_LN_ROWS_NUM / len));
-  const int64_t ngroups = (len - 1) / 4;
-  return ((size_t)R * (len + 4) + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float) <= 64 * 1024;
+  return ln_rows_shm(R, len) <= 64 * 1024;
 }
 
 rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t len,
@@ -400,8 +412,7 @@ rtenhip_status launch_layer_norm(const float* x, float* y, int64_t rows, int64_t
     }();
     const int R = env_rows > 0 ? std::min(env_rows, 64)
                                : (int)std::max<int64_t>(1, std::min<int64_t>(16, RTENHIP_LN_ROWS_NUM / len));
-    const int64_t ngroups = (len - 1) / 4;
-    const size_t rshm = ((size_t)R * (len + 4) + (size_t)ngroups * (R + 1) + 2 * (size_t)R) * sizeof(float);
+    const size_t rshm = ln_rows_shm(R, len);
     if (rshm <= 64 * 1024) {
       const int64_t rblocks = (rows + R - 1) / R;
       // BERT-base / BERT-large widths get the unrolled-fold instances.
