@@ -235,5 +235,8 @@ bool broadcast_shapes(const int64_t* a, int an, const int64_t* b, int bn, int64_
 // set *flag (device int) instead of synchronizing.
 rtenhip_status launch_gather(const rtenhip_tensor* x, const rtenhip_tensor_i32* indices, int64_t axis,
                              rtenhip_tensor* y, int* flag, hipStream_t s);
+// Moves the run's Gather flag to ring[seq % nslots] (host-mapped), clears it
+// and advances seq (indexing.hip).
+rtenhip_status launch_gather_check_finish(int* flag, unsigned* seq, int* ring, int nslots, hipStream_t s);
 
 }  // namespace rtenhip

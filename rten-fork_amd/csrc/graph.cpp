@@ -74,8 +74,9 @@ Plan::~Plan() {
       (void)hipEventSynchronize(c.ev);
       (void)hipEventDestroy(c.ev);
     }
-    if (c.host) (void)hipHostFree(c.host);
   }
+  if (gring_host) (void)hipHostFree(gring_host);
+  if (gseq_dev) (void)hipFree(gseq_dev);
   for (auto& kv : host_dev)
     if (kv.second) (void)hipFree(kv.second);
   for (auto& kv : convs) {
@@ -752,6 +753,13 @@ rtenhip_status Graph::make_plan(const std::vector<int>& in_ids, const std::vecto
     if (ty == "Gather" && !p.gather_flag) {
       RTENHIP_HIP_CHECK(hipMalloc(&p.gather_flag, sizeof(int)));
       RTENHIP_HIP_CHECK(hipMemset(p.gather_flag, 0, sizeof(int)));
+      RTENHIP_HIP_CHECK(hipMalloc(&p.gseq_dev, sizeof(unsigned)));
+      RTENHIP_HIP_CHECK(hipMemset(p.gseq_dev, 0, sizeof(unsigned)));
+      RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.gring_host), Plan::kGatherChecks * sizeof(int),
+                                      hipHostMallocMapped | hipHostMallocCoherent));
+      for (int i = 0; i < Plan::kGatherChecks; i++) p.gring_host[i] = 0;
+      RTENHIP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&p.gring_dev), p.gring_host, 0));
+      p.gseq = 0;
     }
   }
   planning_host = nullptr;
@@ -3284,6 +3292,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     }
     return RTENHIP_OK;
   };
+  bool finish_in_graph = false;  // the replay launched the Gather check's finish
   plan->mm_pack_value = -1;  // packed-A reuse never crosses runs
   plan->pk_ready.clear();
   if (replay) {
@@ -3308,6 +3317,9 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
         for (int op : plan->ops)
           if ((st = run_op(op))) break;
         if (!st) st = copy_static_outputs();
+        if (!st && plan->gather_flag)
+          st = launch_gather_check_finish(plan->gather_flag, plan->gseq_dev, plan->gring_dev, Plan::kGatherChecks,
+                                          exec_stream);
         ctx->stream = exec_stream;
         hipError_t e2 = hipStreamEndCapture(exec_stream, &g);
         if (!st && e2 == hipSuccess) e2 = hipGraphInstantiate(&cap->exec, g, nullptr, nullptr, 0);
@@ -3323,6 +3335,7 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
       cap->last_use = this_run;
       hipError_t e = hipGraphLaunch(cap->exec, exec_stream);
       if (e != hipSuccess) st = hip_fail(e, "hipGraphLaunch");
+      else finish_in_graph = plan->gather_flag != nullptr;  // every capture of the plan ends with it
     }
   } else {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evs;
@@ -3520,23 +3533,29 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     // Gather's index check (gather.rs:52-60): the flag the kernels set on an
     // out-of-range index goes to a pinned word of a check slot and is cleared
     // whatever the run's status; an event marks the copy.
-    Plan::GatherCheck& c = plan->gchk[plan->gchk_next];
+    const int slot = (int)(plan->gseq % Plan::kGatherChecks);
+    Plan::GatherCheck& c = plan->gchk[slot];
     if (c.pending) {
       // (deferred mode) The ring is full: the slot's run must have finished
       // before reuse; its error is kept for synchronize(), not given to this run.
       rtenhip_status cs = collect_gather_checks(*plan, true);
       if (!st) st = cs;  // a HIP error only
     }
-    if (!c.host) {
-      RTENHIP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&c.host), sizeof(int), hipHostMallocDefault));
-      RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
+    if (!c.ev) RTENHIP_HIP_CHECK(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
+    c.host = plan->gring_host + slot;
+    // A replay ran the finish as its last node; an eager run (or a replay
+    // that failed to launch) queues it now, whatever the run's status.
+    rtenhip_status fs = RTENHIP_OK;
+    if (!finish_in_graph)
+      fs = launch_gather_check_finish(plan->gather_flag, plan->gseq_dev, plan->gring_dev, Plan::kGatherChecks,
+                                      exec_stream);
+    if (!fs) {
+      plan->gseq++;
+      plan->gchk_next = (int)(plan->gseq % Plan::kGatherChecks);  // the oldest slot (collect order)
     }
-    *c.host = 0;
-    const hipError_t e0 = hipMemcpyAsync(c.host, plan->gather_flag, sizeof(int), hipMemcpyDeviceToHost, exec_stream);
-    const hipError_t e1 = hipMemsetAsync(plan->gather_flag, 0, sizeof(int), exec_stream);
-    const hipError_t e2 = hipEventRecord(c.ev, exec_stream);
-    if (e0 != hipSuccess || e1 != hipSuccess || e2 != hipSuccess) {
-      if (!st) st = hip_fail(e0 != hipSuccess ? e0 : e1 != hipSuccess ? e1 : e2, "gather flag");
+    const hipError_t e2 = fs ? hipSuccess : hipEventRecord(c.ev, exec_stream);
+    if (fs || e2 != hipSuccess) {
+      if (!st) st = fs ? fs : hip_fail(e2, "gather flag");
     } else if (!deferred_checks) {
       // The reference's behaviour: this run returns its own index error.
       if (hipEventSynchronize(c.ev) != hipSuccess) {
@@ -3547,7 +3566,6 @@ rtenhip_status Graph::run(const int32_t* in_ids, const rtenhip_tensor* ins, int 
     } else {
       c.pending = true;
       c.run = this_run;
-      plan->gchk_next = (plan->gchk_next + 1) % Plan::kGatherChecks;
     }
   }
   if (ext_order) {

@@ -304,10 +304,19 @@ struct Plan {
   // several runs can be queued; each slot carries its run's sequence number
   // and its error is reported only by Graph::synchronize
   // (rtenhip_graph_synchronize), never by a later, unrelated run.
+  // (Round 6: the flag's move and clear are one launch at the end of the run,
+  // inside the captured graph -- launch_gather_check_finish -- into the
+  // check ring gring, a fine-grained host-mapped array of kGatherChecks
+  // words; the run's slot is gseq % kGatherChecks, gseq counting the finish
+  // launches on the host as gseq_dev does on the device.)
   int* gather_flag = nullptr;
   static constexpr int kGatherChecks = 4;
+  int* gring_host = nullptr;
+  int* gring_dev = nullptr;
+  unsigned* gseq_dev = nullptr;
+  uint64_t gseq = 0;
   struct GatherCheck {
-    int* host = nullptr;       // pinned
+    int* host = nullptr;       // the slot's word of gring_host
     hipEvent_t ev = nullptr;
     bool pending = false;
     uint64_t run = 0;          // Graph::run_seq of the run that queued it

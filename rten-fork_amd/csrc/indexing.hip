@@ -206,6 +206,27 @@ rtenhip_status launch_gather(const rtenhip_tensor* x, const rtenhip_tensor_i32* 
   return RTENHIP_OK;
 }
 
+// The end of a run's Gather check (graph executor): the run's flag goes to
+// word seq % nslots of a fine-grained (host-mapped) ring, the flag is
+// cleared and seq advances -- one launch that a hipGraph capture holds, where
+// a device-to-host copy and a fill after the replay each cost a dispatch and
+// an inter-launch gap.
+__global__ void gather_check_finish_kernel(int* flag, unsigned* seq, int* ring, int nslots) {
+  if (threadIdx.x != 0) return;
+  const unsigned q = *seq;
+  ring[q % (unsigned)nslots] = *flag;
+  __threadfence_system();
+  *flag = 0;
+  *seq = q + 1;
+}
+
+rtenhip_status launch_gather_check_finish(int* flag, unsigned* seq, int* ring, int nslots, hipStream_t s) {
+  if (!flag || !seq || !ring || nslots <= 0) return fail(RTENHIP_INVALID_VALUE, "gather check ring");
+  hipLaunchKernelGGL(gather_check_finish_kernel, dim3(1), dim3(64), 0, s, flag, seq, ring, nslots);
+  RTENHIP_LAUNCH_CHECK();
+  return RTENHIP_OK;
+}
+
 }  // namespace rtenhip
 
 using namespace rtenhip;
