@@ -394,7 +394,8 @@ def test_softmax_bitexact(rh, oracle, shape, axis):
 
 
 @pytest.mark.parametrize("shape", [(4, 128, 768), (5, 2), (3, 7, 13), (3, 13, 1024), (7, 64),
-                                   (2, 5, 4096), (3, 12), (2, 3, 8), (1, 3, 8192)])
+                                   (2, 5, 4096), (3, 12), (2, 3, 8), (1, 3, 8192), (9, 24), (5, 40),
+                                   (17, 520), (33, 16)])
 def test_layer_norm_bitexact(rh, oracle, shape):
     x = rnd(oracle, 92, *shape, scale=4.0)
     sc = rnd(oracle, 93, shape[-1]) + np.float32(1.0)
